@@ -1,0 +1,178 @@
+/*
+ * lodestar_bls.h -- C ABI of the MI355X-native BLS12-381 signature-set verifier.
+ *
+ * This is the drop-in boundary for Lodestar's BLS hot path
+ * (packages/beacon-node/src/chain/bls).  Every entry point takes plain
+ * pointers and sizes; no torch or HIP types cross the boundary.  The N-API
+ * stub a maintainer would add on the Lodestar side is in INTEGRATION.md.
+ *
+ * Reference interfaces replaced (paths relative to packages/beacon-node/src/):
+ *   lb_verify_requests      <- worker verifyManySignatureSets(BlsWorkReq[]) -> BlsWorkResult
+ *                              chain/bls/multithread/worker.ts:30-108, types.ts:8-39,
+ *                              with verifySignatureSetsMaybeBatch semantics (chain/bls/maybeBatch.ts:16-46)
+ *                              and main-thread pubkey aggregation fused in
+ *                              (chain/bls/utils.ts:6-21, chain/bls/multithread/jobItem.ts:55-63)
+ *   lb_verify_same_message  <- BlsMultiThreadWorkerPool.verifySignatureSetsSameMessage job path:
+ *                              jobItemWorkReq sameMessage (jobItem.ts:64-86) + retry
+ *                              (index.ts:473-484,557-568, jobItem.ts:93-125); also
+ *                              BlsSingleThreadVerifier.verifySignatureSetsSameMessage (singleThread.ts:37-81)
+ *   lb_aggregate_pubkeys    <- bls.PublicKey.aggregate(pks).toBytes(uncompressed)
+ *                              (chain/bls/utils.ts:13, jobItem.ts:59,80)
+ *   lb_aggregate_signatures <- Signature.fromBytes(validate) x n + bls.Signature.aggregate(sigs).toBytes()
+ *                              (jobItem.ts:73,81)
+ *   lb_create / lb_destroy  <- BlsMultiThreadWorkerPool constructor / close() (index.ts:132-153,244-265)
+ *
+ * Threading: a context is bound to one GPU and is not thread-safe; use one
+ * context per host submission thread (one process per GPU for multi-GPU).
+ */
+#ifndef LODESTAR_BLS_H
+#define LODESTAR_BLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (return values) ------------------------------------- */
+#define LB_OK 0
+#define LB_ERR_INVALID_ARGUMENT (-1) /* API misuse: NULL pointer, bad offsets  */
+#define LB_ERR_DEVICE (-2)           /* HIP runtime failure (maps to Promise rejection, index.ts:503-512) */
+#define LB_ERR_NO_DEVICE (-3)        /* no GPU / bad ordinal                      */
+#define LB_ERR_OUT_OF_MEMORY (-4)
+
+/* ---- per-request error codes (lb_verify_requests out_request_error) ----- */
+#define LB_REQ_OK 0
+#define LB_REQ_EMPTY_AGGREGATE 1 /* aggregate set with zero pubkeys: the reference REJECTS
+                                    the job (EMPTY_AGGREGATE_ARRAY thrown in jobItemWorkReq,
+                                    index.ts:403-409) instead of returning false */
+#define LB_REQ_BAD_PUBKEY 2      /* pubkey bytes that PublicKey.fromBytes would throw on
+                                    (worker.ts:110-116 -> the worker call rejects) */
+
+/* ---- per-set decode status (optional outputs) -------------------------- */
+#define LB_SET_OK 0
+#define LB_SET_BAD_ENCODING 1
+#define LB_SET_NOT_ON_CURVE 2
+#define LB_SET_NOT_IN_GROUP 3
+#define LB_SET_PK_INFINITY 4
+#define LB_SET_EMPTY_AGGREGATE 5
+
+/* Sizes */
+#define LB_PUBKEY_BYTES 96      /* uncompressed affine G1 (PointFormat.uncompressed, index.ts:144) */
+#define LB_PUBKEY_COMPRESSED 48
+#define LB_SIG_COMPRESSED 96
+#define LB_SIG_UNCOMPRESSED 192
+#define LB_MESSAGE_BYTES 32
+#define LB_SEED_BYTES 32
+#define LB_GT_BYTES 576
+
+typedef struct lb_ctx lb_ctx;
+
+/* Create a context on HIP device `device` (one per process per GPU). */
+int lb_create(int device, lb_ctx** out_ctx);
+/* Release device memory and streams.  Safe on NULL. */
+int lb_destroy(lb_ctx* ctx);
+/* Human-readable message for the last error on this context (never NULL). */
+const char* lb_last_error(const lb_ctx* ctx);
+/* Number of visible HIP devices (0 when none). */
+int lb_device_count(void);
+
+/*
+ * A batch of verification requests.  A request is one BlsWorkReq (one
+ * verifySignatureSets job of <= 128 sets); it gets ONE verdict = the AND over
+ * its sets, exactly as verifySignatureSetsMaybeBatch returns it:
+ *   - 0 sets                 -> false ("Empty signature set" caught)
+ *   - any signature that fails Signature.fromBytes(validate=true) -> false
+ *   - infinite (aggregated) pubkey -> false
+ *   - 1 set: core verify (pubkey G1 check, infinite signature -> false)
+ *   - >= 2 sets: random-scalar batch verification with 64-bit scalars drawn
+ *     from the deterministic DRBG  r_i = LE64(SHA-256(seed || LE32(i))[0..8]),
+ *     i = the set's index in this call, 0 -> 1.
+ * Set i's pubkeys are pubkeys[pk_offsets[i] .. pk_offsets[i+1]) (96-byte
+ * uncompressed each); more than one -> aggregated on the GPU (the reference
+ * aggregates on the main thread before dispatch).
+ */
+typedef struct {
+  uint32_t n_requests;
+  uint32_t n_sets;
+  const uint32_t* request_offsets; /* n_requests + 1, sets of request k: [off[k], off[k+1]) */
+  const uint8_t* request_batchable; /* n_requests, opts.batchable (may be NULL)              */
+  const uint8_t* pubkeys;          /* pk_offsets[n_sets] x 96 bytes                          */
+  const uint32_t* pk_offsets;      /* n_sets + 1 (NULL => exactly one pubkey per set)        */
+  const uint8_t* messages;         /* n_sets x 32 bytes (signing roots)                      */
+  const uint8_t* signatures;       /* concatenated signature bytes                           */
+  const uint32_t* sig_offsets;     /* n_sets + 1 byte offsets into signatures                */
+  const uint8_t* seed;             /* 32 bytes of batch randomness seed                      */
+} lb_request_batch;
+
+typedef struct {
+  uint32_t batch_retries;      /* merged batchable groups that had to be retried (worker.ts:80) */
+  uint32_t batch_sigs_success; /* sets verified successfully inside merged groups (worker.ts:71) */
+  double device_ms;            /* wall time of the device pipeline for this call              */
+} lb_verify_stats;
+
+/*
+ * Host-buffer entry point: stages inputs through pinned memory onto the
+ * device, runs the pipeline, copies verdicts back.  out_request_valid[k] is
+ * 1/0; out_request_error[k] is LB_REQ_*; out_set_status (optional, n_sets) is
+ * LB_SET_*; stats optional.  Returns LB_OK or a negative LB_ERR_*.
+ */
+int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* out_request_valid,
+                       uint8_t* out_request_error, uint8_t* out_set_status, lb_verify_stats* stats);
+
+/*
+ * Device-resident variant: every pointer in `batch` and every output pointer
+ * is device memory already resident in HBM (used by bench.py to time the
+ * kernels without PCIe).  Runs on the context's stream and synchronises it
+ * before returning.
+ */
+int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* d_out_request_valid,
+                              uint8_t* d_out_request_error, uint8_t* d_out_set_status, lb_verify_stats* stats);
+
+/*
+ * verifySignatureSetsSameMessage for one job (<= 128 sets in the reference,
+ * any n here): out_valid[i] per set.  Fast path: every signature validates,
+ * aggregate pubkeys and signatures (plain sums, as the reference does) and
+ * core-verify once; otherwise / on failure every set is core-verified alone.
+ * n == 0 -> nothing written (the reference returns []).
+ */
+int lb_verify_same_message(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys /* n x 96 */,
+                           const uint8_t* signatures, const uint32_t* sig_offsets /* n + 1 */,
+                           const uint8_t* message /* 32 */, const uint8_t* seed /* 32 */, uint8_t* out_valid,
+                           uint32_t* out_used_fast_path);
+
+/* Sum of n uncompressed pubkeys -> 96-byte uncompressed encoding.  n == 0 ->
+ * LB_ERR_INVALID_ARGUMENT (EMPTY_AGGREGATE_ARRAY). *out_status = LB_SET_*. */
+int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys, uint8_t* out96, uint8_t* out_status);
+
+/* Validate-deserialize n signatures and sum them -> 192-byte uncompressed
+ * encoding.  *out_bad_index = index of the first invalid signature or -1. */
+int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* signatures, const uint32_t* sig_offsets,
+                            uint8_t* out192, int32_t* out_bad_index);
+
+/* ---- stage-level entry points (parity tests against the CPU oracle) ----- */
+/* hash_to_G2(msg_i) -> 192-byte uncompressed affine encoding each */
+int lb_hash_to_g2(lb_ctx* ctx, uint32_t n, const uint8_t* messages, uint8_t* out192);
+/* Signature.fromBytes(validate=true): status + 192-byte uncompressed re-encoding */
+int lb_decode_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* signatures, const uint32_t* sig_offsets,
+                         uint8_t* out_status, uint8_t* out192);
+/* e(P_i, Q_i) after the final exponentiation (f^(3(p^12-1)/r)), 576 bytes each
+ * (12 big-endian Fp coefficients, c0.c0.c0 ... c1.c2.c1 order) */
+int lb_pairing(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint8_t* g2_192, uint8_t* out576);
+/* batch scalars r_i, i in [first, first + n) */
+int lb_batch_scalars(lb_ctx* ctx, const uint8_t* seed, uint32_t first, uint32_t n, uint64_t* out);
+/* [k_i] P_i on G1 and G2 (uncompressed in/out) */
+int lb_g1_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint64_t* k, uint8_t* out96);
+int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* k, uint8_t* out192);
+
+/* ---- profiling ----------------------------------------------------------- */
+/* Per-stage device time (ms) of the last lb_verify_* call, measured with HIP
+ * events on the context's stream.  Writes up to max_stages values and their
+ * names; returns the number of stages. */
+int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names, int max_stages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LODESTAR_BLS_H */

@@ -1,0 +1,492 @@
+// G1 (over Fp) and G2 (over Fp2) group law, endomorphisms, subgroup checks and
+// ZCash point (de)serialisation for gfx950.  One lane per point.
+//
+// Reference semantics restated here (blst via @chainsafe/bls, not vendored):
+//  * PublicKey.fromBytes / toBytes(uncompressed)  -- multithread/worker.ts:110-116,
+//    multithread/jobItem.ts:59,80 (96-byte uncompressed affine G1, 0x40 = infinity)
+//  * Signature.fromBytes(bytes, affine, validate=true) -- maybeBatch.ts:24,37,
+//    jobItem.ts:73: 96-byte compressed or 192-byte uncompressed G2, then the
+//    G2 subgroup check (psi(P) == [x]P, equivalent to [r]P == O on BLS12-381).
+//  * PublicKey.aggregate / Signature.aggregate -- chain/bls/utils.ts:13,
+//    jobItem.ts:80-81 (Jacobian sums).
+#pragma once
+#include "bls_field.h"
+
+namespace lb {
+
+// ---- overloads so the group law is written once for both fields ------------
+LB_DEV void fadd(fp& r, const fp& a, const fp& b) { fp_add(r, a, b); }
+LB_DEV void fadd(fp2& r, const fp2& a, const fp2& b) { fp2_add(r, a, b); }
+LB_DEV void fsub(fp& r, const fp& a, const fp& b) { fp_sub(r, a, b); }
+LB_DEV void fsub(fp2& r, const fp2& a, const fp2& b) { fp2_sub(r, a, b); }
+LB_DEV void fdbl(fp& r, const fp& a) { fp_dbl(r, a); }
+LB_DEV void fdbl(fp2& r, const fp2& a) { fp2_dbl(r, a); }
+LB_DEV void fneg(fp& r, const fp& a) { fp_neg(r, a); }
+LB_DEV void fneg(fp2& r, const fp2& a) { fp2_neg(r, a); }
+LB_DEV void fmul(fp& r, const fp& a, const fp& b) { fp_mul(r, a, b); }
+LB_DEV void fmul(fp2& r, const fp2& a, const fp2& b) { fp2_mul(r, a, b); }
+LB_DEV void fsqr(fp& r, const fp& a) { fp_sqr(r, a); }
+LB_DEV void fsqr(fp2& r, const fp2& a) { fp2_sqr(r, a); }
+LB_DEV void finv(fp& r, const fp& a) { fp_inv(r, a); }
+LB_DEV void finv(fp2& r, const fp2& a) { fp2_inv(r, a); }
+LB_DEV bool fis_zero(const fp& a) { return fp_is_zero(a); }
+LB_DEV bool fis_zero(const fp2& a) { return fp2_is_zero(a); }
+LB_DEV bool feq(const fp& a, const fp& b) { return fp_eq(a, b); }
+LB_DEV bool feq(const fp2& a, const fp2& b) { return fp2_eq(a, b); }
+LB_DEV void fzero(fp& r) { fp_zero(r); }
+LB_DEV void fzero(fp2& r) { fp2_zero(r); }
+LB_DEV void fone(fp& r) { fp_one(r); }
+LB_DEV void fone(fp2& r) { fp2_one(r); }
+
+template <class F>
+struct jac {
+  F X, Y, Z;  // x = X/Z^2, y = Y/Z^3; Z == 0 <=> infinity
+};
+template <class F>
+struct aff {
+  F x, y;
+  bool inf;
+};
+typedef jac<fp> g1j;
+typedef jac<fp2> g2j;
+typedef aff<fp> g1a;
+typedef aff<fp2> g2a;
+
+template <class F>
+LB_DEV void jac_set_inf(jac<F>& r) {
+  fone(r.X);
+  fone(r.Y);
+  fzero(r.Z);
+}
+template <class F>
+LB_DEV bool jac_is_inf(const jac<F>& p) {
+  return fis_zero(p.Z);
+}
+template <class F>
+LB_DEV void jac_from_aff(jac<F>& r, const aff<F>& a) {
+  if (a.inf) {
+    jac_set_inf(r);
+  } else {
+    r.X = a.x;
+    r.Y = a.y;
+    fone(r.Z);
+  }
+}
+template <class F>
+LB_DEV void jac_neg(jac<F>& r, const jac<F>& p) {
+  r.X = p.X;
+  fneg(r.Y, p.Y);
+  r.Z = p.Z;
+}
+
+// dbl-2009-l (a = 0): 2M + 5S.  Z3 = 2YZ, so 2-torsion and infinity map to Z3 = 0.
+template <class F>
+LB_DEV void jac_dbl(jac<F>& r, const jac<F>& p) {
+  F A, B, C, D, E, Fq, t;
+  fsqr(A, p.X);
+  fsqr(B, p.Y);
+  fsqr(C, B);
+  fadd(t, p.X, B);
+  fsqr(t, t);
+  fsub(t, t, A);
+  fsub(t, t, C);
+  fdbl(D, t);
+  fdbl(E, A);
+  fadd(E, E, A);
+  fsqr(Fq, E);
+  F Z3;
+  fmul(Z3, p.Y, p.Z);
+  fdbl(Z3, Z3);
+  F X3;
+  fdbl(t, D);
+  fsub(X3, Fq, t);
+  F Y3;
+  fsub(t, D, X3);
+  fmul(Y3, E, t);
+  fdbl(C, C);
+  fdbl(C, C);
+  fdbl(C, C);
+  fsub(Y3, Y3, C);
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+}
+
+// add-2007-bl with the exceptional cases resolved (P == Q -> dbl, P == -Q -> O)
+template <class F>
+LB_DEV void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+  if (jac_is_inf(p)) {
+    r = q;
+    return;
+  }
+  if (jac_is_inf(q)) {
+    r = p;
+    return;
+  }
+  F Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, Rr, V, t;
+  fsqr(Z1Z1, p.Z);
+  fsqr(Z2Z2, q.Z);
+  fmul(U1, p.X, Z2Z2);
+  fmul(U2, q.X, Z1Z1);
+  fmul(S1, p.Y, q.Z);
+  fmul(S1, S1, Z2Z2);
+  fmul(S2, q.Y, p.Z);
+  fmul(S2, S2, Z1Z1);
+  fsub(H, U2, U1);
+  fsub(Rr, S2, S1);
+  if (fis_zero(H)) {
+    if (fis_zero(Rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fdbl(I, H);
+  fsqr(I, I);
+  fmul(J, H, I);
+  fdbl(Rr, Rr);
+  fmul(V, U1, I);
+  jac<F> o;
+  fsqr(o.X, Rr);
+  fsub(o.X, o.X, J);
+  fdbl(t, V);
+  fsub(o.X, o.X, t);
+  fsub(t, V, o.X);
+  fmul(o.Y, Rr, t);
+  fmul(t, S1, J);
+  fdbl(t, t);
+  fsub(o.Y, o.Y, t);
+  fadd(t, p.Z, q.Z);
+  fsqr(t, t);
+  fsub(t, t, Z1Z1);
+  fsub(t, t, Z2Z2);
+  fmul(o.Z, t, H);
+  r = o;
+}
+
+// madd-2007-bl: p Jacobian + q affine
+template <class F>
+LB_DEV void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+  if (q.inf) {
+    r = p;
+    return;
+  }
+  if (jac_is_inf(p)) {
+    jac_from_aff(r, q);
+    return;
+  }
+  F Z1Z1, U2, S2, H, HH, I, J, Rr, V, t;
+  fsqr(Z1Z1, p.Z);
+  fmul(U2, q.x, Z1Z1);
+  fmul(S2, q.y, p.Z);
+  fmul(S2, S2, Z1Z1);
+  fsub(H, U2, p.X);
+  fsub(Rr, S2, p.Y);
+  if (fis_zero(H)) {
+    if (fis_zero(Rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fsqr(HH, H);
+  fdbl(I, HH);
+  fdbl(I, I);
+  fmul(J, H, I);
+  fdbl(Rr, Rr);
+  fmul(V, p.X, I);
+  jac<F> o;
+  fsqr(o.X, Rr);
+  fsub(o.X, o.X, J);
+  fdbl(t, V);
+  fsub(o.X, o.X, t);
+  fsub(t, V, o.X);
+  fmul(o.Y, Rr, t);
+  fmul(t, p.Y, J);
+  fdbl(t, t);
+  fsub(o.Y, o.Y, t);
+  fadd(t, p.Z, H);
+  fsqr(t, t);
+  fsub(t, t, Z1Z1);
+  fsub(o.Z, t, HH);
+  r = o;
+}
+
+template <class F>
+LB_DEV void jac_to_aff(aff<F>& r, const jac<F>& p) {
+  if (jac_is_inf(p)) {
+    fzero(r.x);
+    fzero(r.y);
+    r.inf = true;
+    return;
+  }
+  F zi, zi2, zi3;
+  finv(zi, p.Z);
+  fsqr(zi2, zi);
+  fmul(zi3, zi2, zi);
+  fmul(r.x, p.X, zi2);
+  fmul(r.y, p.Y, zi3);
+  r.inf = false;
+}
+
+template <class F>
+LB_DEV bool jac_eq(const jac<F>& p, const jac<F>& q) {
+  const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F z1z1, z2z2, a, b;
+  fsqr(z1z1, p.Z);
+  fsqr(z2z2, q.Z);
+  fmul(a, p.X, z2z2);
+  fmul(b, q.X, z1z1);
+  if (!feq(a, b)) return false;
+  fmul(z1z1, z1z1, p.Z);
+  fmul(z2z2, z2z2, q.Z);
+  fmul(a, p.Y, z2z2);
+  fmul(b, q.Y, z1z1);
+  return feq(a, b);
+}
+
+// [k]P, k a 64-bit scalar (batch-verification randomness), left to right.
+template <class F>
+LB_DEV void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (int i = 63; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((k >> i) & 1ull) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+
+// [|x|]P for the BLS parameter |x| = 0xd201000000010000 (fixed bit pattern:
+// 63 doublings, 5 additions; the branch is wave-uniform).
+template <class F>
+LB_DEV void jac_mul_xabs(jac<F>& r, const jac<F>& p) {
+  jac<F> acc = p;
+  for (int i = 62; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((LB_X_ABS >> i) & 1ull) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+
+// ---- curve equations --------------------------------------------------------
+LB_DEV bool g1_aff_on_curve(const g1a& a) {
+  if (a.inf) return true;
+  fp l, rr, b;
+  fp_sqr(l, a.y);
+  fp_sqr(rr, a.x);
+  fp_mul(rr, rr, a.x);
+  fp_set(b, LB_B1);
+  fp_add(rr, rr, b);
+  return fp_eq(l, rr);
+}
+LB_DEV bool g2_aff_on_curve(const g2a& a) {
+  if (a.inf) return true;
+  fp2 l, rr, b;
+  fp2_sqr(l, a.y);
+  fp2_sqr(rr, a.x);
+  fp2_mul(rr, rr, a.x);
+  fp2_set(b, LB_B2);
+  fp2_add(rr, rr, b);
+  return fp2_eq(l, rr);
+}
+
+// psi(x, y) = (conj(x) cx, conj(y) cy) on Jacobian coordinates
+LB_DEV void g2_psi(g2j& r, const g2j& p) {
+  fp2 t;
+  fp2_conj(t, p.X);
+  fp2_mul_const(r.X, t, LB_PSI_CX);
+  fp2_conj(t, p.Y);
+  fp2_mul_const(r.Y, t, LB_PSI_CY);
+  fp2_conj(r.Z, p.Z);
+}
+
+// G2 membership: psi(P) == [x]P = -[|x|]P  (Scott 2021; blst POINTonE2_in_G2).
+LB_DEV bool g2_in_subgroup(const g2j& p) {
+  if (jac_is_inf(p)) return true;
+  g2j xp, ps;
+  jac_mul_xabs(xp, p);
+  jac_neg(xp, xp);
+  g2_psi(ps, p);
+  return jac_eq(ps, xp);
+}
+
+// G1 membership: phi(P) == [-x^2]P with phi(x, y) = (beta x, y).
+LB_DEV bool g1_in_subgroup(const g1j& p) {
+  if (jac_is_inf(p)) return true;
+  g1j t;
+  jac_mul_xabs(t, p);
+  jac_mul_xabs(t, t);  // [x^2]P
+  jac_neg(t, t);
+  g1j ph = p;
+  fp_mul_const(ph.X, p.X, LB_G1_BETA);
+  return jac_eq(ph, t);
+}
+
+// ---- ZCash serialisation ---------------------------------------------------
+enum : uint8_t {
+  LB_ST_OK = 0,
+  LB_ST_BAD_ENCODING = 1,
+  LB_ST_NOT_ON_CURVE = 2,
+  LB_ST_NOT_IN_GROUP = 3,
+  LB_ST_PK_INFINITY = 4,
+  LB_ST_EMPTY_AGGREGATE = 5,
+};
+
+LB_DEV bool bytes_zero(const uint8_t* b, int n) {
+  uint32_t acc = 0;
+  for (int i = 0; i < n; i++) acc |= b[i];
+  return acc == 0;
+}
+
+// 48 big-endian bytes (with the 3 flag bits masked) -> Montgomery fp; false if >= p
+LB_DEV bool fp_read_masked(fp& r, const uint8_t* b, bool mask_flags) {
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; i++) tmp[i] = b[i];
+  if (mask_flags) tmp[0] &= 0x1f;
+  fp raw;
+  if (!fp_from_be48_raw(raw, tmp)) return false;
+  fp_to_mont(r, raw);
+  return true;
+}
+
+// POINTonE1_Deserialize_Z + the binding's length rule (48 iff compressed).
+LB_DEV uint8_t g1_deserialize(g1a& out, const uint8_t* b, uint32_t len) {
+  out.inf = false;
+  if (len == 0) return LB_ST_BAD_ENCODING;
+  const uint8_t f = b[0];
+  const bool comp = (f & 0x80) != 0;
+  if (len != (comp ? 48u : 96u)) return LB_ST_BAD_ENCODING;
+  if (comp) {
+    if (f & 0x40) {
+      if ((f & 0x3f) == 0 && bytes_zero(b + 1, 47)) {
+        out.inf = true;
+        fp_zero(out.x);
+        fp_zero(out.y);
+        return LB_ST_OK;
+      }
+      return LB_ST_BAD_ENCODING;
+    }
+    if (!fp_read_masked(out.x, b, true)) return LB_ST_BAD_ENCODING;
+    fp rhs, bb;
+    fp_sqr(rhs, out.x);
+    fp_mul(rhs, rhs, out.x);
+    fp_set(bb, LB_B1);
+    fp_add(rhs, rhs, bb);
+    if (!fp_sqrt(out.y, rhs)) return LB_ST_NOT_ON_CURVE;
+    if (fp_lex_largest(out.y) != ((f & 0x20) != 0)) fp_neg(out.y, out.y);
+    return LB_ST_OK;
+  }
+  if (f & 0xe0) {
+    if ((f & 0x40) && (f & 0x3f) == 0 && bytes_zero(b + 1, 95)) {
+      out.inf = true;
+      fp_zero(out.x);
+      fp_zero(out.y);
+      return LB_ST_OK;
+    }
+    return LB_ST_BAD_ENCODING;
+  }
+  if (!fp_read_masked(out.x, b, false)) return LB_ST_BAD_ENCODING;
+  if (!fp_read_masked(out.y, b + 48, false)) return LB_ST_BAD_ENCODING;
+  if (!g1_aff_on_curve(out)) return LB_ST_NOT_ON_CURVE;
+  if (fp_is_zero(out.x) && fp_is_zero(out.y)) return LB_ST_NOT_IN_GROUP;
+  return LB_ST_OK;
+}
+
+// POINTonE2_Deserialize_Z + length rule (96 iff compressed); x = (c1 || c0).
+LB_DEV uint8_t g2_deserialize(g2a& out, const uint8_t* b, uint32_t len) {
+  out.inf = false;
+  if (len == 0) return LB_ST_BAD_ENCODING;
+  const uint8_t f = b[0];
+  const bool comp = (f & 0x80) != 0;
+  if (len != (comp ? 96u : 192u)) return LB_ST_BAD_ENCODING;
+  if (comp) {
+    if (f & 0x40) {
+      if ((f & 0x3f) == 0 && bytes_zero(b + 1, 95)) {
+        out.inf = true;
+        fp2_zero(out.x);
+        fp2_zero(out.y);
+        return LB_ST_OK;
+      }
+      return LB_ST_BAD_ENCODING;
+    }
+    if (!fp_read_masked(out.x.c1, b, true)) return LB_ST_BAD_ENCODING;
+    if (!fp_read_masked(out.x.c0, b + 48, false)) return LB_ST_BAD_ENCODING;
+    fp2 rhs, bb;
+    fp2_sqr(rhs, out.x);
+    fp2_mul(rhs, rhs, out.x);
+    fp2_set(bb, LB_B2);
+    fp2_add(rhs, rhs, bb);
+    if (!fp2_sqrt(out.y, rhs)) return LB_ST_NOT_ON_CURVE;
+    if (fp2_lex_largest(out.y) != ((f & 0x20) != 0)) fp2_neg(out.y, out.y);
+    return LB_ST_OK;
+  }
+  if (f & 0xe0) {
+    if ((f & 0x40) && (f & 0x3f) == 0 && bytes_zero(b + 1, 191)) {
+      out.inf = true;
+      fp2_zero(out.x);
+      fp2_zero(out.y);
+      return LB_ST_OK;
+    }
+    return LB_ST_BAD_ENCODING;
+  }
+  if (!fp_read_masked(out.x.c1, b, false)) return LB_ST_BAD_ENCODING;
+  if (!fp_read_masked(out.x.c0, b + 48, false)) return LB_ST_BAD_ENCODING;
+  if (!fp_read_masked(out.y.c1, b + 96, false)) return LB_ST_BAD_ENCODING;
+  if (!fp_read_masked(out.y.c0, b + 144, false)) return LB_ST_BAD_ENCODING;
+  if (!g2_aff_on_curve(out)) return LB_ST_NOT_ON_CURVE;
+  if (fp2_is_zero(out.x) && fp2_is_zero(out.y)) return LB_ST_NOT_IN_GROUP;
+  return LB_ST_OK;
+}
+
+LB_DEV void fp_write_be(uint8_t* out, const fp& a) {
+  fp raw;
+  fp_from_mont(raw, a);
+  fp_to_be48_raw(out, raw);
+}
+
+// blst_p1_affine_serialize / POINTonE1_Serialize (uncompressed, 96 bytes)
+LB_DEV void g1_serialize(uint8_t* out, const g1a& a) {
+  if (a.inf) {
+    for (int i = 0; i < 96; i++) out[i] = 0;
+    out[0] = 0x40;
+    return;
+  }
+  fp_write_be(out, a.x);
+  fp_write_be(out + 48, a.y);
+}
+LB_DEV void g1_compress(uint8_t* out, const g1a& a) {
+  if (a.inf) {
+    for (int i = 0; i < 48; i++) out[i] = 0;
+    out[0] = 0xc0;
+    return;
+  }
+  fp_write_be(out, a.x);
+  out[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
+}
+LB_DEV void g2_serialize(uint8_t* out, const g2a& a) {
+  if (a.inf) {
+    for (int i = 0; i < 192; i++) out[i] = 0;
+    out[0] = 0x40;
+    return;
+  }
+  fp_write_be(out, a.x.c1);
+  fp_write_be(out + 48, a.x.c0);
+  fp_write_be(out + 96, a.y.c1);
+  fp_write_be(out + 144, a.y.c0);
+}
+LB_DEV void g2_compress(uint8_t* out, const g2a& a) {
+  if (a.inf) {
+    for (int i = 0; i < 96; i++) out[i] = 0;
+    out[0] = 0xc0;
+    return;
+  }
+  fp_write_be(out, a.x.c1);
+  fp_write_be(out + 48, a.x.c0);
+  out[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+}
+
+}  // namespace lb

@@ -1,0 +1,943 @@
+// MI355X (gfx950) BLS12-381 signature-set verification pipeline + C ABI.
+//
+// One lane per signature set for the per-set stages; one workgroup per set
+// for pubkey aggregation; one lane per request for the request reductions.
+// Integer VALU only (v_mad_u64_u32 chains); see DESIGN.md for the roofline.
+//
+// Pipeline of lb_verify_requests (reference: BlsMultiThreadWorkerPool job ->
+// worker verifyManySignatureSets -> verifySignatureSetsMaybeBatch,
+// packages/beacon-node/src/chain/bls/multithread/worker.ts:30-108,
+// chain/bls/maybeBatch.ts:16-46):
+//   k_req_flags     per request : 1-set requests need core-verify checks
+//   k_decode_sigs   per set     : Signature.fromBytes(validate=true)
+//   k_pubkeys       per set (WG): PublicKey.fromBytes + PublicKey.aggregate
+//   k_hash          per set     : hash_to_G2(signing root)
+//   k_scalar        per set     : r_i pk_i (affine), r_i sig_i
+//   k_sum_req       per request : S_k = sum r_i sig_i
+//   k_miller        per pair    : f = Miller(r_i pk_i, H_i), Miller(-g1, S_k)
+//   k_final         per request : prod f, final exponentiation, == 1
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lodestar_bls.h"
+#include "bls_pairing.h"
+
+using namespace lb;
+
+#define LB_ST_ZERO_SIGNATURE 6
+
+// ============================================================================
+// Kernels
+// ============================================================================
+static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at high VGPR counts
+
+__global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   uint8_t* __restrict__ single_flag) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  for (uint32_t i = a; i < b; i++) single_flag[i] = (b - a == 1) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint32_t* __restrict__ sig_off, g2j* __restrict__ out_sig,
+                                                     uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t a = sig_off[i], b = sig_off[i + 1];
+  g2a s;
+  uint8_t st = g2_deserialize(s, sigs + a, b - a);
+  g2j sj;
+  jac_set_inf(sj);
+  if (st == LB_ST_OK) {
+    jac_from_aff(sj, s);
+    if (!g2_in_subgroup(sj)) st = LB_ST_NOT_IN_GROUP;
+  }
+  out_sig[i] = sj;
+  status[i] = st;
+}
+
+// One workgroup (one wave) per set: lanes decode pubkeys strided, LDS tree sum.
+__global__ void __launch_bounds__(TPB) k_pubkeys(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                 const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                 uint8_t* __restrict__ pk_status) {
+  __shared__ g1j sh[TPB];
+  __shared__ uint32_t bad;
+  const uint32_t set = blockIdx.x;
+  if (set >= n_sets) return;
+  const uint32_t a = pk_off ? pk_off[set] : set, b = pk_off ? pk_off[set + 1] : set + 1;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  g1j acc;
+  jac_set_inf(acc);
+  for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
+    g1a p;
+    const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
+    if (st != LB_ST_OK) {
+      atomicOr(&bad, 1u);
+    } else {
+      jac_add_aff(acc, acc, p);
+    }
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+      g1j o = sh[threadIdx.x + s];
+      g1j m = sh[threadIdx.x];
+      jac_add(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out_pk[set] = sh[0];
+    uint8_t st = LB_ST_OK;
+    if (b == a)
+      st = LB_ST_EMPTY_AGGREGATE;
+    else if (bad)
+      st = LB_ST_BAD_ENCODING;
+    else if (jac_is_inf(sh[0]))
+      st = LB_ST_PK_INFINITY;
+    pk_status[set] = st;
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t m[32];
+  for (int k = 0; k < 32; k++) m[k] = msgs[(size_t)i * 32 + k];
+  g2j h;
+  hash_to_g2(h, m);
+  g2a ha;
+  jac_to_aff(ha, h);
+  out_h[i] = ha;
+}
+
+// combined per-set status: signature decode, pubkey decode, core-verify checks
+__global__ void __launch_bounds__(TPB)
+    k_scalar(uint32_t n, const uint8_t* __restrict__ seed, const g1j* __restrict__ pk, const g2j* __restrict__ sig,
+             const uint8_t* __restrict__ sig_status, const uint8_t* __restrict__ pk_status,
+             const uint8_t* __restrict__ single_flag, g1a* __restrict__ rpk, g2j* __restrict__ rsig,
+             uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = sig_status[i];
+  if (st == LB_ST_OK) st = pk_status[i];
+  g1j p = pk[i];
+  g2j s = sig[i];
+  if (st == LB_ST_OK && single_flag[i]) {
+    // BlsVerifier single-set path: sig.verify -> ZeroSignatureError on infinity,
+    // core_verify checks the pubkey subgroup
+    if (jac_is_inf(s)) st = LB_ST_ZERO_SIGNATURE;
+    else if (!g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
+  }
+  g1a pa;
+  fp_zero(pa.x);
+  fp_zero(pa.y);
+  pa.inf = true;
+  g2j rs;
+  jac_set_inf(rs);
+  if (st == LB_ST_OK) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    const uint64_t r = batch_scalar(sd, i);
+    g1j rp;
+    jac_mul_u64(rp, p, r);
+    jac_to_aff(pa, rp);
+    jac_mul_u64(rs, s, r);
+  }
+  rpk[i] = pa;
+  rsig[i] = rs;
+  status[i] = st;
+}
+
+__global__ void __launch_bounds__(TPB) k_sum_req(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                 const g2j* __restrict__ rsig, const uint8_t* __restrict__ status,
+                                                 g2a* __restrict__ S, uint8_t* __restrict__ req_bad) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  uint8_t bad = (a == b) ? 1 : 0;
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint32_t i = a; i < b && !bad; i++) {
+    if (status[i] != LB_ST_OK) {
+      bad = 1;
+    } else {
+      g2j t = rsig[i];
+      jac_add(acc, acc, t);
+    }
+  }
+  g2a sa;
+  jac_to_aff(sa, acc);
+  S[k] = sa;
+  req_bad[k] = bad;
+}
+
+__global__ void __launch_bounds__(TPB)
+    k_miller(uint32_t n_sets, uint32_t n_req, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+             const uint8_t* __restrict__ status, const g2a* __restrict__ S, const uint8_t* __restrict__ req_bad,
+             fp12* __restrict__ f) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_sets + n_req) return;
+  fp12 r;
+  fp12_one(r);
+  if (j < n_sets) {
+    if (status[j] == LB_ST_OK) {
+      g1a p = rpk[j];
+      g2a q = h[j];
+      if (!p.inf && !q.inf) miller_loop(r, p, q);
+    }
+  } else {
+    const uint32_t k = j - n_sets;
+    g2a q = S[k];
+    if (!req_bad[k] && !q.inf) {
+      g1a g;
+      fp_set(g.x, LB_G1_X);
+      fp_set(g.y, LB_G1_NEG_Y);
+      g.inf = false;
+      miller_loop(r, g, q);
+    }
+  }
+  f[j] = r;
+}
+
+__global__ void __launch_bounds__(TPB) k_final(uint32_t n_sets, uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                               const fp12* __restrict__ f, const uint8_t* __restrict__ req_bad,
+                                               uint8_t* __restrict__ valid) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  if (req_bad[k]) {
+    valid[k] = 0;
+    return;
+  }
+  fp12 acc = f[n_sets + k];
+  for (uint32_t i = req_off[k]; i < req_off[k + 1]; i++) {
+    fp12 t = f[i];
+    fp12_mul(acc, acc, t);
+  }
+  fp12 r;
+  final_exp(r, acc);
+  valid[k] = fp12_is_one(r) ? 1 : 0;
+}
+
+// request-level error codes (reject rather than false)
+__global__ void __launch_bounds__(TPB) k_req_errors(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                    const uint8_t* __restrict__ pk_status, uint8_t* __restrict__ err) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  uint8_t e = LB_REQ_OK;
+  for (uint32_t i = req_off[k]; i < req_off[k + 1]; i++) {
+    if (pk_status[i] == LB_ST_EMPTY_AGGREGATE && e == LB_REQ_OK) e = LB_REQ_EMPTY_AGGREGATE;
+    if (pk_status[i] == LB_ST_BAD_ENCODING && e == LB_REQ_OK) e = LB_REQ_BAD_PUBKEY;
+  }
+  err[k] = e;
+}
+
+// ---- generic point sums (one workgroup, LDS tree) ------------------------
+template <class F>
+__global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out) {
+  __shared__ jac<F> sh[256];
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    jac<F> t = in[i];
+    jac_add(acc, acc, t);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      jac<F> m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      jac_add(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sh[0];
+}
+
+__global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1j p = in[i];
+  g1a a;
+  jac_to_aff(a, p);
+  g1_serialize(out96 + (size_t)i * 96, a);
+}
+__global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* __restrict__ out192) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j p = in[i];
+  g2a a;
+  jac_to_aff(a, p);
+  g2_serialize(out192 + (size_t)i * 192, a);
+}
+__global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a a = in[i];
+  g2_serialize(out192 + (size_t)i * 192, a);
+}
+
+// ---- stage-level kernels for parity tests ---------------------------------
+__global__ void k_pairing(uint32_t n, const uint8_t* __restrict__ g1b, const uint8_t* __restrict__ g2b,
+                          uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a p;
+  g2a q;
+  const uint8_t s1 = g1_deserialize(p, g1b + (size_t)i * 96, 96);
+  const uint8_t s2 = g2_deserialize(q, g2b + (size_t)i * 192, 192);
+  fp12 f, r;
+  fp12_one(f);
+  if (s1 == LB_ST_OK && s2 == LB_ST_OK && !p.inf && !q.inf) miller_loop(f, p, q);
+  final_exp(r, f);
+  uint8_t* o = out + (size_t)i * 576;
+  const fp2* c[6] = {&r.c0.c0, &r.c0.c1, &r.c0.c2, &r.c1.c0, &r.c1.c1, &r.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    fp_write_be(o + 96 * k, c[k]->c0);
+    fp_write_be(o + 96 * k + 48, c[k]->c1);
+  }
+}
+__global__ void k_scalars(const uint8_t* __restrict__ seed, uint32_t first, uint32_t n, uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t sd[32];
+  for (int k = 0; k < 32; k++) sd[k] = seed[k];
+  out[i] = batch_scalar(sd, first + i);
+}
+__global__ void k_g1_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a a;
+  g1_deserialize(a, in + (size_t)i * 96, 96);
+  g1j p, r;
+  jac_from_aff(p, a);
+  jac_mul_u64(r, p, k[i]);
+  jac_to_aff(a, r);
+  g1_serialize(out + (size_t)i * 96, a);
+}
+__global__ void k_g2_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a a;
+  g2_deserialize(a, in + (size_t)i * 192, 192);
+  g2j p, r;
+  jac_from_aff(p, a);
+  jac_mul_u64(r, p, k[i]);
+  jac_to_aff(a, r);
+  g2_serialize(out + (size_t)i * 192, a);
+}
+
+// ============================================================================
+// Host side: context, workspace, C ABI
+// ============================================================================
+struct lb_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  std::string err;
+  char* d_ws = nullptr;
+  size_t ws_cap = 0;
+  char* h_pin = nullptr;
+  size_t pin_cap = 0;
+  static constexpr int kMaxEv = 16;
+  hipEvent_t ev[kMaxEv] = {};
+  const char* ev_name[kMaxEv] = {};
+  int n_ev = 0;
+  float stage_ms[kMaxEv] = {};
+  const char* stage_name[kMaxEv] = {};
+  int n_stages = 0;
+};
+
+namespace {
+
+#define LB_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);                    \
+      return LB_ERR_DEVICE;                                                            \
+    }                                                                                  \
+  } while (0)
+
+inline uint32_t blocks_for(uint32_t n, uint32_t tpb = TPB) { return (n + tpb - 1) / tpb; }
+
+struct Bump {
+  char* base;
+  size_t off = 0;
+  size_t cap;
+  template <class T>
+  T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = reinterpret_cast<T*>(base + off);
+    off += sizeof(T) * count;
+    return p;
+  }
+};
+
+int ensure_ws(lb_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->ws_cap) return LB_OK;
+  if (ctx->d_ws) {
+    LB_HIP(hipStreamSynchronize(ctx->stream));
+    LB_HIP(hipFree(ctx->d_ws));
+    ctx->d_ws = nullptr;
+    ctx->ws_cap = 0;
+  }
+  size_t cap = bytes + bytes / 4 + (1 << 20);
+  if (hipMalloc(&ctx->d_ws, cap) != hipSuccess) {
+    ctx->err = "hipMalloc workspace failed";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  ctx->ws_cap = cap;
+  return LB_OK;
+}
+
+int ensure_pin(lb_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->pin_cap) return LB_OK;
+  if (ctx->h_pin) {
+    LB_HIP(hipStreamSynchronize(ctx->stream));
+    LB_HIP(hipHostFree(ctx->h_pin));
+    ctx->h_pin = nullptr;
+    ctx->pin_cap = 0;
+  }
+  size_t cap = bytes + bytes / 4 + (1 << 20);
+  if (hipHostMalloc(&ctx->h_pin, cap, hipHostMallocDefault) != hipSuccess) {
+    ctx->err = "hipHostMalloc staging failed";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  ctx->pin_cap = cap;
+  return LB_OK;
+}
+
+int mark(lb_ctx* ctx, const char* name) {
+  if (ctx->n_ev >= lb_ctx::kMaxEv) return LB_OK;
+  LB_HIP(hipEventRecord(ctx->ev[ctx->n_ev], ctx->stream));
+  ctx->ev_name[ctx->n_ev] = name;
+  ctx->n_ev++;
+  return LB_OK;
+}
+
+int collect_marks(lb_ctx* ctx) {
+  ctx->n_stages = 0;
+  for (int i = 1; i < ctx->n_ev; i++) {
+    float ms = 0.f;
+    LB_HIP(hipEventElapsedTime(&ms, ctx->ev[i - 1], ctx->ev[i]));
+    ctx->stage_ms[ctx->n_stages] = ms;
+    ctx->stage_name[ctx->n_stages] = ctx->ev_name[i];
+    ctx->n_stages++;
+  }
+  return LB_OK;
+}
+
+#define LB_TRY(x)             \
+  do {                        \
+    int rc_ = (x);            \
+    if (rc_ != LB_OK) return rc_; \
+  } while (0)
+
+#define LB_LAUNCH(kern, grid, block, ...)                                     \
+  do {                                                                        \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, ctx->stream, __VA_ARGS__); \
+    LB_HIP(hipGetLastError());                                                \
+  } while (0)
+
+// Core pipeline on device-resident inputs.  All pointers are device pointers.
+int run_pipeline(lb_ctx* ctx, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off, const uint8_t* d_pks,
+                 const uint32_t* d_pk_off, const uint8_t* d_msgs, const uint8_t* d_sigs, const uint32_t* d_sig_off,
+                 const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err, uint8_t* d_set_status, Bump& ws) {
+  g2j* d_sig = ws.take<g2j>(n_sets);
+  g1j* d_pk = ws.take<g1j>(n_sets);
+  g1a* d_rpk = ws.take<g1a>(n_sets);
+  g2j* d_rsig = ws.take<g2j>(n_sets);
+  g2a* d_h = ws.take<g2a>(n_sets);
+  uint8_t* d_sig_st = ws.take<uint8_t>(n_sets);
+  uint8_t* d_pk_st = ws.take<uint8_t>(n_sets);
+  uint8_t* d_single = ws.take<uint8_t>(n_sets);
+  uint8_t* d_st = d_set_status ? d_set_status : ws.take<uint8_t>(n_sets);
+  g2a* d_S = ws.take<g2a>(n_req);
+  uint8_t* d_bad = ws.take<uint8_t>(n_req);
+  fp12* d_f = ws.take<fp12>((size_t)n_sets + n_req);
+  if (ws.off > ws.cap) {
+    ctx->err = "workspace overflow";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  if (n_sets > 0) {
+    LB_LAUNCH(k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
+    LB_TRY(mark(ctx, "req_flags"));
+    LB_LAUNCH(k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off, d_sig, d_sig_st);
+    LB_TRY(mark(ctx, "decode_sigs"));
+    LB_LAUNCH(k_pubkeys, n_sets, TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
+    LB_TRY(mark(ctx, "pubkeys"));
+    LB_LAUNCH(k_hash, blocks_for(n_sets), TPB, n_sets, d_msgs, d_h);
+    LB_TRY(mark(ctx, "hash_to_g2"));
+    LB_LAUNCH(k_scalar, blocks_for(n_sets), TPB, n_sets, d_seed, d_pk, d_sig, d_sig_st, d_pk_st, d_single, d_rpk,
+              d_rsig, d_st);
+    LB_TRY(mark(ctx, "scalar_mul"));
+  }
+  LB_LAUNCH(k_sum_req, blocks_for(n_req), TPB, n_req, d_req_off, d_rsig, d_st, d_S, d_bad);
+  LB_TRY(mark(ctx, "sum_sigs"));
+  LB_LAUNCH(k_miller, blocks_for(n_sets + n_req), TPB, n_sets, n_req, d_rpk, d_h, d_st, d_S, d_bad, d_f);
+  LB_TRY(mark(ctx, "miller"));
+  LB_LAUNCH(k_final, blocks_for(n_req), TPB, n_sets, n_req, d_req_off, d_f, d_bad, d_valid);
+  LB_TRY(mark(ctx, "final_exp"));
+  LB_LAUNCH(k_req_errors, blocks_for(n_req), TPB, n_req, d_req_off, d_pk_st, d_req_err);
+  return LB_OK;
+}
+
+size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
+  size_t per_set = sizeof(g2j) * 2 + sizeof(g1j) + sizeof(g1a) + sizeof(g2a) + 4 + sizeof(fp12) + 6 * 256 / 64;
+  size_t per_req = sizeof(g2a) + 1 + sizeof(fp12);
+  return (size_t)n_sets * per_set + (size_t)n_req * per_req + 64 * 256;
+}
+
+int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
+  if (!b || !b->request_offsets || !b->messages || !b->signatures || !b->sig_offsets || !b->seed ||
+      (b->n_sets && !b->pubkeys)) {
+    ctx->err = "null pointer in lb_request_batch";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  return LB_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int lb_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int lb_create(int device, lb_ctx** out_ctx) {
+  if (!out_ctx) return LB_ERR_INVALID_ARGUMENT;
+  *out_ctx = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || device < 0 || device >= n) return LB_ERR_NO_DEVICE;
+  lb_ctx* ctx = new lb_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return LB_ERR_DEVICE;
+  }
+  for (int i = 0; i < lb_ctx::kMaxEv; i++) {
+    if (hipEventCreate(&ctx->ev[i]) != hipSuccess) {
+      delete ctx;
+      return LB_ERR_DEVICE;
+    }
+  }
+  *out_ctx = ctx;
+  return LB_OK;
+}
+
+int lb_destroy(lb_ctx* ctx) {
+  if (!ctx) return LB_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  for (int i = 0; i < lb_ctx::kMaxEv; i++)
+    if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return LB_OK;
+}
+
+const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names, int max_stages) {
+  if (!ctx) return 0;
+  int n = ctx->n_stages < max_stages ? ctx->n_stages : max_stages;
+  for (int i = 0; i < n; i++) {
+    if (out_ms) out_ms[i] = ctx->stage_ms[i];
+    if (out_names) out_names[i] = ctx->stage_name[i];
+  }
+  return ctx->n_stages;
+}
+
+int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
+                              uint8_t* d_set_status, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  auto t0 = std::chrono::steady_clock::now();
+  if (b->n_requests == 0) {
+    if (stats) *stats = lb_verify_stats{0, 0, 0.0};
+    return LB_OK;
+  }
+  LB_TRY(ensure_ws(ctx, pipeline_ws_bytes(b->n_requests, b->n_sets)));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  ctx->n_ev = 0;
+  LB_TRY(mark(ctx, "start"));
+  LB_TRY(run_pipeline(ctx, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets, b->messages,
+                      b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err, d_set_status, ws));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  LB_TRY(collect_marks(ctx));
+  if (stats) {
+    stats->batch_retries = 0;
+    stats->batch_sigs_success = 0;
+    stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return LB_OK;
+}
+
+int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
+                       uint8_t* out_set_status, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  auto t0 = std::chrono::steady_clock::now();
+  const uint32_t nr = b->n_requests, ns = b->n_sets;
+  if (nr == 0) {
+    if (stats) *stats = lb_verify_stats{0, 0, 0.0};
+    return LB_OK;
+  }
+  // validate offsets on the host (a kernel must never index out of bounds)
+  if (b->request_offsets[0] != 0 || b->request_offsets[nr] != ns) {
+    ctx->err = "request_offsets must start at 0 and end at n_sets";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  for (uint32_t k = 0; k < nr; k++)
+    if (b->request_offsets[k + 1] < b->request_offsets[k]) {
+      ctx->err = "request_offsets not monotone";
+      return LB_ERR_INVALID_ARGUMENT;
+    }
+  for (uint32_t i = 0; i < ns; i++)
+    if (b->sig_offsets[i + 1] < b->sig_offsets[i]) {
+      ctx->err = "sig_offsets not monotone";
+      return LB_ERR_INVALID_ARGUMENT;
+    }
+  std::vector<uint32_t> pk_off_local;
+  const uint32_t* pk_off = b->pk_offsets;
+  if (!pk_off) {
+    pk_off_local.resize(ns + 1);
+    for (uint32_t i = 0; i <= ns; i++) pk_off_local[i] = i;
+    pk_off = pk_off_local.data();
+  } else {
+    if (pk_off[0] != 0) {
+      ctx->err = "pk_offsets must start at 0";
+      return LB_ERR_INVALID_ARGUMENT;
+    }
+    for (uint32_t i = 0; i < ns; i++)
+      if (pk_off[i + 1] < pk_off[i]) {
+        ctx->err = "pk_offsets not monotone";
+        return LB_ERR_INVALID_ARGUMENT;
+      }
+  }
+  const size_t n_pk = pk_off[ns];
+  const size_t sig_bytes = b->sig_offsets[ns];
+  // staging layout
+  const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = sizeof(uint32_t) * (ns + 1),
+               sz_pk = n_pk * 96, sz_msg = (size_t)ns * 32, sz_sigo = sizeof(uint32_t) * (ns + 1),
+               sz_sig = sig_bytes, sz_seed = 32;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
+  const size_t out_bytes = al(nr) * 2 + al(ns);
+  LB_TRY(ensure_pin(ctx, in_bytes + out_bytes));
+  LB_TRY(ensure_ws(ctx, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  char* h = ctx->h_pin;
+  size_t ho = 0;
+  auto stage = [&](const void* src, size_t n) {
+    char* p = h + ho;
+    if (n) memcpy(p, src, n);
+    ho += al(n);
+    return p;
+  };
+  stage(b->request_offsets, sz_req);
+  stage(pk_off, sz_pko);
+  stage(b->pubkeys, sz_pk);
+  stage(b->messages, sz_msg);
+  stage(b->sig_offsets, sz_sigo);
+  stage(b->signatures, sz_sig);
+  stage(b->seed, sz_seed);
+  char* d_in = ws.take<char>(in_bytes);
+  uint8_t* d_valid = ws.take<uint8_t>(nr);
+  uint8_t* d_err = ws.take<uint8_t>(nr);
+  uint8_t* d_sst = ws.take<uint8_t>(ns ? ns : 1);
+  ctx->n_ev = 0;
+  LB_TRY(mark(ctx, "start"));
+  LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+  LB_TRY(mark(ctx, "h2d"));
+  size_t o = 0;
+  auto dptr = [&](size_t n) {
+    char* p = d_in + o;
+    o += al(n);
+    return p;
+  };
+  const uint32_t* d_req = (const uint32_t*)dptr(sz_req);
+  const uint32_t* d_pko = (const uint32_t*)dptr(sz_pko);
+  const uint8_t* d_pks = (const uint8_t*)dptr(sz_pk);
+  const uint8_t* d_msg = (const uint8_t*)dptr(sz_msg);
+  const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
+  const uint8_t* d_sig = (const uint8_t*)dptr(sz_sig);
+  const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
+  LB_TRY(run_pipeline(ctx, nr, ns, d_req, d_pks, d_pko, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
+  char* h_out = h + in_bytes;
+  LB_HIP(hipMemcpyAsync(h_out, d_valid, nr, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipMemcpyAsync(h_out + al(nr), d_err, nr, hipMemcpyDeviceToHost, ctx->stream));
+  if (ns) LB_HIP(hipMemcpyAsync(h_out + 2 * al(nr), d_sst, ns, hipMemcpyDeviceToHost, ctx->stream));
+  LB_TRY(mark(ctx, "d2h"));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  LB_TRY(collect_marks(ctx));
+  memcpy(out_valid, h_out, nr);
+  memcpy(out_req_err, h_out + al(nr), nr);
+  if (out_set_status && ns) memcpy(out_set_status, h_out + 2 * al(nr), ns);
+  if (stats) {
+    stats->batch_retries = 0;
+    stats->batch_sigs_success = 0;
+    stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return LB_OK;
+}
+
+// ---- helpers for small host-buffer calls ----------------------------------
+static int upload(lb_ctx* ctx, Bump& ws, const void* src, size_t n, void** out) {
+  char* d = ws.take<char>(n ? n : 1);
+  if (n) LB_HIP(hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, ctx->stream));
+  *out = d;
+  return LB_OK;
+}
+
+int lb_hash_to_g2(lb_ctx* ctx, uint32_t n, const uint8_t* messages, uint8_t* out192) {
+  if (!ctx || (n && (!messages || !out192))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (32 + sizeof(g2a) + 192) + 4096));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void* d_msg;
+  LB_TRY(upload(ctx, ws, messages, (size_t)n * 32, &d_msg));
+  g2a* d_h = ws.take<g2a>(n);
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
+  LB_LAUNCH(k_hash, blocks_for(n), TPB, n, (const uint8_t*)d_msg, d_h);
+  LB_LAUNCH(k_g2a_serialize, blocks_for(n), TPB, n, (const g2a*)d_h, d_out);
+  LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_decode_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const uint32_t* sig_off, uint8_t* out_status,
+                         uint8_t* out192) {
+  if (!ctx || (n && (!sigs || !sig_off || !out_status))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  for (uint32_t i = 0; i < n; i++)
+    if (sig_off[i + 1] < sig_off[i]) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  const size_t nb = sig_off[n];
+  LB_TRY(ensure_ws(ctx, nb + (size_t)n * (4 + sizeof(g2j) + 1 + 192) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d_s, *d_o;
+  LB_TRY(upload(ctx, ws, sigs, nb, &d_s));
+  LB_TRY(upload(ctx, ws, sig_off, sizeof(uint32_t) * (n + 1), &d_o));
+  g2j* d_sig = ws.take<g2j>(n);
+  uint8_t* d_st = ws.take<uint8_t>(n);
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
+  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, d_sig, d_st);
+  LB_LAUNCH(k_g2_serialize, blocks_for(n), TPB, n, (const g2j*)d_sig, d_out);
+  LB_HIP(hipMemcpyAsync(out_status, d_st, n, hipMemcpyDeviceToHost, ctx->stream));
+  if (out192) LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint8_t* out96, uint8_t* out_status) {
+  if (!ctx || !out96 || (n && !pks)) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) {
+    ctx->err = "EMPTY_AGGREGATE_ARRAY";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * 96 + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void* d_p;
+  LB_TRY(upload(ctx, ws, pks, (size_t)n * 96, &d_p));
+  uint32_t off[2] = {0, n};
+  void* d_off;
+  LB_TRY(upload(ctx, ws, off, sizeof(off), &d_off));
+  g1j* d_pk = ws.take<g1j>(1);
+  uint8_t* d_st = ws.take<uint8_t>(1);
+  uint8_t* d_out = ws.take<uint8_t>(96);
+  LB_LAUNCH(k_pubkeys, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_g1_serialize, 1, TPB, 1u, (const g1j*)d_pk, d_out);
+  uint8_t st = 0;
+  LB_HIP(hipMemcpyAsync(out96, d_out, 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipMemcpyAsync(&st, d_st, 1, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  if (st == LB_ST_PK_INFINITY) st = LB_ST_OK;  // an infinite aggregate is a valid encoding (0x40...)
+  if (out_status) *out_status = st;
+  return LB_OK;
+}
+
+int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const uint32_t* sig_off, uint8_t* out192,
+                            int32_t* out_bad_index) {
+  if (!ctx || !out192 || !out_bad_index || (n && (!sigs || !sig_off))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) {
+    ctx->err = "EMPTY_AGGREGATE_ARRAY";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  for (uint32_t i = 0; i < n; i++)
+    if (sig_off[i + 1] < sig_off[i]) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  const size_t nb = sig_off[n];
+  LB_TRY(ensure_ws(ctx, nb + (size_t)n * (4 + sizeof(g2j) + 1) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d_s, *d_o;
+  LB_TRY(upload(ctx, ws, sigs, nb, &d_s));
+  LB_TRY(upload(ctx, ws, sig_off, sizeof(uint32_t) * (n + 1), &d_o));
+  g2j* d_sig = ws.take<g2j>(n);
+  uint8_t* d_st = ws.take<uint8_t>(n);
+  g2j* d_sum = ws.take<g2j>(1);
+  uint8_t* d_out = ws.take<uint8_t>(192);
+  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, d_sig, d_st);
+  LB_LAUNCH(k_jac_sum<fp2>, 1, 256, n, (const g2j*)d_sig, d_sum);
+  LB_LAUNCH(k_g2_serialize, 1, TPB, 1u, (const g2j*)d_sum, d_out);
+  std::vector<uint8_t> st(n);
+  LB_HIP(hipMemcpyAsync(st.data(), d_st, n, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipMemcpyAsync(out192, d_out, 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  *out_bad_index = -1;
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] != LB_ST_OK) {
+      *out_bad_index = (int32_t)i;
+      break;
+    }
+  return LB_OK;
+}
+
+int lb_verify_same_message(lb_ctx* ctx, uint32_t n, const uint8_t* pks, const uint8_t* sigs, const uint32_t* sig_off,
+                           const uint8_t* message, const uint8_t* seed, uint8_t* out_valid,
+                           uint32_t* out_used_fast_path) {
+  if (!ctx || (n && (!pks || !sigs || !sig_off || !message || !seed || !out_valid))) return LB_ERR_INVALID_ARGUMENT;
+  if (out_used_fast_path) *out_used_fast_path = 0;
+  if (n == 0) return LB_OK;
+  // 1. validate-deserialize every signature (jobItemWorkReq sameMessage, jobItem.ts:72-74)
+  std::vector<uint8_t> st(n);
+  LB_TRY(lb_decode_signatures(ctx, n, sigs, sig_off, st.data(), nullptr));
+  bool all_ok = true;
+  for (uint32_t i = 0; i < n; i++) all_ok &= (st[i] == LB_ST_OK);
+  if (all_ok) {
+    // 2. aggregate pubkeys and signatures (plain sums, no randomness) and
+    //    verify once: worker maybeBatch with one set (index.ts:455-489)
+    uint8_t agg_pk[96], agg_sig[192];
+    uint8_t pst = 0;
+    int32_t bad = -1;
+    LB_TRY(lb_aggregate_pubkeys(ctx, n, pks, agg_pk, &pst));
+    LB_TRY(lb_aggregate_signatures(ctx, n, sigs, sig_off, agg_sig, &bad));
+    uint32_t req_off[2] = {0, 1}, so[2] = {0, 192};
+    lb_request_batch b{};
+    b.n_requests = 1;
+    b.n_sets = 1;
+    b.request_offsets = req_off;
+    b.pubkeys = agg_pk;
+    b.messages = message;
+    b.signatures = agg_sig;
+    b.sig_offsets = so;
+    b.seed = seed;
+    uint8_t valid = 0, err = 0;
+    LB_TRY(lb_verify_requests(ctx, &b, &valid, &err, nullptr, nullptr));
+    if (valid && err == LB_REQ_OK && pst == LB_ST_OK) {
+      for (uint32_t i = 0; i < n; i++) out_valid[i] = 1;
+      if (out_used_fast_path) *out_used_fast_path = 1;
+      return LB_OK;
+    }
+  }
+  // 3. retry every set alone (jobItemSameMessageToMultiSet, jobItem.ts:93-125)
+  std::vector<uint32_t> req_off(n + 1);
+  for (uint32_t i = 0; i <= n; i++) req_off[i] = i;
+  std::vector<uint8_t> msgs((size_t)n * 32);
+  for (uint32_t i = 0; i < n; i++) memcpy(&msgs[(size_t)i * 32], message, 32);
+  lb_request_batch b{};
+  b.n_requests = n;
+  b.n_sets = n;
+  b.request_offsets = req_off.data();
+  b.pubkeys = pks;
+  b.messages = msgs.data();
+  b.signatures = sigs;
+  b.sig_offsets = sig_off;
+  b.seed = seed;
+  std::vector<uint8_t> err(n);
+  LB_TRY(lb_verify_requests(ctx, &b, out_valid, err.data(), nullptr, nullptr));
+  for (uint32_t i = 0; i < n; i++)
+    if (err[i] != LB_REQ_OK) out_valid[i] = 0;
+  return LB_OK;
+}
+
+int lb_pairing(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint8_t* g2_192, uint8_t* out576) {
+  if (!ctx || (n && (!g1_96 || !g2_192 || !out576))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (96 + 192 + 576) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d1, *d2;
+  LB_TRY(upload(ctx, ws, g1_96, (size_t)n * 96, &d1));
+  LB_TRY(upload(ctx, ws, g2_192, (size_t)n * 192, &d2));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 576);
+  LB_LAUNCH(k_pairing, blocks_for(n), TPB, n, (const uint8_t*)d1, (const uint8_t*)d2, d_out);
+  LB_HIP(hipMemcpyAsync(out576, d_out, (size_t)n * 576, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_batch_scalars(lb_ctx* ctx, const uint8_t* seed, uint32_t first, uint32_t n, uint64_t* out) {
+  if (!ctx || !seed || (n && !out)) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * 8 + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void* d_seed;
+  LB_TRY(upload(ctx, ws, seed, 32, &d_seed));
+  uint64_t* d_out = ws.take<uint64_t>(n);
+  LB_LAUNCH(k_scalars, blocks_for(n), TPB, (const uint8_t*)d_seed, first, n, d_out);
+  LB_HIP(hipMemcpyAsync(out, d_out, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_g1_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in96, const uint64_t* k, uint8_t* out96) {
+  if (!ctx || (n && (!in96 || !k || !out96))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (96 * 2 + 8) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d_in, *d_k;
+  LB_TRY(upload(ctx, ws, in96, (size_t)n * 96, &d_in));
+  LB_TRY(upload(ctx, ws, k, (size_t)n * 8, &d_k));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
+  LB_LAUNCH(k_g1_mul, blocks_for(n), TPB, n, (const uint8_t*)d_in, (const uint64_t*)d_k, d_out);
+  LB_HIP(hipMemcpyAsync(out96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* k, uint8_t* out192) {
+  if (!ctx || (n && (!in192 || !k || !out192))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (192 * 2 + 8) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d_in, *d_k;
+  LB_TRY(upload(ctx, ws, in192, (size_t)n * 192, &d_in));
+  LB_TRY(upload(ctx, ws, k, (size_t)n * 8, &d_k));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
+  LB_LAUNCH(k_g2_mul, blocks_for(n), TPB, n, (const uint8_t*)d_in, (const uint64_t*)d_k, d_out);
+  LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+}  // extern "C"

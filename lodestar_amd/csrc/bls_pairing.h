@@ -1,0 +1,168 @@
+// Optimal-ate pairing for BLS12-381 on gfx950: Miller loop with the twisted
+// point T in homogeneous projective coordinates, and the shared final
+// exponentiation.  The checked quantity is the batch equation of blst's
+// Pairing.mul_n_aggregate + finalverify (reached from
+// packages/beacon-node/src/chain/bls/maybeBatch.ts:19):
+//     prod_i e(r_i pk_i, H(m_i)) * e(-g1, sum_i r_i sig_i) == 1.
+//
+// Lines are scaled by w^3 and by Fp2 factors, both of which vanish in the
+// final exponentiation, so f^((p^12-1)/r) is canonical.  The final
+// exponentiation computes f^(3 (p^12-1)/r) via
+//   3 (p^4 - p^2 + 1)/r = (x-1)^2 (x+p) (x^2+p^2-1) + 3,
+// (checked against the definition by tests/test_oracle_mirror.py); the factor
+// 3 is coprime to r, so "== 1" verdicts are unchanged.
+#pragma once
+#include "bls_hash.h"
+
+namespace lb {
+
+struct g2proj {
+  fp2 X, Y, Z;  // homogeneous: x = X/Z, y = Y/Z
+};
+
+// T <- 2T and the tangent line at T evaluated at P = (xp, yp):
+//   l = (Y^2 - 3b'Z^2) + (-3X^2 xp) v + (2YZ yp) v w
+LB_DEV void miller_dbl_step(g2proj& T, fp2& l0, fp2& l1, fp2& l4, const fp& xp, const fp& yp) {
+  fp2 XX, B, C, E, F, A, G, H, t;
+  fp2_sqr(XX, T.X);
+  fp2_sqr(B, T.Y);
+  fp2_sqr(C, T.Z);
+  fp2_mul_const(E, C, LB_B2X3);  // 3 b' Z^2
+  fp2_mul3(F, E);
+  fp half;
+  fp_set(half, LB_HALF);
+  fp2_mul(A, T.X, T.Y);
+  fp2_mul_fp(A, A, half);
+  fp2_add(G, B, F);
+  fp2_mul_fp(G, G, half);
+  fp2_add(H, T.Y, T.Z);
+  fp2_sqr(H, H);
+  fp2_sub(H, H, B);
+  fp2_sub(H, H, C);  // 2YZ
+  // line
+  fp2_sub(l0, B, E);
+  fp2_mul3(t, XX);
+  fp2_mul_fp(t, t, xp);
+  fp2_neg(l1, t);
+  fp2_mul_fp(l4, H, yp);
+  // point
+  fp2_sub(t, B, F);
+  fp2_mul(T.X, A, t);
+  fp2 E2_;
+  fp2_sqr(E2_, E);
+  fp2_mul3(E2_, E2_);
+  fp2_sqr(T.Y, G);
+  fp2_sub(T.Y, T.Y, E2_);
+  fp2_mul(T.Z, B, H);
+}
+
+// T <- T + Q (Q affine) and the chord through T, Q evaluated at P:
+//   th = Y - yq Z, la = X - xq Z
+//   l = (th xq - la yq) + (-th xp) v + (la yp) v w
+LB_DEV void miller_add_step(g2proj& T, const fp2& xq, const fp2& yq, fp2& l0, fp2& l1, fp2& l4, const fp& xp,
+                            const fp& yp) {
+  fp2 th, la, C, D, E, F, G, H, t;
+  fp2_mul(t, yq, T.Z);
+  fp2_sub(th, T.Y, t);
+  fp2_mul(t, xq, T.Z);
+  fp2_sub(la, T.X, t);
+  // line
+  fp2_mul(l0, th, xq);
+  fp2_mul(t, la, yq);
+  fp2_sub(l0, l0, t);
+  fp2_mul_fp(t, th, xp);
+  fp2_neg(l1, t);
+  fp2_mul_fp(l4, la, yp);
+  // point
+  fp2_sqr(C, th);
+  fp2_sqr(D, la);
+  fp2_mul(E, la, D);
+  fp2_mul(F, T.Z, C);
+  fp2_mul(G, T.X, D);
+  fp2_add(H, E, F);
+  fp2_sub(H, H, G);
+  fp2_sub(H, H, G);
+  fp2_mul(T.X, la, H);
+  fp2_sub(t, G, H);
+  fp2_mul(t, th, t);
+  fp2 ye;
+  fp2_mul(ye, T.Y, E);
+  fp2_sub(T.Y, t, ye);
+  fp2_mul(T.Z, T.Z, E);
+}
+
+// f = f_{|x|,Q}(P), conjugated (x < 0).  P, Q affine, not infinity.
+LB_NOINL void miller_loop(fp12& f, const g1a& P, const g2a& Q) {
+  g2proj T;
+  T.X = Q.x;
+  T.Y = Q.y;
+  fp2_one(T.Z);
+  fp2 l0, l1, l4;
+  // first iteration (bit 62 of |x|): f = 1 * line
+  miller_dbl_step(T, l0, l1, l4, P.x, P.y);
+  fp6_zero(f.c0);
+  fp6_zero(f.c1);
+  f.c0.c0 = l0;
+  f.c0.c1 = l1;
+  f.c1.c1 = l4;
+  if ((LB_X_ABS >> 62) & 1ull) {
+    miller_add_step(T, Q.x, Q.y, l0, l1, l4, P.x, P.y);
+    fp12_mul_line(f, f, l0, l1, l4);
+  }
+  for (int i = 61; i >= 0; i--) {
+    fp12_sqr(f, f);
+    miller_dbl_step(T, l0, l1, l4, P.x, P.y);
+    fp12_mul_line(f, f, l0, l1, l4);
+    if ((LB_X_ABS >> i) & 1ull) {
+      miller_add_step(T, Q.x, Q.y, l0, l1, l4, P.x, P.y);
+      fp12_mul_line(f, f, l0, l1, l4);
+    }
+  }
+  fp12_conj(f, f);
+}
+
+// a^x for the (negative) BLS parameter, a in the cyclotomic subgroup (so a^-1 = conj(a))
+LB_NOINL void fp12_exp_x(fp12& r, const fp12& a) {
+  fp12 acc = a;
+  for (int i = 62; i >= 0; i--) {
+    fp12_sqr(acc, acc);
+    if ((LB_X_ABS >> i) & 1ull) fp12_mul(acc, acc, a);
+  }
+  fp12_conj(r, acc);
+}
+
+// f^(3 (p^12 - 1)/r)
+LB_NOINL void final_exp(fp12& r, const fp12& f) {
+  fp12 t0, t1, f2, a, b, c;
+  // easy part: f^(p^6 - 1) then ^(p^2 + 1)
+  fp12_conj(t0, f);
+  fp12_inv(t1, f);
+  fp12_mul(t0, t0, t1);
+  fp12_frob2(t1, t0);
+  fp12_mul(f2, t1, t0);
+  // a = f2^(x-1)
+  fp12_exp_x(t0, f2);
+  fp12_conj(t1, f2);
+  fp12_mul(a, t0, t1);
+  // a = a^(x-1)
+  fp12_exp_x(t0, a);
+  fp12_conj(t1, a);
+  fp12_mul(a, t0, t1);
+  // b = a^(x+p)
+  fp12_exp_x(t0, a);
+  fp12_frob1(t1, a);
+  fp12_mul(b, t0, t1);
+  // c = b^(x^2 + p^2 - 1)
+  fp12_exp_x(t0, b);
+  fp12_exp_x(t0, t0);
+  fp12_frob2(t1, b);
+  fp12_mul(c, t0, t1);
+  fp12_conj(t1, b);
+  fp12_mul(c, c, t1);
+  // r = c * f2^3
+  fp12_sqr(t0, f2);
+  fp12_mul(t0, t0, f2);
+  fp12_mul(r, c, t0);
+}
+
+}  // namespace lb

@@ -1,0 +1,301 @@
+"""ctypes binding of ``liblodestar_bls.so`` (the C ABI in include/lodestar_bls.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+GPU is visible, constructing :class:`Device` raises.  (The CPU checker lives in
+``oracle/`` and is only ever used by tests and the bench's cpu_baseline leg.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_LIB_NAME = "liblodestar_bls.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+LB_OK = 0
+LB_ERR_INVALID_ARGUMENT = -1
+LB_ERR_DEVICE = -2
+LB_ERR_NO_DEVICE = -3
+LB_ERR_OUT_OF_MEMORY = -4
+
+LB_REQ_OK = 0
+LB_REQ_EMPTY_AGGREGATE = 1
+LB_REQ_BAD_PUBKEY = 2
+
+SET_STATUS_NAMES = {0: "OK", 1: "BAD_ENCODING", 2: "NOT_ON_CURVE", 3: "NOT_IN_GROUP", 4: "PK_INFINITY",
+                    5: "EMPTY_AGGREGATE", 6: "ZERO_SIGNATURE"}
+
+# Every symbol include/lodestar_bls.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED_SYMBOLS = (
+    "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
+    "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
+    "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
+    "lb_last_stage_times",
+)
+
+
+class LodestarBlsError(RuntimeError):
+    pass
+
+
+class EmptyAggregateError(LodestarBlsError):
+    """Mirrors @chainsafe/bls EMPTY_AGGREGATE_ARRAY (a rejected job, not a false verdict)."""
+
+
+class BadPubkeyError(LodestarBlsError):
+    """Pubkey bytes PublicKey.fromBytes would throw on (worker.ts:110-116)."""
+
+
+def library_path() -> str:
+    return os.path.join(_HERE, _LIB_NAME)
+
+
+class _RequestBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_requests", ctypes.c_uint32),
+        ("n_sets", ctypes.c_uint32),
+        ("request_offsets", ctypes.c_void_p),
+        ("request_batchable", ctypes.c_void_p),
+        ("pubkeys", ctypes.c_void_p),
+        ("pk_offsets", ctypes.c_void_p),
+        ("messages", ctypes.c_void_p),
+        ("signatures", ctypes.c_void_p),
+        ("sig_offsets", ctypes.c_void_p),
+        ("seed", ctypes.c_void_p),
+    ]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("batch_retries", ctypes.c_uint32), ("batch_sigs_success", ctypes.c_uint32),
+                ("device_ms", ctypes.c_double)]
+
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load the HIP library (raises if it was not built -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not os.path.exists(path):
+        raise LodestarBlsError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    lib.lb_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.lb_destroy.argtypes = [vp]
+    lib.lb_last_error.argtypes = [vp]
+    lib.lb_last_error.restype = ctypes.c_char_p
+    lib.lb_device_count.argtypes = []
+    lib.lb_verify_requests.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
+    lib.lb_verify_requests_device.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
+    lib.lb_verify_same_message.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, ctypes.POINTER(u32)]
+    lib.lb_aggregate_pubkeys.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_aggregate_signatures.argtypes = [vp, u32, vp, vp, vp, ctypes.POINTER(ctypes.c_int32)]
+    lib.lb_hash_to_g2.argtypes = [vp, u32, vp, vp]
+    lib.lb_decode_signatures.argtypes = [vp, u32, vp, vp, vp, vp]
+    lib.lb_pairing.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_batch_scalars.argtypes = [vp, vp, u32, u32, vp]
+    lib.lb_g1_mul.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_g2_mul.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
+    for name in EXPORTED_SYMBOLS:
+        getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray]) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+def _u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def pack_blobs(items: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate variable-length byte strings -> (blob, offsets[n+1])."""
+    offs = np.zeros(len(items) + 1, dtype=np.uint32)
+    total = 0
+    for i, it in enumerate(items):
+        total += len(it)
+        offs[i + 1] = total
+    blob = np.frombuffer(b"".join(bytes(x) for x in items), dtype=np.uint8).copy() if total else np.zeros(1, np.uint8)
+    return blob, offs
+
+
+@dataclass
+class VerifyResult:
+    valid: np.ndarray          # uint8 per request
+    errors: np.ndarray         # uint8 per request (LB_REQ_*)
+    set_status: np.ndarray     # uint8 per set (LB_SET_*)
+    device_ms: float
+
+
+class Device:
+    """One lb_ctx bound to one GPU (one per process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.lb_create(device, ctypes.byref(h))
+        if rc != LB_OK:
+            raise LodestarBlsError(f"lb_create({device}) failed with {rc} (no GPU visible?)")
+        self._h = h
+        self.device = device
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            self.lib.lb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != LB_OK:
+            msg = self.lib.lb_last_error(self._h).decode(errors="replace")
+            raise LodestarBlsError(f"{what} failed ({rc}): {msg}")
+
+    # -- hot path ------------------------------------------------------------
+    def verify_requests(self, request_offsets: np.ndarray, pubkeys: np.ndarray, pk_offsets: Optional[np.ndarray],
+                        messages: np.ndarray, sig_blob: np.ndarray, sig_offsets: np.ndarray, seed: bytes,
+                        batchable: Optional[np.ndarray] = None) -> VerifyResult:
+        request_offsets = np.ascontiguousarray(request_offsets, dtype=np.uint32)
+        n_req = len(request_offsets) - 1
+        n_sets = int(request_offsets[-1]) if n_req >= 0 else 0
+        pubkeys = _u8(pubkeys) if pubkeys is not None and len(pubkeys) else np.zeros(1, np.uint8)
+        messages = _u8(messages) if len(messages) else np.zeros(1, np.uint8)
+        sig_blob = _u8(sig_blob) if len(sig_blob) else np.zeros(1, np.uint8)
+        sig_offsets = np.ascontiguousarray(sig_offsets, dtype=np.uint32)
+        pk_offsets = None if pk_offsets is None else np.ascontiguousarray(pk_offsets, dtype=np.uint32)
+        seed_a = _u8(seed)
+        assert len(seed_a) == 32
+        b = _RequestBatch(n_req, n_sets, _ptr(request_offsets), _ptr(batchable), _ptr(pubkeys), _ptr(pk_offsets),
+                          _ptr(messages), _ptr(sig_blob), _ptr(sig_offsets), _ptr(seed_a))
+        valid = np.zeros(max(n_req, 1), np.uint8)
+        err = np.zeros(max(n_req, 1), np.uint8)
+        sst = np.zeros(max(n_sets, 1), np.uint8)
+        st = _Stats()
+        rc = self.lib.lb_verify_requests(self._h, ctypes.byref(b), _ptr(valid), _ptr(err), _ptr(sst), ctypes.byref(st))
+        self._check(rc, "lb_verify_requests")
+        return VerifyResult(valid[:n_req], err[:n_req], sst[:n_sets], st.device_ms)
+
+    def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
+                               d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,
+                               d_set_status: Optional[int] = None) -> float:
+        """All arguments are device pointers (ints).  Returns device_ms."""
+        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed)
+        st = _Stats()
+        rc = self.lib.lb_verify_requests_device(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
+                                                ctypes.byref(st))
+        self._check(rc, "lb_verify_requests_device")
+        return st.device_ms
+
+    def verify_same_message(self, pubkeys: Sequence[bytes], signatures: Sequence[bytes], message: bytes,
+                            seed: bytes) -> Tuple[List[bool], bool]:
+        n = len(pubkeys)
+        if n == 0:
+            return [], False
+        pk = _u8(b"".join(pubkeys))
+        blob, offs = pack_blobs(signatures)
+        msg = _u8(message)
+        sd = _u8(seed)
+        out = np.zeros(n, np.uint8)
+        fast = ctypes.c_uint32(0)
+        rc = self.lib.lb_verify_same_message(self._h, n, _ptr(pk), _ptr(blob), _ptr(offs), _ptr(msg), _ptr(sd),
+                                             _ptr(out), ctypes.byref(fast))
+        self._check(rc, "lb_verify_same_message")
+        return [bool(x) for x in out], bool(fast.value)
+
+    def aggregate_pubkeys(self, pubkeys: Sequence[bytes]) -> bytes:
+        if len(pubkeys) == 0:
+            raise EmptyAggregateError("EMPTY_AGGREGATE_ARRAY")
+        pk = _u8(b"".join(pubkeys))
+        out = np.zeros(96, np.uint8)
+        st = np.zeros(1, np.uint8)
+        rc = self.lib.lb_aggregate_pubkeys(self._h, len(pubkeys), _ptr(pk), _ptr(out), _ptr(st))
+        self._check(rc, "lb_aggregate_pubkeys")
+        if st[0] != 0:
+            raise BadPubkeyError(SET_STATUS_NAMES.get(int(st[0]), str(st[0])))
+        return out.tobytes()
+
+    def aggregate_signatures(self, signatures: Sequence[bytes]) -> Tuple[bytes, int]:
+        if len(signatures) == 0:
+            raise EmptyAggregateError("EMPTY_AGGREGATE_ARRAY")
+        blob, offs = pack_blobs(signatures)
+        out = np.zeros(192, np.uint8)
+        bad = ctypes.c_int32(-1)
+        rc = self.lib.lb_aggregate_signatures(self._h, len(signatures), _ptr(blob), _ptr(offs), _ptr(out),
+                                              ctypes.byref(bad))
+        self._check(rc, "lb_aggregate_signatures")
+        return out.tobytes(), int(bad.value)
+
+    # -- stage-level entry points (parity tests) ---------------------------------
+    def hash_to_g2(self, messages: Sequence[bytes]) -> List[bytes]:
+        n = len(messages)
+        m = _u8(b"".join(messages))
+        out = np.zeros(max(n, 1) * 192, np.uint8)
+        self._check(self.lib.lb_hash_to_g2(self._h, n, _ptr(m), _ptr(out)), "lb_hash_to_g2")
+        return [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
+
+    def decode_signatures(self, signatures: Sequence[bytes]) -> Tuple[List[int], List[bytes]]:
+        n = len(signatures)
+        blob, offs = pack_blobs(signatures)
+        st = np.zeros(max(n, 1), np.uint8)
+        out = np.zeros(max(n, 1) * 192, np.uint8)
+        self._check(self.lib.lb_decode_signatures(self._h, n, _ptr(blob), _ptr(offs), _ptr(st), _ptr(out)),
+                    "lb_decode_signatures")
+        return [int(x) for x in st[:n]], [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
+
+    def pairing(self, g1s: Sequence[bytes], g2s: Sequence[bytes]) -> List[bytes]:
+        n = len(g1s)
+        a = _u8(b"".join(g1s))
+        b = _u8(b"".join(g2s))
+        out = np.zeros(max(n, 1) * 576, np.uint8)
+        self._check(self.lib.lb_pairing(self._h, n, _ptr(a), _ptr(b), _ptr(out)), "lb_pairing")
+        return [out[i * 576:(i + 1) * 576].tobytes() for i in range(n)]
+
+    def batch_scalars(self, seed: bytes, first: int, n: int) -> List[int]:
+        sd = _u8(seed)
+        out = np.zeros(max(n, 1), np.uint64)
+        self._check(self.lib.lb_batch_scalars(self._h, _ptr(sd), first, n, _ptr(out)), "lb_batch_scalars")
+        return [int(x) for x in out[:n]]
+
+    def g1_mul(self, pts: Sequence[bytes], ks: Sequence[int]) -> List[bytes]:
+        n = len(pts)
+        a = _u8(b"".join(pts))
+        k = np.array(ks, dtype=np.uint64)
+        out = np.zeros(max(n, 1) * 96, np.uint8)
+        self._check(self.lib.lb_g1_mul(self._h, n, _ptr(a), _ptr(k), _ptr(out)), "lb_g1_mul")
+        return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
+
+    def g2_mul(self, pts: Sequence[bytes], ks: Sequence[int]) -> List[bytes]:
+        n = len(pts)
+        a = _u8(b"".join(pts))
+        k = np.array(ks, dtype=np.uint64)
+        out = np.zeros(max(n, 1) * 192, np.uint8)
+        self._check(self.lib.lb_g2_mul(self._h, n, _ptr(a), _ptr(k), _ptr(out)), "lb_g2_mul")
+        return [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
+
+    def last_stage_times(self) -> List[Tuple[str, float]]:
+        ms = (ctypes.c_float * 16)()
+        names = (ctypes.c_char_p * 16)()
+        n = self.lib.lb_last_stage_times(self._h, ms, names, 16)
+        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 16))]
+
+
+def device_count() -> int:
+    return int(load_library().lb_device_count())
