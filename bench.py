@@ -1,0 +1,235 @@
+"""Benchmark: verified BLS signature sets/sec on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], the single-GPU config the metric is quoted
+on): 65,536 distinct-message single-pubkey attestation sets per GPU, submitted
+as 512 requests x 128 sets (MAX_SIGNATURE_SETS_PER_JOB, packages/beacon-node/
+src/chain/bls/multithread/index.ts:57), each request verified with
+verifySignatureSetsMaybeBatch semantics.  A "step" = one lb_verify_requests
+call over the whole 65,536-set batch with inputs already resident in HBM.
+Synthetic data: interop secret keys (packages/state-transition/src/util/
+interop.ts:19-23), messages sha256(seed || LE64(i)), signatures from the GPU
+signer (parity-checked against the oracle by tests and smoke()).
+
+Multi-GPU: each rank verifies its own 65,536 sets (weak scaling; sets are
+independent, no data-path collective).  value = total sets over all ranks /
+max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+# Roofline peak: v_mad_u64_u32 is quarter-rate on gfx950 (measured 30.5 of 32
+# per clk per CU, tools/microbench/mad_rate.hip); chip = 256 CU x 4 SIMD x 32
+# lanes / 4 x 2.4 GHz (MI355X_MICROARCH.md chip table).
+PEAK_MAD_PER_S = 256 * 4 * 32 / 4 * 2.4e9
+
+
+def interop_sk_be(i: int) -> bytes:
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return (int.from_bytes(d, "little") % R_ORDER).to_bytes(32, "big")
+
+
+def make_workload(dev, n_sets: int, first_index: int, seed: bytes):
+    sks = [interop_sk_be(first_index + i) for i in range(n_sets)]
+    msgs = [hashlib.sha256(seed + (first_index + i).to_bytes(8, "little")).digest() for i in range(n_sets)]
+    pks, sigs = [], []
+    chunk = 16384
+    for s in range(0, n_sets, chunk):
+        pks += dev.sk_to_pk(sks[s:s + chunk])
+        sigs += dev.sign(sks[s:s + chunk], msgs[s:s + chunk])
+    return sks, pks, msgs, sigs
+
+
+def cpu_baseline_oracle(pks, msgs, sigs, seconds: float, workers: int):
+    """Time the CPU oracle (pure-Python port) verifying 16-set batches of the
+    same workload for ~`seconds` of wall time on `workers` processes."""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    batches = [(pks[i:i + 16], msgs[i:i + 16], sigs[i:i + 16]) for i in range(0, min(len(pks), 16 * workers * 4), 16)]
+    deadline = time.time() + seconds
+    done = 0
+    t0 = time.time()
+    with ctx.Pool(workers) as pool:
+        pending = []
+        bi = 0
+        while time.time() < deadline or pending:
+            while len(pending) < workers and time.time() < deadline:
+                pending.append(pool.apply_async(_oracle_verify_batch, (batches[bi % len(batches)],)))
+                bi += 1
+            still = []
+            for p in pending:
+                if p.ready():
+                    ok = p.get()
+                    assert ok, "CPU oracle rejected a valid batch"
+                    done += 16
+                else:
+                    still.append(p)
+            pending = still
+            time.sleep(0.01)
+    el = time.time() - t0
+    return done / el, done, el
+
+
+def _oracle_verify_batch(batch):
+    from oracle import batch as OB
+    pks, msgs, sigs = batch
+    return OB.verify_signature_sets_maybe_batch(list(zip(pks, msgs, sigs)), seed=bytes(32))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sets", type=int, default=65536)
+    ap.add_argument("--per-request", type=int, default=128)
+    ap.add_argument("--latency-reps", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    from lodestar_amd.native import Device
+    dev = Device(local)
+
+    n = a.sets
+    seed = hashlib.sha256(b"lodestar-mi355x-bench").digest()
+    t_gen = time.time()
+    sks, pks, msgs, sigs = make_workload(dev, n, rank * n, seed)
+    t_gen = time.time() - t_gen
+
+    cuda = torch.device("cuda", local)
+    d_pk = torch.from_numpy(np.frombuffer(b"".join(pks), np.uint8).copy()).to(cuda)
+    d_msg = torch.from_numpy(np.frombuffer(b"".join(msgs), np.uint8).copy()).to(cuda)
+    d_sig = torch.from_numpy(np.frombuffer(b"".join(sigs), np.uint8).copy()).to(cuda)
+    sig_off = np.arange(0, 96 * (n + 1), 96, dtype=np.uint32)
+    req_off = np.arange(0, n + 1, a.per_request, dtype=np.uint32)
+    if req_off[-1] != n:
+        req_off = np.append(req_off, np.uint32(n))
+    n_req = len(req_off) - 1
+    d_sigoff = torch.from_numpy(sig_off.view(np.int32)).to(cuda)
+    d_reqoff = torch.from_numpy(req_off.view(np.int32)).to(cuda)
+    d_seed = torch.from_numpy(np.frombuffer(hashlib.sha256(b"batch-rand").digest(), np.uint8).copy()).to(cuda)
+    d_valid = torch.zeros(n_req, dtype=torch.uint8, device=cuda)
+    d_err = torch.zeros(n_req, dtype=torch.uint8, device=cuda)
+    torch.cuda.synchronize()
+
+    def step(nr=n_req, ns=n):
+        dev.verify_requests_device(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
+                                   d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(), d_valid.data_ptr(),
+                                   d_err.data_ptr())
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stage_acc = {}
+    for _ in range(a.steps):
+        step()
+        for name, ms in dev.last_stage_times():
+            stage_acc[name] = stage_acc.get(name, 0.0) + ms
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = bool(d_valid.cpu().numpy().all()) and not bool(d_err.cpu().numpy().any())
+
+    # p50 latency of one 128-set batch (one request)
+    lat = []
+    if a.latency_reps > 0:
+        step(1, a.per_request)
+        for _ in range(a.latency_reps):
+            t1 = time.perf_counter()
+            step(1, a.per_request)
+            lat.append((time.perf_counter() - t1) * 1e3)
+    p50 = float(np.median(lat)) if lat else None
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+        return
+    total_sets = n * world * a.steps
+    value = total_sets / elapsed
+    stage_ms = {k: v / a.steps for k, v in stage_acc.items()}
+    # roofline over the dominant kernel
+    roof = None
+    counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
+    dom = max((k for k in stage_ms if k not in ("start", "h2d", "d2h")), key=lambda k: stage_ms[k])
+    if os.path.exists(counts_path):
+        oc = json.load(open(counts_path))
+        st = oc["stages"].get(dom)
+        if st:
+            mads = st["fp_mul_per_set"] * n * oc["mads_per_fp_mul"]
+            achieved = mads / (stage_ms[dom] * 1e-3) / 1e12
+            peak = PEAK_MAD_PER_S / 1e12
+            traffic = None
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_path):
+                traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+            roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
+                    "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
+                    "algorithmic_mads_per_launch": mads}
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        workers = max(1, min(16, (os.cpu_count() or 2) - 1))
+        rate, done, el = cpu_baseline_oracle(pks, msgs, sigs, a.cpu_seconds, workers)
+        cpu = {"value": round(rate, 3), "unit": "sets/s", "cores": workers, "kind": "port",
+               "sample": f"{done} sets of the same workload in 16-set batches (pure-Python oracle, "
+                         f"{workers} processes, {el:.1f} s)"}
+    out = {
+        "metric": "verified signature sets/sec",
+        "value": round(value, 2),
+        "unit": "sets/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (interop keys, sha256 messages, GPU-signed)",
+        "config": {"workload": f"C2: {n} distinct-message single-pubkey sets per GPU, {n_req} requests x "
+                               f"{a.per_request} sets, verifySignatureSetsMaybeBatch semantics",
+                   "sets_per_gpu": n, "sets_per_request": a.per_request, "parallelism": f"shard{world}"},
+        "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
+        "all_valid": ok,
+        "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "datagen_s": round(t_gen, 2),
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -166,6 +166,14 @@ int lb_batch_scalars(lb_ctx* ctx, const uint8_t* seed, uint32_t first, uint32_t 
 int lb_g1_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint64_t* k, uint8_t* out96);
 int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* k, uint8_t* out192);
 
+/* ---- synthetic data generation (bench / tests) ---------------------------- */
+/* SecretKey.fromBytes(sk).toPublicKey().toBytes(uncompressed) and
+ * SecretKey.sign(msg).toBytes() (compressed), as the reference's own perf/unit
+ * tests build their inputs (test/perf/bls/bls.test.ts:19-40).  sk32 = 32-byte
+ * big-endian secret keys (< r). */
+int lb_sk_to_pk(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, uint8_t* out96);
+int lb_sign(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, const uint8_t* messages, uint8_t* out96);
+
 /* ---- profiling ----------------------------------------------------------- */
 /* Per-stage device time (ms) of the last lb_verify_* call, measured with HIP
  * events on the context's stream.  Writes up to max_stages values and their

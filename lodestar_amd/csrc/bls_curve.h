@@ -260,6 +260,18 @@ LB_DEV void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
   r = acc;
 }
 
+// [k]P for a 32-byte big-endian scalar (secret keys: SecretKey.fromBytes is BE)
+template <class F>
+LB_DEV void jac_mul_be32(jac<F>& r, const jac<F>& p, const uint8_t k[32]) {
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (int i = 0; i < 256; i++) {
+    jac_dbl(acc, acc);
+    if ((k[i >> 3] >> (7 - (i & 7))) & 1) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+
 // [|x|]P for the BLS parameter |x| = 0xd201000000010000 (fixed bit pattern:
 // 63 doublings, 5 additions; the branch is wave-uniform).
 template <class F>

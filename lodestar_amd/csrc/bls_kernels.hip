@@ -339,6 +339,48 @@ __global__ void k_g2_mul(uint32_t n, const uint8_t* __restrict__ in, const uint6
   g2_serialize(out + (size_t)i * 192, a);
 }
 
+// ---- synthetic data generation (bench / tests): SecretKey.toPublicKey, sign --
+__global__ void __launch_bounds__(TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32,
+                                                  uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t k[32];
+  for (int b = 0; b < 32; b++) k[b] = sk32[(size_t)i * 32 + b];
+  g1j g, r;
+  fp_set(g.X, LB_G1_X);
+  fp_set(g.Y, LB_G1_Y);
+  fp_one(g.Z);
+  jac_mul_be32(r, g, k);
+  g1a a;
+  jac_to_aff(a, r);
+  g1_serialize(out96 + (size_t)i * 96, a);
+}
+__global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sk32,
+                                              const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t k[32], m[32];
+  for (int b = 0; b < 32; b++) {
+    k[b] = sk32[(size_t)i * 32 + b];
+    m[b] = msgs[(size_t)i * 32 + b];
+  }
+  g2j h, r;
+  hash_to_g2(h, m);
+  jac_mul_be32(r, h, k);
+  g2a a;
+  jac_to_aff(a, r);
+  g2_compress(out96 + (size_t)i * 96, a);
+}
+
+#ifdef LB_COUNT_OPS
+static unsigned long long opcount_read_reset() {
+  unsigned long long v = 0, z = 0;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_lb_fpmul_count), sizeof(v));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lb_fpmul_count), &z, sizeof(z));
+  return v;
+}
+#endif
+
 // ============================================================================
 // Host side: context, workspace, C ABI
 // ============================================================================
@@ -355,6 +397,7 @@ struct lb_ctx {
   const char* ev_name[kMaxEv] = {};
   int n_ev = 0;
   float stage_ms[kMaxEv] = {};
+  unsigned long long stage_ops[kMaxEv] = {};
   const char* stage_name[kMaxEv] = {};
   int n_stages = 0;
 };
@@ -421,6 +464,10 @@ int ensure_pin(lb_ctx* ctx, size_t bytes) {
 
 int mark(lb_ctx* ctx, const char* name) {
   if (ctx->n_ev >= lb_ctx::kMaxEv) return LB_OK;
+#ifdef LB_COUNT_OPS
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->stage_ops[ctx->n_ev] = opcount_read_reset();
+#endif
   LB_HIP(hipEventRecord(ctx->ev[ctx->n_ev], ctx->stream));
   ctx->ev_name[ctx->n_ev] = name;
   ctx->n_ev++;
@@ -557,6 +604,16 @@ int lb_destroy(lb_ctx* ctx) {
 }
 
 const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+#ifdef LB_COUNT_OPS
+// Fp products executed per stage of the last lb_verify_* call (count build only)
+int lb_opcount_stages(const lb_ctx* ctx, unsigned long long* out, int max_stages) {
+  if (!ctx) return 0;
+  int n = 0;
+  for (int i = 1; i < ctx->n_ev && n < max_stages; i++) out[n++] = ctx->stage_ops[i];
+  return n;
+}
+#endif
 
 int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names, int max_stages) {
   if (!ctx) return 0;
@@ -936,6 +993,37 @@ int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* k, 
   uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
   LB_LAUNCH(k_g2_mul, blocks_for(n), TPB, n, (const uint8_t*)d_in, (const uint64_t*)d_k, d_out);
   LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_sk_to_pk(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, uint8_t* out96) {
+  if (!ctx || (n && (!sk32 || !out96))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (32 + 96) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void* d_k;
+  LB_TRY(upload(ctx, ws, sk32, (size_t)n * 32, &d_k));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
+  LB_LAUNCH(k_sk_to_pk, blocks_for(n), TPB, n, (const uint8_t*)d_k, d_out);
+  LB_HIP(hipMemcpyAsync(out96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_sign(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, const uint8_t* messages, uint8_t* out96) {
+  if (!ctx || (n && (!sk32 || !messages || !out96))) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (32 + 32 + 96) + 8192));
+  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  void *d_k, *d_m;
+  LB_TRY(upload(ctx, ws, sk32, (size_t)n * 32, &d_k));
+  LB_TRY(upload(ctx, ws, messages, (size_t)n * 32, &d_m));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
+  LB_LAUNCH(k_sign, blocks_for(n), TPB, n, (const uint8_t*)d_k, (const uint8_t*)d_m, d_out);
+  LB_HIP(hipMemcpyAsync(out96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, ctx->stream));
   LB_HIP(hipStreamSynchronize(ctx->stream));
   return LB_OK;
 }

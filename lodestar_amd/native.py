@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
     "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
-    "lb_last_stage_times",
+    "lb_last_stage_times", "lb_sk_to_pk", "lb_sign",
 )
 
 
@@ -104,6 +104,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_batch_scalars.argtypes = [vp, vp, u32, u32, vp]
     lib.lb_g1_mul.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_g2_mul.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
+    lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
     for name in EXPORTED_SYMBOLS:
         getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int
@@ -289,6 +291,21 @@ class Device:
         out = np.zeros(max(n, 1) * 192, np.uint8)
         self._check(self.lib.lb_g2_mul(self._h, n, _ptr(a), _ptr(k), _ptr(out)), "lb_g2_mul")
         return [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
+
+    def sk_to_pk(self, sks_be32: Sequence[bytes]) -> List[bytes]:
+        n = len(sks_be32)
+        k = _u8(b"".join(sks_be32))
+        out = np.zeros(max(n, 1) * 96, np.uint8)
+        self._check(self.lib.lb_sk_to_pk(self._h, n, _ptr(k), _ptr(out)), "lb_sk_to_pk")
+        return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
+
+    def sign(self, sks_be32: Sequence[bytes], messages: Sequence[bytes]) -> List[bytes]:
+        n = len(sks_be32)
+        k = _u8(b"".join(sks_be32))
+        m = _u8(b"".join(messages))
+        out = np.zeros(max(n, 1) * 96, np.uint8)
+        self._check(self.lib.lb_sign(self._h, n, _ptr(k), _ptr(m), _ptr(out)), "lb_sign")
+        return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
 
     def last_stage_times(self) -> List[Tuple[str, float]]:
         ms = (ctypes.c_float * 16)()

@@ -1,0 +1,249 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle's golden
+fixtures and the reference's own KATs.  Bit-exact for every byte/integer output.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from lodestar_amd.native import pack_blobs
+from oracle import batch as OB
+from oracle import bls12_381 as O
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_golden("kats.json")
+VEC = load_golden("vectors.json")
+R_ORDER = O.R
+
+
+def interop_sk_be(i):
+    return O.interop_secret_key(i).to_bytes(32, "big")
+
+
+def run_requests(dev, requests, seed=bytes(32)):
+    """requests: [[{"pks": [hex], "msg": hex, "sig": hex}, ...], ...] -> VerifyResult"""
+    pks, pk_off, msgs, sigs, req_off = [], [0], [], [], [0]
+    for req in requests:
+        for st in req:
+            pks += [bytes.fromhex(p) for p in st["pks"]]
+            pk_off.append(len(pks))
+            msgs.append(bytes.fromhex(st["msg"]))
+            sigs.append(bytes.fromhex(st["sig"]))
+        req_off.append(len(msgs))
+    blob, offs = pack_blobs(sigs)
+    return dev.verify_requests(np.array(req_off, np.uint32), np.frombuffer(b"".join(pks) or b"\0", np.uint8),
+                               np.array(pk_off, np.uint32), np.frombuffer(b"".join(msgs) or b"\0", np.uint8), blob,
+                               offs, seed)
+
+
+# ---- reference KATs --------------------------------------------------------------
+def test_sk_to_pk_interop_kat(device):
+    """GPU keygen reproduces all 100 interop pubkeys (interop-pubkeys.json)."""
+    out = device.sk_to_pk([interop_sk_be(i) for i in range(100)])
+    for i, unc in enumerate(out):
+        pt = O.g1_from_bytes(unc)
+        assert O.g1_to_bytes(pt).hex() == KATS["interop_pubkeys"][i], i
+
+
+def test_sign_deposit_kat(device):
+    """GPU hash_to_G2 + sign reproduce the interop deposit signature (genesisState.test.ts:51-55)."""
+    d = KATS["deposit"]
+    sig = device.sign([interop_sk_be(0)], [bytes.fromhex(d["signing_root"])])[0]
+    assert sig.hex() == d["signature"]
+
+
+def test_mainnet_signatures_decode(device):
+    sigs = [bytes.fromhex(s) for s in KATS["mainnet_signatures"]] + [bytes.fromhex(KATS["valid_g2_oppool"])]
+    st, dec = device.decode_signatures(sigs)
+    assert st == [0] * len(sigs)
+    for s, d in zip(sigs, dec):
+        assert O.g2_to_bytes(O.g2_from_bytes(d)) == s
+
+
+def test_negative_kats_decode(device):
+    st, _ = device.decode_signatures([bytes.fromhex(h) for h in KATS["malformed_signatures"]])
+    assert st == [1, 1]
+
+
+# ---- stage vectors (golden, oracle-generated) ------------------------------------------
+def test_hash_to_g2_golden(device):
+    out = device.hash_to_g2([bytes.fromhex(v["msg"]) for v in VEC["hash_to_g2"]])
+    assert [o.hex() for o in out] == [v["point"] for v in VEC["hash_to_g2"]]
+
+
+def test_signature_decode_golden(device):
+    cases = VEC["sig_decode"]
+    st, dec = device.decode_signatures([bytes.fromhex(c["bytes"]) for c in cases])
+    for c, s, d in zip(cases, st, dec):
+        assert s == c["status"], c["name"]
+        if c["point"] is not None:
+            assert d.hex() == c["point"], c["name"]
+
+
+def test_pairing_golden(device):
+    cases = VEC["pairing"]
+    out = device.pairing([bytes.fromhex(c["g1"]) for c in cases], [bytes.fromhex(c["g2"]) for c in cases])
+    assert [o.hex() for o in out] == [c["gt"] for c in cases]
+
+
+def test_scalar_mul_golden(device):
+    g1 = VEC["g1_mul"]
+    out = device.g1_mul([bytes.fromhex(c["p"]) for c in g1], [int(c["k"]) for c in g1])
+    assert [o.hex() for o in out] == [c["out"] for c in g1]
+    g2 = VEC["g2_mul"]
+    out = device.g2_mul([bytes.fromhex(c["p"]) for c in g2], [int(c["k"]) for c in g2])
+    assert [o.hex() for o in out] == [c["out"] for c in g2]
+
+
+def test_batch_scalars_golden(device):
+    v = VEC["batch_scalars"]
+    out = device.batch_scalars(bytes.fromhex(v["seed"]), v["first"], len(v["values"]))
+    assert [str(x) for x in out] == v["values"]
+
+
+def test_aggregate_pubkeys_golden(device):
+    v = VEC["aggregate_pubkeys"]
+    assert device.aggregate_pubkeys([bytes.fromhex(p) for p in v["pubkeys"]]).hex() == v["out"]
+
+
+def test_aggregate_signatures_golden(device):
+    v = VEC["aggregate_signatures"]
+    out, bad = device.aggregate_signatures([bytes.fromhex(s) for s in v["signatures"]])
+    assert bad == -1 and out.hex() == v["out"]
+
+
+# ---- verdict scenarios (maybeBatch / worker semantics) -----------------------------------
+@pytest.mark.parametrize("idx", range(len(VEC["verify_requests"])))
+def test_verify_requests_scenarios(device, idx):
+    sc = VEC["verify_requests"][idx]
+    res = run_requests(device, sc["requests"])
+    errors = sc.get("errors", [0] * len(sc["expect"]))
+    assert list(res.errors) == errors, sc["name"]
+    for e, v, err in zip(sc["expect"], res.valid, errors):
+        if err == 0:
+            assert bool(v) == e, sc["name"]
+
+
+@pytest.mark.parametrize("idx", range(len(VEC["same_message"])))
+def test_same_message_scenarios(device, idx):
+    sc = VEC["same_message"][idx]
+    verdicts, fast = device.verify_same_message([bytes.fromhex(p) for p in sc["pubkeys"]],
+                                                [bytes.fromhex(s) for s in sc["signatures"]],
+                                                bytes.fromhex(sc["message"]), bytes(32))
+    assert verdicts == sc["expect"], sc["name"]
+    assert fast == sc["fast_path"], sc["name"]
+
+
+def test_same_message_empty(device):
+    assert device.verify_same_message([], [], bytes(32), bytes(32)) == ([], False)
+
+
+def test_aggregate_empty_rejects(device):
+    from lodestar_amd.native import EmptyAggregateError
+    with pytest.raises(EmptyAggregateError):
+        device.aggregate_pubkeys([])
+
+
+# ---- random cases vs the live oracle --------------------------------------------------
+def test_sign_matches_oracle_random(device):
+    rnd = random.Random(77)
+    sks = [rnd.randrange(1, R_ORDER) for _ in range(6)]
+    msgs = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(6)]
+    out = device.sign([k.to_bytes(32, "big") for k in sks], msgs)
+    for k, m, s in zip(sks, msgs, out):
+        assert s == O.g2_to_bytes(O.sign(k, m))
+
+
+def test_random_batches_vs_oracle(device):
+    """Random mixes of valid / wrong-message / malformed sets: verdicts equal oracle.batch."""
+    rnd = random.Random(1234)
+    n = 24
+    sks = [interop_sk_be(i) for i in range(n)]
+    pks = device.sk_to_pk(sks)
+    msgs = [hashlib.sha256(b"rb" + bytes([i])).digest() for i in range(n)]
+    sigs = device.sign(sks, msgs)
+    reqs, expect = [], []
+    i = 0
+    while i < n:
+        k = rnd.choice([1, 2, 3, 5])
+        req = []
+        for j in range(i, min(n, i + k)):
+            sig = sigs[j]
+            msg = msgs[j]
+            roll = rnd.random()
+            if roll < 0.15:
+                msg = hashlib.sha256(b"other" + bytes([j])).digest()
+            elif roll < 0.22:
+                sig = bytes([rnd.getrandbits(8) for _ in range(96)])
+            req.append({"pks": [pks[j].hex()], "msg": msg.hex(), "sig": sig.hex()})
+        reqs.append(req)
+        i += k
+    res = run_requests(device, reqs)
+    for req, v in zip(reqs, res.valid):
+        want = all(OB.individually_valid(bytes.fromhex(s["pks"][0]), bytes.fromhex(s["msg"]), bytes.fromhex(s["sig"]))
+                   for s in req) if req else False
+        assert bool(v) == want
+
+
+# ---- full-size properties (BASELINE.json config sizes) -----------------------------------
+def _gen(device, n, tag):
+    sks = [interop_sk_be(i) for i in range(n)]
+    msgs = [hashlib.sha256(tag + i.to_bytes(8, "little")).digest() for i in range(n)]
+    pks, sigs = [], []
+    for s in range(0, n, 8192):
+        pks += device.sk_to_pk(sks[s:s + 8192])
+        sigs += device.sign(sks[s:s + 8192], msgs[s:s + 8192])
+    return pks, msgs, sigs
+
+
+def test_c2_full_size_with_injected_invalids(device):
+    """65,536 sets (BASELINE configs[1]) in 512 requests of 128: all valid except the
+    requests holding injected invalid sets (wrong message / malformed)."""
+    n, per = 65536, 128
+    pks, msgs, sigs = _gen(device, n, b"c2")
+    rnd = random.Random(42)
+    bad = sorted(rnd.sample(range(n), 20))
+    msgs2, sigs2 = list(msgs), list(sigs)
+    for t, j in enumerate(bad):
+        if t % 2:
+            msgs2[j] = bytes(32)
+        else:
+            sigs2[j] = bytes([10]) * 96
+    blob, offs = pack_blobs(sigs2)
+    res = device.verify_requests(np.arange(0, n + 1, per, dtype=np.uint32), np.frombuffer(b"".join(pks), np.uint8),
+                                 None, np.frombuffer(b"".join(msgs2), np.uint8), blob, offs, bytes(32))
+    bad_req = {j // per for j in bad}
+    assert [k for k in range(n // per) if not res.valid[k]] == sorted(bad_req)
+    assert not res.errors.any()
+
+
+def test_c3_committee_aggregation_2048(device):
+    """2048-pubkey aggregation -> 96-byte uncompressed, bit-exact vs the oracle (config C3)."""
+    n = 2048
+    sks = [interop_sk_be(i) for i in range(n)]
+    pks = device.sk_to_pk(sks)
+    got = device.aggregate_pubkeys(pks)
+    ssum = sum(O.interop_secret_key(i) for i in range(n)) % R_ORDER
+    assert got == O.g1_to_bytes(O.sk_to_pk(ssum), compressed=False)
+
+
+def test_c3_sync_aggregate_512(device):
+    """512-key same-message sync aggregate: aggregate set verifies; one wrong key fails."""
+    n = 512
+    sks = [interop_sk_be(i) for i in range(n)]
+    pks = device.sk_to_pk(sks)
+    msg = hashlib.sha256(b"sync").digest()
+    sigs = device.sign(sks, [msg] * n)
+    agg_sig, bad = device.aggregate_signatures(sigs)
+    assert bad == -1
+    blob, offs = pack_blobs([agg_sig, agg_sig])
+    pk_all = b"".join(pks) + b"".join(pks[:-1]) + pks[0]
+    res = device.verify_requests(np.array([0, 1, 2], np.uint32), np.frombuffer(pk_all, np.uint8),
+                                 np.array([0, n, 2 * n], np.uint32), np.frombuffer(msg * 2, np.uint8), blob, offs,
+                                 bytes(32))
+    assert list(res.valid) == [1, 0]

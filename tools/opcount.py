@@ -1,0 +1,72 @@
+"""Count Fp products per pipeline stage (the roofline's algorithmic-op figure).
+
+Build (CPU container):  python tools/opcount.py --build
+Run (GPU box):          python tools/opcount.py --run  -> profiles/op_counts.json
+
+Uses a separate build of the same sources with -DLB_COUNT_OPS (every fp_mul /
+fp_sqr does one device atomicAdd).  The counts are exact for the data used:
+the only data-dependent branches are the 64-bit scalar bits (add or not) and
+the SSWU square/non-square path, both averaged over 256 random sets.
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT_DIR = os.path.join(ROOT, "tools", "opcount_build")
+MADS_PER_FPMUL = 288  # 12x12 limb products + 12x12 reduction products (CIOS, 32-bit limbs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--run", action="store_true")
+    ap.add_argument("--sets", type=int, default=256)
+    ap.add_argument("--per-request", type=int, default=128)
+    a = ap.parse_args()
+    from lodestar_amd import build as b
+    if a.build:
+        print(b.build_opcount(OUT_DIR))
+    if not a.run:
+        return
+    import numpy as np
+    from lodestar_amd import native
+    native.library_path = lambda: os.path.join(OUT_DIR, "liblodestar_bls_count.so")
+    native._lib = None
+    lib = native.load_library()
+    lib.lb_opcount_stages.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    dev = native.Device(0)
+    n = a.sets
+    r_order = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    sks = [(int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % r_order).to_bytes(32, "big")
+           for i in range(n)]
+    msgs = [hashlib.sha256(b"opcount" + i.to_bytes(8, "little")).digest() for i in range(n)]
+    pks = dev.sk_to_pk(sks)
+    sigs = dev.sign(sks, msgs)
+    blob, offs = native.pack_blobs(sigs)
+    req = np.arange(0, n + 1, a.per_request, dtype=np.uint32)
+    res = dev.verify_requests(req, np.frombuffer(b"".join(pks), np.uint8), None, np.frombuffer(b"".join(msgs), np.uint8),
+                              blob, offs, bytes(32))
+    assert res.valid.all(), res.valid
+    names = [nm for nm, _ in dev.last_stage_times()]
+    buf = (ctypes.c_ulonglong * 16)()
+    k = lib.lb_opcount_stages(dev._h, buf, 16)
+    n_req = len(req) - 1
+    per = {}
+    for i in range(k):
+        per[names[i]] = {"fp_mul_total": int(buf[i]), "fp_mul_per_set": buf[i] / n}
+    total = sum(int(buf[i]) for i in range(k))
+    out = {"sets": n, "requests": n_req, "sets_per_request": a.per_request, "mads_per_fp_mul": MADS_PER_FPMUL,
+           "stages": per, "fp_mul_per_set_total": total / n, "mads_per_set_total": total / n * MADS_PER_FPMUL}
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "op_counts.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
