@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--latency-reps", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("LB_SLOTS", "3")),
+                    help="calls kept in flight (= library slots, env LB_SLOTS)")
     a = ap.parse_args()
 
     import torch
@@ -131,26 +134,50 @@ def main():
     d_sigoff = torch.from_numpy(sig_off.view(np.int32)).to(cuda)
     d_reqoff = torch.from_numpy(req_off.view(np.int32)).to(cuda)
     d_seed = torch.from_numpy(np.frombuffer(hashlib.sha256(b"batch-rand").digest(), np.uint8).copy()).to(cuda)
-    d_valid = torch.zeros(n_req, dtype=torch.uint8, device=cuda)
-    d_err = torch.zeros(n_req, dtype=torch.uint8, device=cuda)
+    # one output buffer per in-flight call (the library keeps one call per slot)
+    nbuf = max(1, a.inflight)
+    d_valid = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
+    d_err = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
     torch.cuda.synchronize()
 
-    def step(nr=n_req, ns=n):
-        dev.verify_requests_device(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
-                                   d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(), d_valid.data_ptr(),
-                                   d_err.data_ptr())
+    def submit(k, nr=n_req, ns=n):
+        return dev.verify_requests_device_async(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
+                                                d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
+                                                d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
 
-    for _ in range(a.warmup):
-        step()
+    def step(k=0, nr=n_req, ns=n):
+        # synchronous call (library slot 0: two-stream DAG, lowest latency)
+        dev.verify_requests_device(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
+                                   d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
+                                   d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
+
+    for k in range(a.warmup):
+        step(k)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stage_acc = {}
-    for _ in range(a.steps):
-        step()
+    n_acc = [0]
+
+    def accumulate():
+        n_acc[0] += 1
         for name, ms in dev.last_stage_times():
             stage_acc[name] = stage_acc.get(name, 0.0) + ms
+
+    pending = []
+    for k in range(a.steps):
+        if a.sync:
+            step(k)
+            accumulate()
+        else:
+            pending.append(submit(k))
+            if len(pending) >= nbuf:
+                dev.wait(pending.pop(0))
+                accumulate()
+    for t in pending:
+        dev.wait(t)
+        accumulate()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,15 +186,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ok = bool(d_valid.cpu().numpy().all()) and not bool(d_err.cpu().numpy().any())
+    ok = all(bool(v.cpu().numpy().all()) for v in d_valid) and not any(bool(e.cpu().numpy().any()) for e in d_err)
 
     # p50 latency of one 128-set batch (one request)
     lat = []
     if a.latency_reps > 0:
-        step(1, a.per_request)
+        step(0, 1, a.per_request)
         for _ in range(a.latency_reps):
             t1 = time.perf_counter()
-            step(1, a.per_request)
+            step(0, 1, a.per_request)
             lat.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.median(lat)) if lat else None
 
@@ -177,7 +204,7 @@ def main():
         return
     total_sets = n * world * a.steps
     value = total_sets / elapsed
-    stage_ms = {k: v / a.steps for k, v in stage_acc.items()}
+    stage_ms = {k: v / max(n_acc[0], 1) for k, v in stage_acc.items()}
     # roofline over the dominant kernel
     roof = None
     counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
@@ -221,6 +248,7 @@ def main():
                    "sets_per_gpu": n, "sets_per_request": a.per_request, "parallelism": f"shard{world}"},
         "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
         "all_valid": ok,
+        "overlap": "sync" if a.sync else f"{nbuf} calls in flight (lb_verify_requests_device_async)",
         "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
         "roofline": roof,
         "cpu_baseline": cpu,

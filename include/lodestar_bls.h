@@ -131,6 +131,18 @@ int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* batch, uint8_
                               uint8_t* d_out_request_error, uint8_t* d_out_set_status, lb_verify_stats* stats);
 
 /*
+ * Asynchronous device-resident variant: enqueue the call and return a ticket;
+ * lb_wait(ticket) blocks until it is complete.  Up to two calls are in flight
+ * per context (each on its own pair of HIP streams and workspace), so the
+ * tail of one call overlaps the per-set stages of the next -- the way the
+ * reference pool keeps several worker packages in flight (index.ts:362-519).
+ * Input and output buffers must stay valid until lb_wait returns.
+ */
+int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* d_out_request_valid,
+                                    uint8_t* d_out_request_error, uint8_t* d_out_set_status, uint64_t* out_ticket);
+int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats);
+
+/*
  * verifySignatureSetsSameMessage for one job (<= 128 sets in the reference,
  * any n here): out_valid[i] per set.  Fast path: every signature validates,
  * aggregate pubkeys and signatures (plain sums, as the reference does) and

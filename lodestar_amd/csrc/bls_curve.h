@@ -81,7 +81,7 @@ LB_DEV void jac_neg(jac<F>& r, const jac<F>& p) {
 
 // dbl-2009-l (a = 0): 2M + 5S.  Z3 = 2YZ, so 2-torsion and infinity map to Z3 = 0.
 template <class F>
-LB_DEV void jac_dbl(jac<F>& r, const jac<F>& p) {
+LB_DEV void jac_dbl_impl(jac<F>& r, const jac<F>& p) {
   F A, B, C, D, E, Fq, t;
   fsqr(A, p.X);
   fsqr(B, p.Y);
@@ -114,7 +114,7 @@ LB_DEV void jac_dbl(jac<F>& r, const jac<F>& p) {
 
 // add-2007-bl with the exceptional cases resolved (P == Q -> dbl, P == -Q -> O)
 template <class F>
-LB_DEV void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+LB_DEV void jac_add_impl(jac<F>& r, const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) {
     r = q;
     return;
@@ -167,7 +167,7 @@ LB_DEV void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
 
 // madd-2007-bl: p Jacobian + q affine
 template <class F>
-LB_DEV void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+LB_DEV void jac_add_aff_impl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (q.inf) {
     r = p;
     return;
@@ -213,6 +213,15 @@ LB_DEV void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   fsub(o.Z, t, HH);
   r = o;
 }
+
+// G1 point ops inline; G2 point ops out of line (an inlined Fp2 group law
+// pushes the per-set kernels to 512 VGPRs = one wave per SIMD).
+LB_DEV void jac_dbl(g1j& r, const g1j& p) { jac_dbl_impl(r, p); }
+LB_DEV void jac_add(g1j& r, const g1j& p, const g1j& q) { jac_add_impl(r, p, q); }
+LB_DEV void jac_add_aff(g1j& r, const g1j& p, const g1a& q) { jac_add_aff_impl(r, p, q); }
+LB_NOINL void jac_dbl(g2j& r, const g2j& p) { jac_dbl_impl(r, p); }
+LB_NOINL void jac_add(g2j& r, const g2j& p, const g2j& q) { jac_add_impl(r, p, q); }
+LB_NOINL void jac_add_aff(g2j& r, const g2j& p, const g2a& q) { jac_add_aff_impl(r, p, q); }
 
 template <class F>
 LB_DEV void jac_to_aff(aff<F>& r, const jac<F>& p) {

@@ -129,6 +129,63 @@ LB_DEV void fp_mul_body(fp& r, const fp& a, const fp& b) {
   for (int j = 0; j < 12; j++) r.l[j] = br ? t[j] : s[j];
 }
 
+// Montgomery squaring: 66 cross products (doubled) + 12 squares + one
+// 12x12 reduction = 222 v_mad_u64_u32 instead of 288.
+LB_DEV void fp_sqr_body(fp& r, const fp& a) {
+  uint32_t t[24];
+#pragma unroll
+  for (int j = 0; j < 24; j++) t[j] = 0;
+  // cross products a_i a_j, i < j
+#pragma unroll
+  for (int i = 0; i < 11; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 12; j++) {
+      c = (uint64_t)a.l[i] * a.l[j] + (uint64_t)t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    t[i + 12] = (uint32_t)(c >> 32);
+  }
+  // double
+  t[23] = t[22] >> 31;
+#pragma unroll
+  for (int j = 22; j > 0; j--) t[j] = (t[j] << 1) | (t[j - 1] >> 31);
+  t[0] <<= 1;
+  // + squares
+  {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint64_t sq = (uint64_t)a.l[i] * a.l[i];
+      c = (uint64_t)t[2 * i] + (uint32_t)sq + (c >> 32);
+      t[2 * i] = (uint32_t)c;
+      c = (uint64_t)t[2 * i + 1] + (uint32_t)(sq >> 32) + (c >> 32);
+      t[2 * i + 1] = (uint32_t)c;
+    }
+  }
+  // Montgomery reduction of the 768-bit t (t < p^2 < 2^762)
+  uint32_t carry_hi = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t m = t[i] * LB_P_INV32;
+    uint64_t c = (uint64_t)m * P_[0] + t[i];
+#pragma unroll
+    for (int j = 1; j < 12; j++) {
+      c = (uint64_t)m * P_[j] + (uint64_t)t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    c = (uint64_t)t[i + 12] + (c >> 32) + carry_hi;
+    t[i + 12] = (uint32_t)c;
+    carry_hi = (uint32_t)(c >> 32);
+  }
+  uint32_t s[12];
+  uint32_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) s[j] = __builtin_subc(t[12 + j], P_[j], br, &br);
+#pragma unroll
+  for (int j = 0; j < 12; j++) r.l[j] = br ? t[12 + j] : s[j];
+}
+
 #ifdef LB_COUNT_OPS
 __device__ unsigned long long g_lb_fpmul_count;
 #define LB_COUNT_MUL() atomicAdd(&g_lb_fpmul_count, 1ull)
@@ -136,14 +193,49 @@ __device__ unsigned long long g_lb_fpmul_count;
 #define LB_COUNT_MUL() ((void)0)
 #endif
 
-LB_NOINL void fp_mul(fp& r, const fp& a, const fp& b) {
+// Register calling convention: 24 scalar arguments in, a struct of 12 scalars
+// out.  (A byval/by-reference fp argument would be passed through scratch
+// memory by the AMDGPU ABI and expose its latency on every call.)
+struct fp_ret {
+  uint32_t v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11;
+};
+#define LB_FP_PARAMS(x)                                                                                   \
+  uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6, \
+      uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
+#define LB_FP_PACK(x) {{x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11}}
+#define LB_FP_ARGS(f) \
+  f.l[0], f.l[1], f.l[2], f.l[3], f.l[4], f.l[5], f.l[6], f.l[7], f.l[8], f.l[9], f.l[10], f.l[11]
+
+LB_NOINL fp_ret fp_mul_r(LB_FP_PARAMS(a), LB_FP_PARAMS(b)) {
   LB_COUNT_MUL();
-  fp_mul_body(r, a, b);
+  const fp A = LB_FP_PACK(a), B = LB_FP_PACK(b);
+  fp r;
+  fp_mul_body(r, A, B);
+  return fp_ret{r.l[0], r.l[1], r.l[2], r.l[3], r.l[4], r.l[5], r.l[6], r.l[7], r.l[8], r.l[9], r.l[10], r.l[11]};
 }
-LB_NOINL void fp_sqr(fp& r, const fp& a) {
+LB_NOINL fp_ret fp_sqr_r(LB_FP_PARAMS(a)) {
   LB_COUNT_MUL();
-  fp_mul_body(r, a, a);
+  const fp A = LB_FP_PACK(a);
+  fp r;
+  fp_sqr_body(r, A);
+  return fp_ret{r.l[0], r.l[1], r.l[2], r.l[3], r.l[4], r.l[5], r.l[6], r.l[7], r.l[8], r.l[9], r.l[10], r.l[11]};
 }
+LB_DEV void fp_unret(fp& r, const fp_ret& v) {
+  r.l[0] = v.v0;
+  r.l[1] = v.v1;
+  r.l[2] = v.v2;
+  r.l[3] = v.v3;
+  r.l[4] = v.v4;
+  r.l[5] = v.v5;
+  r.l[6] = v.v6;
+  r.l[7] = v.v7;
+  r.l[8] = v.v8;
+  r.l[9] = v.v9;
+  r.l[10] = v.v10;
+  r.l[11] = v.v11;
+}
+LB_DEV void fp_mul(fp& r, const fp& a, const fp& b) { fp_unret(r, fp_mul_r(LB_FP_ARGS(a), LB_FP_ARGS(b))); }
+LB_DEV void fp_sqr(fp& r, const fp& a) { fp_unret(r, fp_sqr_r(LB_FP_ARGS(a))); }
 
 LB_DEV void fp_mul_const(fp& r, const fp& a, const uint32_t* c) {
   fp k;
@@ -583,6 +675,52 @@ LB_NOINL void fp12_sqr(fp12& r, const fp12& a) {
   fp6_sub(r.c0, s, u);
   fp6_add(r.c1, t, t);
 }
+// Granger-Scott squaring for f in the cyclotomic subgroup (after the easy part
+// of the final exponentiation).  View Fp12 = Fp4[w]/(w^3 - s), Fp4 = Fp2[s]/(s^2 - xi):
+//   f = A + B w + C w^2,  A = (c0.c0, c1.c1), B = (c1.c0, c0.c2), C = (c0.c1, c1.c2)
+//   f^2 = (3A^2 - 2conj(A)) + (3 s C^2 + 2conj(B)) w + (3B^2 - 2conj(C)) w^2
+// 9 Fp2 squarings = 18 Fp products instead of 36.
+LB_DEV void fp4_sqr(fp2& rx, fp2& ry, const fp2& x, const fp2& y) {
+  fp2 t0, t1, t2;
+  fp2_sqr(t0, x);
+  fp2_sqr(t1, y);
+  fp2_add(t2, x, y);
+  fp2_sqr(t2, t2);
+  fp2_sub(t2, t2, t0);
+  fp2_sub(ry, t2, t1);
+  fp2_mul_xi(t1, t1);
+  fp2_add(rx, t0, t1);
+}
+// r = 3 a - 2 b   /   r = 3 a + 2 b
+LB_DEV void fp2_3a_m2b(fp2& r, const fp2& a, const fp2& b) {
+  fp2 t;
+  fp2_sub(t, a, b);
+  fp2_dbl(t, t);
+  fp2_add(r, t, a);
+}
+LB_DEV void fp2_3a_p2b(fp2& r, const fp2& a, const fp2& b) {
+  fp2 t;
+  fp2_add(t, a, b);
+  fp2_dbl(t, t);
+  fp2_add(r, t, a);
+}
+LB_NOINL void fp12_cyc_sqr(fp12& r, const fp12& f) {
+  fp2 Ax, Ay, Bx, By, Cx, Cy;
+  fp4_sqr(Ax, Ay, f.c0.c0, f.c1.c1);
+  fp4_sqr(Bx, By, f.c1.c0, f.c0.c2);
+  fp4_sqr(Cx, Cy, f.c0.c1, f.c1.c2);
+  fp12 o;
+  fp2_3a_m2b(o.c0.c0, Ax, f.c0.c0);
+  fp2_3a_p2b(o.c1.c1, Ay, f.c1.c1);
+  fp2 sCx;
+  fp2_mul_xi(sCx, Cy);  // s C^2 = xi Cy + Cx s
+  fp2_3a_p2b(o.c1.c0, sCx, f.c1.c0);
+  fp2_3a_m2b(o.c0.c2, Cx, f.c0.c2);
+  fp2_3a_m2b(o.c0.c1, Bx, f.c0.c1);
+  fp2_3a_p2b(o.c1.c2, By, f.c1.c2);
+  r = o;
+}
+
 // f * l, l = (l0 + l1 v) + (l4 v) w  (the Miller-loop line shape): 13 Fp2 products
 LB_NOINL void fp12_mul_line(fp12& r, const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
   fp6 t0, t1, s;

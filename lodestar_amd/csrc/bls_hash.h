@@ -282,6 +282,25 @@ LB_DEV void clear_cofactor_g2(g2j& r, const g2j& p) {
   jac_add(r, t3, n);
 }
 
+// One half of hash_to_curve: u_j = hash_to_field(msg)[j] -> SSWU -> iso (Jacobian).
+// Two lanes per message run j = 0, 1 concurrently (the halves are independent).
+LB_DEV void hash_to_g2_half(g2j& r, const uint8_t msg[32], int j) {
+  uint32_t ub[64];
+  expand_message_xmd_32(ub, msg);
+  fp2 u;
+  fp_from_64be_words(u.c0, ub + 32 * j);
+  fp_from_64be_words(u.c1, ub + 32 * j + 16);
+  g2a q;
+  map_to_curve_sswu(q, u);
+  iso_map_g2(r, q);
+}
+// Q0 + Q1 -> clear_cofactor
+LB_DEV void hash_to_g2_finish(g2j& r, const g2j& q0, const g2j& q1) {
+  g2j s;
+  jac_add(s, q0, q1);
+  clear_cofactor_g2(r, s);
+}
+
 // hash_to_curve(msg) -> Jacobian point of G2
 LB_DEV void hash_to_g2(g2j& r, const uint8_t msg[32]) {
   fp2 u[2];

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -44,9 +45,12 @@ __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_
   for (uint32_t i = a; i < b; i++) single_flag[i] = (b - a == 1) ? 1 : 0;
 }
 
+// Signature.fromBytes(validate=true); for single-set requests also the
+// ZeroSignatureError of @chainsafe/bls Signature.verify.
 __global__ void __launch_bounds__(TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
-                                                     const uint32_t* __restrict__ sig_off, g2j* __restrict__ out_sig,
-                                                     uint8_t* __restrict__ status) {
+                                                     const uint32_t* __restrict__ sig_off,
+                                                     const uint8_t* __restrict__ single_flag,
+                                                     g2j* __restrict__ out_sig, uint8_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t a = sig_off[i], b = sig_off[i + 1];
@@ -57,57 +61,274 @@ __global__ void __launch_bounds__(TPB) k_decode_sigs(uint32_t n, const uint8_t* 
   if (st == LB_ST_OK) {
     jac_from_aff(sj, s);
     if (!g2_in_subgroup(sj)) st = LB_ST_NOT_IN_GROUP;
+    else if (single_flag && single_flag[i] && s.inf) st = LB_ST_ZERO_SIGNATURE;
   }
   out_sig[i] = sj;
   status[i] = st;
 }
 
-// One workgroup (one wave) per set: lanes decode pubkeys strided, LDS tree sum.
-__global__ void __launch_bounds__(TPB) k_pubkeys(uint32_t n_sets, const uint8_t* __restrict__ pks,
-                                                 const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
-                                                 uint8_t* __restrict__ pk_status) {
-  __shared__ g1j sh[TPB];
-  __shared__ uint32_t bad;
-  const uint32_t set = blockIdx.x;
+// Sets with exactly one pubkey (the common case): one lane per set.
+__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                        const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                        uint8_t* __restrict__ pk_status) {
+  const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
   if (set >= n_sets) return;
   const uint32_t a = pk_off ? pk_off[set] : set, b = pk_off ? pk_off[set + 1] : set + 1;
-  if (threadIdx.x == 0) bad = 0;
-  __syncthreads();
+  if (b - a > 1) return;  // aggregate: k_pubkeys_agg
   g1j acc;
   jac_set_inf(acc);
-  for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
+  uint8_t st = LB_ST_EMPTY_AGGREGATE;
+  if (b == a + 1) {
     g1a p;
-    const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
-    if (st != LB_ST_OK) {
-      atomicOr(&bad, 1u);
+    st = g1_deserialize(p, pks + (size_t)a * 96, 96);
+    if (st == LB_ST_OK) {
+      jac_from_aff(acc, p);
+      if (p.inf) st = LB_ST_PK_INFINITY;
     } else {
-      jac_add_aff(acc, acc, p);
+      st = LB_ST_BAD_ENCODING;
     }
+  }
+  out_pk[set] = acc;
+  pk_status[set] = st;
+}
+
+// Sets with >= 2 pubkeys (PublicKey.aggregate, chain/bls/utils.ts:13): one
+// wave per set, grid-stride over sets; lanes decode strided, LDS tree sum.
+__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                     const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                     uint8_t* __restrict__ pk_status) {
+  __shared__ g1j sh[TPB];
+  __shared__ uint32_t bad;
+  if (!pk_off) return;
+  for (uint32_t set = blockIdx.x; set < n_sets; set += gridDim.x) {
+    const uint32_t a = pk_off[set], b = pk_off[set + 1];
+    if (b - a <= 1) continue;  // uniform across the block
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    g1j acc;
+    jac_set_inf(acc);
+    for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
+      g1a p;
+      const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
+      if (st != LB_ST_OK) {
+        atomicOr(&bad, 1u);
+      } else {
+        jac_add_aff(acc, acc, p);
+      }
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = TPB / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+        g1j o = sh[threadIdx.x + s];
+        g1j m = sh[threadIdx.x];
+        jac_add(m, m, o);
+        sh[threadIdx.x] = m;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      out_pk[set] = sh[0];
+      pk_status[set] = bad ? LB_ST_BAD_ENCODING : jac_is_inf(sh[0]) ? LB_ST_PK_INFINITY : LB_ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+// hash_to_G2, first half: lane 2i+j maps u_j of message i (SSWU + 3-isogeny)
+__global__ void __launch_bounds__(TPB) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                   g2j* __restrict__ q) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n) return;
+  uint8_t m[32];
+  const uint8_t* src = msgs + (size_t)(t >> 1) * 32;
+  for (int k = 0; k < 32; k++) m[k] = src[k];
+  g2j r;
+  hash_to_g2_half(r, m, (int)(t & 1));
+  q[t] = r;
+}
+// hash_to_G2, second half: Q0 + Q1, clear cofactor, affine
+__global__ void __launch_bounds__(TPB) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
+  hash_to_g2_finish(h, q0, q1);
+  g2a ha;
+  jac_to_aff(ha, h);
+  out_h[i] = ha;
+}
+
+// r_i sig_i
+__global__ void __launch_bounds__(TPB) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+                                                    const g2j* __restrict__ sig,
+                                                    const uint8_t* __restrict__ sig_status,
+                                                    g2j* __restrict__ rsig) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j rs;
+  jac_set_inf(rs);
+  if (sig_status[i] == LB_ST_OK) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    const uint64_t r = batch_scalar(sd, i);
+    g2j s = sig[i];
+    jac_mul_u64(rs, s, r);
+  }
+  rsig[i] = rs;
+}
+
+// r_i pk_i (affine); core-verify pubkey subgroup check for single-set requests
+__global__ void __launch_bounds__(TPB) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+                                                   const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
+                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = pk_status[i];
+  g1j p = pk[i];
+  if (st == LB_ST_OK && single_flag[i] && !g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
+  g1a pa;
+  fp_zero(pa.x);
+  fp_zero(pa.y);
+  pa.inf = true;
+  if (st == LB_ST_OK) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    const uint64_t r = batch_scalar(sd, i);
+    g1j rp;
+    jac_mul_u64(rp, p, r);
+    jac_to_aff(pa, rp);
+  }
+  rpk[i] = pa;
+  pk_status[i] = st;
+}
+
+// S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
+__global__ void __launch_bounds__(TPB) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S) {
+  __shared__ g2j sh[TPB];
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
+    g2j t = rsig[i];
+    jac_add(acc, acc, t);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
   for (int s = TPB / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-      g1j o = sh[threadIdx.x + s];
-      g1j m = sh[threadIdx.x];
+      g2j m = sh[threadIdx.x], o = sh[threadIdx.x + s];
       jac_add(m, m, o);
       sh[threadIdx.x] = m;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    out_pk[set] = sh[0];
-    uint8_t st = LB_ST_OK;
-    if (b == a)
-      st = LB_ST_EMPTY_AGGREGATE;
-    else if (bad)
-      st = LB_ST_BAD_ENCODING;
-    else if (jac_is_inf(sh[0]))
-      st = LB_ST_PK_INFINITY;
-    pk_status[set] = st;
+    g2j tot = sh[0];
+    g2a sa;
+    jac_to_aff(sa, tot);
+    S[k] = sa;
   }
 }
 
+// f_S[k] = Miller(-g1, S_k)
+__global__ void __launch_bounds__(TPB) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  fp12 r;
+  fp12_one(r);
+  g2a q = S[k];
+  if (!q.inf) {
+    g1a g;
+    fp_set(g.x, LB_G1_X);
+    fp_set(g.y, LB_G1_NEG_Y);
+    g.inf = false;
+    miller_loop(r, g, q);
+  }
+  fS[k] = r;
+}
+
+// f_i = Miller(r_i pk_i, H(m_i))
+__global__ void __launch_bounds__(TPB) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+                                                     fp12* __restrict__ f) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp12 r;
+  fp12_one(r);
+  g1a p = rpk[i];
+  g2a q = h[i];
+  if (!p.inf && !q.inf) miller_loop(r, p, q);
+  f[i] = r;
+}
+
+// F_k = f_S[k] * prod f_i, request status and errors: one wave per request
+__global__ void __launch_bounds__(TPB) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   const fp12* __restrict__ f, const fp12* __restrict__ fS,
+                                                   const uint8_t* __restrict__ sig_status,
+                                                   const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
+                                                   uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err) {
+  __shared__ fp12 sh[TPB];
+  __shared__ uint32_t bad, err_empty, err_pk;
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  if (threadIdx.x == 0) {
+    bad = (a == b) ? 1u : 0u;
+    err_empty = 0;
+    err_pk = 0;
+  }
+  __syncthreads();
+  fp12 acc;
+  fp12_one(acc);
+  bool first = true;
+  for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
+    const uint8_t ss = sig_status[i], ps = pk_status[i];
+    if (ss != LB_ST_OK || ps != LB_ST_OK) atomicOr(&bad, 1u);
+    if (ps == LB_ST_EMPTY_AGGREGATE) atomicOr(&err_empty, 1u);
+    if (ps == LB_ST_BAD_ENCODING) atomicOr(&err_pk, 1u);
+    fp12 t = f[i];
+    if (first) {
+      acc = t;
+      first = false;
+    } else {
+      fp12_mul(acc, acc, t);
+    }
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+      fp12 m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      fp12_mul(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    fp12 tot = sh[0], s = fS[k];
+    fp12_mul(tot, tot, s);
+    F[k] = tot;
+    req_bad[k] = bad ? 1 : 0;
+    req_err[k] = err_empty ? LB_REQ_EMPTY_AGGREGATE : err_pk ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_final(uint32_t n_req, const fp12* __restrict__ F,
+                                               const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  if (req_bad[k]) {
+    valid[k] = 0;
+    return;
+  }
+  fp12 acc = F[k], r;
+  final_exp(r, acc);
+  valid[k] = fp12_is_one(r) ? 1 : 0;
+}
+
+// ---- hash_to_G2 in one lane (stage-level API) ------------------------------
 __global__ void __launch_bounds__(TPB) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -118,127 +339,6 @@ __global__ void __launch_bounds__(TPB) k_hash(uint32_t n, const uint8_t* __restr
   g2a ha;
   jac_to_aff(ha, h);
   out_h[i] = ha;
-}
-
-// combined per-set status: signature decode, pubkey decode, core-verify checks
-__global__ void __launch_bounds__(TPB)
-    k_scalar(uint32_t n, const uint8_t* __restrict__ seed, const g1j* __restrict__ pk, const g2j* __restrict__ sig,
-             const uint8_t* __restrict__ sig_status, const uint8_t* __restrict__ pk_status,
-             const uint8_t* __restrict__ single_flag, g1a* __restrict__ rpk, g2j* __restrict__ rsig,
-             uint8_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t st = sig_status[i];
-  if (st == LB_ST_OK) st = pk_status[i];
-  g1j p = pk[i];
-  g2j s = sig[i];
-  if (st == LB_ST_OK && single_flag[i]) {
-    // BlsVerifier single-set path: sig.verify -> ZeroSignatureError on infinity,
-    // core_verify checks the pubkey subgroup
-    if (jac_is_inf(s)) st = LB_ST_ZERO_SIGNATURE;
-    else if (!g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
-  }
-  g1a pa;
-  fp_zero(pa.x);
-  fp_zero(pa.y);
-  pa.inf = true;
-  g2j rs;
-  jac_set_inf(rs);
-  if (st == LB_ST_OK) {
-    uint8_t sd[32];
-    for (int k = 0; k < 32; k++) sd[k] = seed[k];
-    const uint64_t r = batch_scalar(sd, i);
-    g1j rp;
-    jac_mul_u64(rp, p, r);
-    jac_to_aff(pa, rp);
-    jac_mul_u64(rs, s, r);
-  }
-  rpk[i] = pa;
-  rsig[i] = rs;
-  status[i] = st;
-}
-
-__global__ void __launch_bounds__(TPB) k_sum_req(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                 const g2j* __restrict__ rsig, const uint8_t* __restrict__ status,
-                                                 g2a* __restrict__ S, uint8_t* __restrict__ req_bad) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  const uint32_t a = req_off[k], b = req_off[k + 1];
-  uint8_t bad = (a == b) ? 1 : 0;
-  g2j acc;
-  jac_set_inf(acc);
-  for (uint32_t i = a; i < b && !bad; i++) {
-    if (status[i] != LB_ST_OK) {
-      bad = 1;
-    } else {
-      g2j t = rsig[i];
-      jac_add(acc, acc, t);
-    }
-  }
-  g2a sa;
-  jac_to_aff(sa, acc);
-  S[k] = sa;
-  req_bad[k] = bad;
-}
-
-__global__ void __launch_bounds__(TPB)
-    k_miller(uint32_t n_sets, uint32_t n_req, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
-             const uint8_t* __restrict__ status, const g2a* __restrict__ S, const uint8_t* __restrict__ req_bad,
-             fp12* __restrict__ f) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_sets + n_req) return;
-  fp12 r;
-  fp12_one(r);
-  if (j < n_sets) {
-    if (status[j] == LB_ST_OK) {
-      g1a p = rpk[j];
-      g2a q = h[j];
-      if (!p.inf && !q.inf) miller_loop(r, p, q);
-    }
-  } else {
-    const uint32_t k = j - n_sets;
-    g2a q = S[k];
-    if (!req_bad[k] && !q.inf) {
-      g1a g;
-      fp_set(g.x, LB_G1_X);
-      fp_set(g.y, LB_G1_NEG_Y);
-      g.inf = false;
-      miller_loop(r, g, q);
-    }
-  }
-  f[j] = r;
-}
-
-__global__ void __launch_bounds__(TPB) k_final(uint32_t n_sets, uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                               const fp12* __restrict__ f, const uint8_t* __restrict__ req_bad,
-                                               uint8_t* __restrict__ valid) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  if (req_bad[k]) {
-    valid[k] = 0;
-    return;
-  }
-  fp12 acc = f[n_sets + k];
-  for (uint32_t i = req_off[k]; i < req_off[k + 1]; i++) {
-    fp12 t = f[i];
-    fp12_mul(acc, acc, t);
-  }
-  fp12 r;
-  final_exp(r, acc);
-  valid[k] = fp12_is_one(r) ? 1 : 0;
-}
-
-// request-level error codes (reject rather than false)
-__global__ void __launch_bounds__(TPB) k_req_errors(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                    const uint8_t* __restrict__ pk_status, uint8_t* __restrict__ err) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  uint8_t e = LB_REQ_OK;
-  for (uint32_t i = req_off[k]; i < req_off[k + 1]; i++) {
-    if (pk_status[i] == LB_ST_EMPTY_AGGREGATE && e == LB_REQ_OK) e = LB_REQ_EMPTY_AGGREGATE;
-    if (pk_status[i] == LB_ST_BAD_ENCODING && e == LB_REQ_OK) e = LB_REQ_BAD_PUBKEY;
-  }
-  err[k] = e;
 }
 
 // ---- generic point sums (one workgroup, LDS tree) ------------------------
@@ -384,22 +484,45 @@ static unsigned long long opcount_read_reset() {
 // ============================================================================
 // Host side: context, workspace, C ABI
 // ============================================================================
-struct lb_ctx {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  std::string err;
+// One in-flight call: two streams (DAG), own workspace, staging and events.
+struct Slot {
+  hipStream_t st[2] = {};
+  hipEvent_t dep[8] = {};
+  hipEvent_t done = nullptr;
   char* d_ws = nullptr;
   size_t ws_cap = 0;
   char* h_pin = nullptr;
   size_t pin_cap = 0;
-  static constexpr int kMaxEv = 16;
-  hipEvent_t ev[kMaxEv] = {};
-  const char* ev_name[kMaxEv] = {};
-  int n_ev = 0;
-  float stage_ms[kMaxEv] = {};
-  unsigned long long stage_ops[kMaxEv] = {};
-  const char* stage_name[kMaxEv] = {};
+  static constexpr int kMaxStages = 20;
+  hipEvent_t ev0[kMaxStages] = {}, ev1[kMaxStages] = {};
+  const char* stage_name[kMaxStages] = {};
   int n_stages = 0;
+  unsigned long long stage_ops[kMaxStages] = {};
+  hipEvent_t wall0 = nullptr, wall1 = nullptr;
+  bool busy = false;
+  uint64_t ticket = 0;
+};
+
+struct lb_ctx {
+  int device = -1;
+  // total streams <= GPU_MAX_HW_QUEUES (4 on the box).  Default LB_SLOTS=3: slot 0
+  // runs the two-stream DAG (synchronous calls, lowest latency), slots 1-2 one
+  // stream each; the async API round-robins all slots.  LB_SLOTS=2: two DAG
+  // slots; LB_SLOTS=4: four single-stream slots.
+  static constexpr int kMaxSlots = 4;
+  int n_slots = 3;
+  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1};
+  Slot slots[kMaxSlots];
+  int next_slot = 0;
+  uint64_t next_ticket = 1;
+  std::string err;
+  hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
+  // timing of the last completed verify call
+  int n_stages = 0;
+  float stage_ms[Slot::kMaxStages] = {};
+  const char* stage_name[Slot::kMaxStages] = {};
+  unsigned long long stage_ops[Slot::kMaxStages] = {};
+  float wall_ms = 0.f;
 };
 
 namespace {
@@ -411,6 +534,12 @@ namespace {
       ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);                    \
       return LB_ERR_DEVICE;                                                            \
     }                                                                                  \
+  } while (0)
+
+#define LB_TRY(x)                 \
+  do {                            \
+    int rc_ = (x);                \
+    if (rc_ != LB_OK) return rc_; \
   } while (0)
 
 inline uint32_t blocks_for(uint32_t n, uint32_t tpb = TPB) { return (n + tpb - 1) / tpb; }
@@ -428,123 +557,147 @@ struct Bump {
   }
 };
 
-int ensure_ws(lb_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->ws_cap) return LB_OK;
-  if (ctx->d_ws) {
-    LB_HIP(hipStreamSynchronize(ctx->stream));
-    LB_HIP(hipFree(ctx->d_ws));
-    ctx->d_ws = nullptr;
-    ctx->ws_cap = 0;
+int ensure_ws(lb_ctx* ctx, Slot& sl, size_t bytes) {
+  if (bytes <= sl.ws_cap) return LB_OK;
+  if (sl.d_ws) {
+    LB_HIP(hipStreamSynchronize(sl.st[0]));
+    LB_HIP(hipStreamSynchronize(sl.st[1]));
+    LB_HIP(hipFree(sl.d_ws));
+    sl.d_ws = nullptr;
+    sl.ws_cap = 0;
   }
   size_t cap = bytes + bytes / 4 + (1 << 20);
-  if (hipMalloc(&ctx->d_ws, cap) != hipSuccess) {
+  if (hipMalloc(&sl.d_ws, cap) != hipSuccess) {
     ctx->err = "hipMalloc workspace failed";
     return LB_ERR_OUT_OF_MEMORY;
   }
-  ctx->ws_cap = cap;
+  sl.ws_cap = cap;
   return LB_OK;
 }
+int ensure_ws(lb_ctx* ctx, size_t bytes) { return ensure_ws(ctx, ctx->slots[0], bytes); }
 
-int ensure_pin(lb_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->pin_cap) return LB_OK;
-  if (ctx->h_pin) {
-    LB_HIP(hipStreamSynchronize(ctx->stream));
-    LB_HIP(hipHostFree(ctx->h_pin));
-    ctx->h_pin = nullptr;
-    ctx->pin_cap = 0;
+int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
+  if (bytes <= sl.pin_cap) return LB_OK;
+  if (sl.h_pin) {
+    LB_HIP(hipStreamSynchronize(sl.st[0]));
+    LB_HIP(hipHostFree(sl.h_pin));
+    sl.h_pin = nullptr;
+    sl.pin_cap = 0;
   }
   size_t cap = bytes + bytes / 4 + (1 << 20);
-  if (hipHostMalloc(&ctx->h_pin, cap, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&sl.h_pin, cap, hipHostMallocDefault) != hipSuccess) {
     ctx->err = "hipHostMalloc staging failed";
     return LB_ERR_OUT_OF_MEMORY;
   }
-  ctx->pin_cap = cap;
+  sl.pin_cap = cap;
   return LB_OK;
 }
 
-int mark(lb_ctx* ctx, const char* name) {
-  if (ctx->n_ev >= lb_ctx::kMaxEv) return LB_OK;
 #ifdef LB_COUNT_OPS
-  LB_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->stage_ops[ctx->n_ev] = opcount_read_reset();
+#define LB_COUNT_SYNC() LB_HIP(hipDeviceSynchronize())
+#define LB_COUNT_TAKE(i) sl.stage_ops[i] = opcount_read_reset()
+#else
+#define LB_COUNT_SYNC() ((void)0)
+#define LB_COUNT_TAKE(i) ((void)0)
 #endif
-  LB_HIP(hipEventRecord(ctx->ev[ctx->n_ev], ctx->stream));
-  ctx->ev_name[ctx->n_ev] = name;
-  ctx->n_ev++;
+
+// Launch `kern` on stream `s` of slot `sl`, bracketed by timing events.
+#define LB_STAGE(name, s, kern, grid, block, ...)                                          \
+  do {                                                                                     \
+    const int si_ = sl.n_stages < Slot::kMaxStages ? sl.n_stages++ : -1;                   \
+    LB_COUNT_SYNC();                                                                       \
+    if (si_ >= 0) {                                                                        \
+      LB_COUNT_TAKE(si_);                                                                  \
+      sl.stage_name[si_] = name;                                                           \
+      LB_HIP(hipEventRecord(sl.ev0[si_], sl.st[s]));                                       \
+    }                                                                                      \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, sl.st[s], __VA_ARGS__);          \
+    LB_HIP(hipGetLastError());                                                             \
+    if (si_ >= 0) LB_HIP(hipEventRecord(sl.ev1[si_], sl.st[s]));                           \
+    LB_COUNT_SYNC();                                                                       \
+    if (si_ >= 0) {                                                                        \
+      LB_COUNT_TAKE(si_);                                                                  \
+    }                                                                                      \
+  } while (0)
+
+#define LB_LAUNCH(kern, grid, block, ...)                                                  \
+  do {                                                                                     \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, ctx->stream, __VA_ARGS__);       \
+    LB_HIP(hipGetLastError());                                                             \
+  } while (0)
+
+// stream `to` of the slot waits for everything enqueued so far on stream `from`
+int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
+  LB_HIP(hipEventRecord(sl.dep[ev], sl.st[from]));
+  LB_HIP(hipStreamWaitEvent(sl.st[to], sl.dep[ev], 0));
   return LB_OK;
 }
 
-int collect_marks(lb_ctx* ctx) {
-  ctx->n_stages = 0;
-  for (int i = 1; i < ctx->n_ev; i++) {
-    float ms = 0.f;
-    LB_HIP(hipEventElapsedTime(&ms, ctx->ev[i - 1], ctx->ev[i]));
-    ctx->stage_ms[ctx->n_stages] = ms;
-    ctx->stage_name[ctx->n_stages] = ctx->ev_name[i];
-    ctx->n_stages++;
-  }
-  return LB_OK;
-}
-
-#define LB_TRY(x)             \
-  do {                        \
-    int rc_ = (x);            \
-    if (rc_ != LB_OK) return rc_; \
-  } while (0)
-
-#define LB_LAUNCH(kern, grid, block, ...)                                     \
-  do {                                                                        \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, ctx->stream, __VA_ARGS__); \
-    LB_HIP(hipGetLastError());                                                \
-  } while (0)
-
-// Core pipeline on device-resident inputs.  All pointers are device pointers.
-int run_pipeline(lb_ctx* ctx, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off, const uint8_t* d_pks,
-                 const uint32_t* d_pk_off, const uint8_t* d_msgs, const uint8_t* d_sigs, const uint32_t* d_sig_off,
-                 const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err, uint8_t* d_set_status, Bump& ws) {
-  g2j* d_sig = ws.take<g2j>(n_sets);
-  g1j* d_pk = ws.take<g1j>(n_sets);
-  g1a* d_rpk = ws.take<g1a>(n_sets);
-  g2j* d_rsig = ws.take<g2j>(n_sets);
-  g2a* d_h = ws.take<g2a>(n_sets);
-  uint8_t* d_sig_st = ws.take<uint8_t>(n_sets);
-  uint8_t* d_pk_st = ws.take<uint8_t>(n_sets);
-  uint8_t* d_single = ws.take<uint8_t>(n_sets);
-  uint8_t* d_st = d_set_status ? d_set_status : ws.take<uint8_t>(n_sets);
+// Core pipeline on device-resident inputs (all pointers are device pointers),
+// as a two-stream DAG inside the slot:
+//   A: flags -> pubkeys -> r_i pk_i -> [evPK] -> decode sigs -> r_i sig_i -> S_k (tree)
+//      -> Miller(-g1, S_k) -> [wait B] -> per-request product (tree) -> final exp
+//   B: hash_to_G2 (two lanes per message) -> [wait evPK] -> Miller(r_i pk_i, H_i)
+int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
+                 const uint8_t* d_pks, const uint32_t* d_pk_off, const uint8_t* d_msgs, const uint8_t* d_sigs,
+                 const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
+                 uint8_t* d_set_status, Bump& ws) {
+  const uint32_t ns = n_sets ? n_sets : 1;
+  g2j* d_sig = ws.take<g2j>(ns);
+  g2j* d_rsig = ws.take<g2j>(ns);
+  g2j* d_q = ws.take<g2j>(2 * (size_t)ns);
+  g2a* d_h = ws.take<g2a>(ns);
+  g1j* d_pk = ws.take<g1j>(ns);
+  g1a* d_rpk = ws.take<g1a>(ns);
+  fp12* d_f = ws.take<fp12>(ns);
+  uint8_t* d_single = ws.take<uint8_t>(ns);
+  uint8_t* d_pk_st = ws.take<uint8_t>(ns);
+  uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
   g2a* d_S = ws.take<g2a>(n_req);
+  fp12* d_fS = ws.take<fp12>(n_req);
+  fp12* d_F = ws.take<fp12>(n_req);
   uint8_t* d_bad = ws.take<uint8_t>(n_req);
-  fp12* d_f = ws.take<fp12>((size_t)n_sets + n_req);
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
   }
-  if (n_sets > 0) {
-    LB_LAUNCH(k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
-    LB_TRY(mark(ctx, "req_flags"));
-    LB_LAUNCH(k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off, d_sig, d_sig_st);
-    LB_TRY(mark(ctx, "decode_sigs"));
-    LB_LAUNCH(k_pubkeys, n_sets, TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
-    LB_TRY(mark(ctx, "pubkeys"));
-    LB_LAUNCH(k_hash, blocks_for(n_sets), TPB, n_sets, d_msgs, d_h);
-    LB_TRY(mark(ctx, "hash_to_g2"));
-    LB_LAUNCH(k_scalar, blocks_for(n_sets), TPB, n_sets, d_seed, d_pk, d_sig, d_sig_st, d_pk_st, d_single, d_rpk,
-              d_rsig, d_st);
-    LB_TRY(mark(ctx, "scalar_mul"));
+  LB_TRY(stream_wait(ctx, sl, 0, 1, 0));
+  if (n_sets) {
+    LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
+    LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, (const g2j*)d_q, d_h);
   }
-  LB_LAUNCH(k_sum_req, blocks_for(n_req), TPB, n_req, d_req_off, d_rsig, d_st, d_S, d_bad);
-  LB_TRY(mark(ctx, "sum_sigs"));
-  LB_LAUNCH(k_miller, blocks_for(n_sets + n_req), TPB, n_sets, n_req, d_rpk, d_h, d_st, d_S, d_bad, d_f);
-  LB_TRY(mark(ctx, "miller"));
-  LB_LAUNCH(k_final, blocks_for(n_req), TPB, n_sets, n_req, d_req_off, d_f, d_bad, d_valid);
-  LB_TRY(mark(ctx, "final_exp"));
-  LB_LAUNCH(k_req_errors, blocks_for(n_req), TPB, n_req, d_req_off, d_pk_st, d_req_err);
+  LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
+  if (n_sets) {
+    LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
+    if (d_pk_off)
+      LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, 2048u, TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
+    LB_STAGE("scalar_pk", 0, k_scalar_pk, blocks_for(n_sets), TPB, n_sets, d_seed, (const g1j*)d_pk,
+             (const uint8_t*)d_single, d_pk_st, d_rpk);
+  }
+  LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
+  if (n_sets)
+    LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1a*)d_rpk, (const g2a*)d_h,
+             d_f);
+  if (n_sets) {
+    LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
+             (const uint8_t*)d_single, d_sig, d_sig_st);
+    LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
+             (const uint8_t*)d_sig_st, d_rsig);
+  }
+  LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S);
+  LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
+  LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
+  LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, (const fp12*)d_fS,
+           (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
+  LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
   return LB_OK;
 }
 
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
-  size_t per_set = sizeof(g2j) * 2 + sizeof(g1j) + sizeof(g1a) + sizeof(g2a) + 4 + sizeof(fp12) + 6 * 256 / 64;
-  size_t per_req = sizeof(g2a) + 1 + sizeof(fp12);
-  return (size_t)n_sets * per_set + (size_t)n_req * per_req + 64 * 256;
+  size_t ns = n_sets ? n_sets : 1;
+  size_t per_set = sizeof(g2j) * 4 + sizeof(g2a) + sizeof(g1j) + sizeof(g1a) + sizeof(fp12) + 3 + 16 * 256 / 64;
+  size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64;
+  return ns * per_set + (size_t)n_req * per_req + 64 * 256;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -553,6 +706,42 @@ int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
     ctx->err = "null pointer in lb_request_batch";
     return LB_ERR_INVALID_ARGUMENT;
   }
+  return LB_OK;
+}
+
+// Wait for a slot's outstanding call and publish its stage times.
+int finish_slot(lb_ctx* ctx, Slot& sl) {
+  if (!sl.busy) return LB_OK;
+  LB_HIP(hipEventSynchronize(sl.done));
+  ctx->n_stages = sl.n_stages;
+  for (int i = 0; i < sl.n_stages; i++) {
+    float ms = 0.f;
+    LB_HIP(hipEventElapsedTime(&ms, sl.ev0[i], sl.ev1[i]));
+    ctx->stage_ms[i] = ms;
+    ctx->stage_name[i] = sl.stage_name[i];
+    ctx->stage_ops[i] = sl.stage_ops[i];
+  }
+  LB_HIP(hipEventElapsedTime(&ctx->wall_ms, sl.wall0, sl.wall1));
+  sl.busy = false;
+  return LB_OK;
+}
+
+int begin_call(lb_ctx* ctx, Slot& sl) {
+  sl.n_stages = 0;
+  LB_HIP(hipEventRecord(sl.wall0, sl.st[0]));
+  return LB_OK;
+}
+int end_call_async(lb_ctx* ctx, Slot& sl) {
+  LB_HIP(hipEventRecord(sl.wall1, sl.st[0]));
+  LB_HIP(hipEventRecord(sl.done, sl.st[0]));
+  sl.busy = true;
+  sl.ticket = ctx->next_ticket++;
+  return LB_OK;
+}
+
+// Idle slot 0 for the synchronous helper entry points.
+int helper_slot(lb_ctx* ctx) {
+  for (int i = 0; i < ctx->n_slots; i++) LB_TRY(finish_slot(ctx, ctx->slots[i]));
   return LB_OK;
 }
 
@@ -576,15 +765,28 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || device < 0 || device >= n) return LB_ERR_NO_DEVICE;
   lb_ctx* ctx = new lb_ctx();
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return LB_ERR_DEVICE;
+  bool ok = hipSetDevice(device) == hipSuccess;
+  if (const char* e = getenv("LB_SLOTS")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
   }
-  for (int i = 0; i < lb_ctx::kMaxEv; i++) {
-    if (hipEventCreate(&ctx->ev[i]) != hipSuccess) {
-      delete ctx;
-      return LB_ERR_DEVICE;
-    }
+  for (int s = 0; s < lb_ctx::kMaxSlots; s++)
+    ctx->streams_per_slot[s] = ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;
+  for (int s = 0; ok && s < ctx->n_slots; s++) {
+    Slot& sl = ctx->slots[s];
+    for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++)
+      ok = hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking) == hipSuccess;
+    if (ctx->streams_per_slot[s] == 1) sl.st[1] = sl.st[0];
+    for (int i = 0; ok && i < 8; i++) ok = hipEventCreateWithFlags(&sl.dep[i], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < Slot::kMaxStages; i++)
+      ok = hipEventCreate(&sl.ev0[i]) == hipSuccess && hipEventCreate(&sl.ev1[i]) == hipSuccess;
+    ok = ok && hipEventCreate(&sl.wall0) == hipSuccess && hipEventCreate(&sl.wall1) == hipSuccess &&
+         hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+  }
+  ctx->stream = ctx->slots[0].st[0];
+  if (!ok) {
+    lb_destroy(ctx);
+    return LB_ERR_DEVICE;
   }
   *out_ctx = ctx;
   return LB_OK;
@@ -593,12 +795,24 @@ int lb_create(int device, lb_ctx** out_ctx) {
 int lb_destroy(lb_ctx* ctx) {
   if (!ctx) return LB_OK;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->d_ws) (void)hipFree(ctx->d_ws);
-  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
-  for (int i = 0; i < lb_ctx::kMaxEv; i++)
-    if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (int s = 0; s < ctx->n_slots; s++) {
+    Slot& sl = ctx->slots[s];
+    for (int i = 0; i < ctx->streams_per_slot[s]; i++)
+      if (sl.st[i]) (void)hipStreamSynchronize(sl.st[i]);
+    if (sl.d_ws) (void)hipFree(sl.d_ws);
+    if (sl.h_pin) (void)hipHostFree(sl.h_pin);
+    for (int i = 0; i < 8; i++)
+      if (sl.dep[i]) (void)hipEventDestroy(sl.dep[i]);
+    for (int i = 0; i < Slot::kMaxStages; i++) {
+      if (sl.ev0[i]) (void)hipEventDestroy(sl.ev0[i]);
+      if (sl.ev1[i]) (void)hipEventDestroy(sl.ev1[i]);
+    }
+    if (sl.wall0) (void)hipEventDestroy(sl.wall0);
+    if (sl.wall1) (void)hipEventDestroy(sl.wall1);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    for (int i = 0; i < ctx->streams_per_slot[s]; i++)
+      if (sl.st[i]) (void)hipStreamDestroy(sl.st[i]);
+  }
   delete ctx;
   return LB_OK;
 }
@@ -606,11 +820,11 @@ int lb_destroy(lb_ctx* ctx) {
 const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 #ifdef LB_COUNT_OPS
-// Fp products executed per stage of the last lb_verify_* call (count build only)
+// Fp products executed per stage of the last completed verify call (count build only)
 int lb_opcount_stages(const lb_ctx* ctx, unsigned long long* out, int max_stages) {
   if (!ctx) return 0;
   int n = 0;
-  for (int i = 1; i < ctx->n_ev && n < max_stages; i++) out[n++] = ctx->stage_ops[i];
+  for (int i = 0; i < ctx->n_stages && n < max_stages; i++) out[n++] = ctx->stage_ops[i];
   return n;
 }
 #endif
@@ -625,31 +839,55 @@ int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names
   return ctx->n_stages;
 }
 
+static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
+                         uint8_t* d_set_status, uint64_t* out_ticket) {
+  LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
+  LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(b->n_requests, b->n_sets)));
+  Bump ws{sl.d_ws, 0, sl.ws_cap};
+  LB_TRY(begin_call(ctx, sl));
+  if (b->n_requests)
+    LB_TRY(run_pipeline(ctx, sl, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets, b->messages,
+                        b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err, d_set_status, ws));
+  LB_TRY(end_call_async(ctx, sl));
+  *out_ticket = sl.ticket;
+  return LB_OK;
+}
+
+int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
+                                    uint8_t* d_set_status, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot& sl = ctx->slots[ctx->next_slot];
+  ctx->next_slot = (ctx->next_slot + 1) % ctx->n_slots;
+  return submit_device(ctx, sl, b, d_valid, d_req_err, d_set_status, out_ticket);
+}
+
+int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  for (int s = 0; s < ctx->n_slots; s++) {
+    Slot& sl = ctx->slots[s];
+    if (sl.busy && sl.ticket == ticket) LB_TRY(finish_slot(ctx, sl));
+  }
+  if (stats) {
+    stats->batch_retries = 0;
+    stats->batch_sigs_success = 0;
+    stats->device_ms = ctx->wall_ms;
+  }
+  return LB_OK;
+}
+
 int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
                               uint8_t* d_set_status, lb_verify_stats* stats) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_TRY(validate_batch(ctx, b));
   if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
-  auto t0 = std::chrono::steady_clock::now();
-  if (b->n_requests == 0) {
-    if (stats) *stats = lb_verify_stats{0, 0, 0.0};
-    return LB_OK;
-  }
-  LB_TRY(ensure_ws(ctx, pipeline_ws_bytes(b->n_requests, b->n_sets)));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
-  ctx->n_ev = 0;
-  LB_TRY(mark(ctx, "start"));
-  LB_TRY(run_pipeline(ctx, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets, b->messages,
-                      b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err, d_set_status, ws));
-  LB_HIP(hipStreamSynchronize(ctx->stream));
-  LB_TRY(collect_marks(ctx));
-  if (stats) {
-    stats->batch_retries = 0;
-    stats->batch_sigs_success = 0;
-    stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  return LB_OK;
+  uint64_t t = 0;
+  LB_TRY(submit_device(ctx, ctx->slots[0], b, d_valid, d_req_err, d_set_status, &t));  // slot 0: DAG, lowest latency
+  return lb_wait(ctx, t, stats);
 }
 
 int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
@@ -658,7 +896,6 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   LB_TRY(validate_batch(ctx, b));
   if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
-  auto t0 = std::chrono::steady_clock::now();
   const uint32_t nr = b->n_requests, ns = b->n_sets;
   if (nr == 0) {
     if (stats) *stats = lb_verify_stats{0, 0, 0.0};
@@ -674,6 +911,10 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
       ctx->err = "request_offsets not monotone";
       return LB_ERR_INVALID_ARGUMENT;
     }
+  if (b->sig_offsets[0] != 0) {
+    ctx->err = "sig_offsets must start at 0";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
   for (uint32_t i = 0; i < ns; i++)
     if (b->sig_offsets[i + 1] < b->sig_offsets[i]) {
       ctx->err = "sig_offsets not monotone";
@@ -681,11 +922,7 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
     }
   std::vector<uint32_t> pk_off_local;
   const uint32_t* pk_off = b->pk_offsets;
-  if (!pk_off) {
-    pk_off_local.resize(ns + 1);
-    for (uint32_t i = 0; i <= ns; i++) pk_off_local[i] = i;
-    pk_off = pk_off_local.data();
-  } else {
+  if (pk_off) {
     if (pk_off[0] != 0) {
       ctx->err = "pk_offsets must start at 0";
       return LB_ERR_INVALID_ARGUMENT;
@@ -696,28 +933,27 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
         return LB_ERR_INVALID_ARGUMENT;
       }
   }
-  const size_t n_pk = pk_off[ns];
+  const size_t n_pk = pk_off ? pk_off[ns] : ns;
   const size_t sig_bytes = b->sig_offsets[ns];
-  // staging layout
-  const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = sizeof(uint32_t) * (ns + 1),
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = pk_off ? sizeof(uint32_t) * (ns + 1) : 0,
                sz_pk = n_pk * 96, sz_msg = (size_t)ns * 32, sz_sigo = sizeof(uint32_t) * (ns + 1),
                sz_sig = sig_bytes, sz_seed = 32;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
-  const size_t out_bytes = al(nr) * 2 + al(ns);
-  LB_TRY(ensure_pin(ctx, in_bytes + out_bytes));
-  LB_TRY(ensure_ws(ctx, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
-  char* h = ctx->h_pin;
+  const size_t out_bytes = al(nr) * 2 + al(ns ? ns : 1);
+  Slot& sl = ctx->slots[0];  // synchronous host API: slot 0 (two-stream DAG)
+  LB_TRY(finish_slot(ctx, sl));
+  LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
+  LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
+  Bump ws{sl.d_ws, 0, sl.ws_cap};
+  char* h = sl.h_pin;
   size_t ho = 0;
   auto stage = [&](const void* src, size_t n) {
-    char* p = h + ho;
-    if (n) memcpy(p, src, n);
+    if (n) memcpy(h + ho, src, n);
     ho += al(n);
-    return p;
   };
   stage(b->request_offsets, sz_req);
-  stage(pk_off, sz_pko);
+  if (pk_off) stage(pk_off, sz_pko);
   stage(b->pubkeys, sz_pk);
   stage(b->messages, sz_msg);
   stage(b->sig_offsets, sz_sigo);
@@ -727,10 +963,8 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   uint8_t* d_valid = ws.take<uint8_t>(nr);
   uint8_t* d_err = ws.take<uint8_t>(nr);
   uint8_t* d_sst = ws.take<uint8_t>(ns ? ns : 1);
-  ctx->n_ev = 0;
-  LB_TRY(mark(ctx, "start"));
-  LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, ctx->stream));
-  LB_TRY(mark(ctx, "h2d"));
+  LB_TRY(begin_call(ctx, sl));
+  LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
   size_t o = 0;
   auto dptr = [&](size_t n) {
     char* p = d_in + o;
@@ -738,27 +972,26 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
     return p;
   };
   const uint32_t* d_req = (const uint32_t*)dptr(sz_req);
-  const uint32_t* d_pko = (const uint32_t*)dptr(sz_pko);
+  const uint32_t* d_pko = pk_off ? (const uint32_t*)dptr(sz_pko) : nullptr;
   const uint8_t* d_pks = (const uint8_t*)dptr(sz_pk);
   const uint8_t* d_msg = (const uint8_t*)dptr(sz_msg);
   const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
   const uint8_t* d_sig = (const uint8_t*)dptr(sz_sig);
   const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
-  LB_TRY(run_pipeline(ctx, nr, ns, d_req, d_pks, d_pko, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
+  LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, d_pks, d_pko, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
   char* h_out = h + in_bytes;
-  LB_HIP(hipMemcpyAsync(h_out, d_valid, nr, hipMemcpyDeviceToHost, ctx->stream));
-  LB_HIP(hipMemcpyAsync(h_out + al(nr), d_err, nr, hipMemcpyDeviceToHost, ctx->stream));
-  if (ns) LB_HIP(hipMemcpyAsync(h_out + 2 * al(nr), d_sst, ns, hipMemcpyDeviceToHost, ctx->stream));
-  LB_TRY(mark(ctx, "d2h"));
-  LB_HIP(hipStreamSynchronize(ctx->stream));
-  LB_TRY(collect_marks(ctx));
+  LB_HIP(hipMemcpyAsync(h_out, d_valid, nr, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_HIP(hipMemcpyAsync(h_out + al(nr), d_err, nr, hipMemcpyDeviceToHost, sl.st[0]));
+  if (ns) LB_HIP(hipMemcpyAsync(h_out + 2 * al(nr), d_sst, ns, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_TRY(end_call_async(ctx, sl));
+  LB_TRY(finish_slot(ctx, sl));
   memcpy(out_valid, h_out, nr);
   memcpy(out_req_err, h_out + al(nr), nr);
   if (out_set_status && ns) memcpy(out_set_status, h_out + 2 * al(nr), ns);
   if (stats) {
     stats->batch_retries = 0;
     stats->batch_sigs_success = 0;
-    stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->device_ms = ctx->wall_ms;
   }
   return LB_OK;
 }
@@ -775,8 +1008,9 @@ int lb_hash_to_g2(lb_ctx* ctx, uint32_t n, const uint8_t* messages, uint8_t* out
   if (!ctx || (n && (!messages || !out192))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (32 + sizeof(g2a) + 192) + 4096));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void* d_msg;
   LB_TRY(upload(ctx, ws, messages, (size_t)n * 32, &d_msg));
   g2a* d_h = ws.take<g2a>(n);
@@ -795,16 +1029,18 @@ int lb_decode_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const uin
   for (uint32_t i = 0; i < n; i++)
     if (sig_off[i + 1] < sig_off[i]) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   const size_t nb = sig_off[n];
   LB_TRY(ensure_ws(ctx, nb + (size_t)n * (4 + sizeof(g2j) + 1 + 192) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d_s, *d_o;
   LB_TRY(upload(ctx, ws, sigs, nb, &d_s));
   LB_TRY(upload(ctx, ws, sig_off, sizeof(uint32_t) * (n + 1), &d_o));
   g2j* d_sig = ws.take<g2j>(n);
   uint8_t* d_st = ws.take<uint8_t>(n);
   uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
-  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, d_sig, d_st);
+  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, (const uint8_t*)nullptr,
+            d_sig, d_st);
   LB_LAUNCH(k_g2_serialize, blocks_for(n), TPB, n, (const g2j*)d_sig, d_out);
   LB_HIP(hipMemcpyAsync(out_status, d_st, n, hipMemcpyDeviceToHost, ctx->stream));
   if (out192) LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
@@ -819,8 +1055,9 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint8_t* o
     return LB_ERR_INVALID_ARGUMENT;
   }
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * 96 + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void* d_p;
   LB_TRY(upload(ctx, ws, pks, (size_t)n * 96, &d_p));
   uint32_t off[2] = {0, n};
@@ -829,7 +1066,8 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint8_t* o
   g1j* d_pk = ws.take<g1j>(1);
   uint8_t* d_st = ws.take<uint8_t>(1);
   uint8_t* d_out = ws.take<uint8_t>(96);
-  LB_LAUNCH(k_pubkeys, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_pubkeys_single, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_pubkeys_agg, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
   LB_LAUNCH(k_g1_serialize, 1, TPB, 1u, (const g1j*)d_pk, d_out);
   uint8_t st = 0;
   LB_HIP(hipMemcpyAsync(out96, d_out, 96, hipMemcpyDeviceToHost, ctx->stream));
@@ -850,9 +1088,10 @@ int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const 
   for (uint32_t i = 0; i < n; i++)
     if (sig_off[i + 1] < sig_off[i]) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   const size_t nb = sig_off[n];
   LB_TRY(ensure_ws(ctx, nb + (size_t)n * (4 + sizeof(g2j) + 1) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d_s, *d_o;
   LB_TRY(upload(ctx, ws, sigs, nb, &d_s));
   LB_TRY(upload(ctx, ws, sig_off, sizeof(uint32_t) * (n + 1), &d_o));
@@ -860,7 +1099,8 @@ int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const 
   uint8_t* d_st = ws.take<uint8_t>(n);
   g2j* d_sum = ws.take<g2j>(1);
   uint8_t* d_out = ws.take<uint8_t>(192);
-  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, d_sig, d_st);
+  LB_LAUNCH(k_decode_sigs, blocks_for(n), TPB, n, (const uint8_t*)d_s, (const uint32_t*)d_o, (const uint8_t*)nullptr,
+            d_sig, d_st);
   LB_LAUNCH(k_jac_sum<fp2>, 1, 256, n, (const g2j*)d_sig, d_sum);
   LB_LAUNCH(k_g2_serialize, 1, TPB, 1u, (const g2j*)d_sum, d_out);
   std::vector<uint8_t> st(n);
@@ -938,8 +1178,9 @@ int lb_pairing(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint8_t* g2_
   if (!ctx || (n && (!g1_96 || !g2_192 || !out576))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (96 + 192 + 576) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d1, *d2;
   LB_TRY(upload(ctx, ws, g1_96, (size_t)n * 96, &d1));
   LB_TRY(upload(ctx, ws, g2_192, (size_t)n * 192, &d2));
@@ -954,8 +1195,9 @@ int lb_batch_scalars(lb_ctx* ctx, const uint8_t* seed, uint32_t first, uint32_t 
   if (!ctx || !seed || (n && !out)) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * 8 + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void* d_seed;
   LB_TRY(upload(ctx, ws, seed, 32, &d_seed));
   uint64_t* d_out = ws.take<uint64_t>(n);
@@ -969,8 +1211,9 @@ int lb_g1_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in96, const uint64_t* k, u
   if (!ctx || (n && (!in96 || !k || !out96))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (96 * 2 + 8) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d_in, *d_k;
   LB_TRY(upload(ctx, ws, in96, (size_t)n * 96, &d_in));
   LB_TRY(upload(ctx, ws, k, (size_t)n * 8, &d_k));
@@ -985,8 +1228,9 @@ int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* k, 
   if (!ctx || (n && (!in192 || !k || !out192))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (192 * 2 + 8) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d_in, *d_k;
   LB_TRY(upload(ctx, ws, in192, (size_t)n * 192, &d_in));
   LB_TRY(upload(ctx, ws, k, (size_t)n * 8, &d_k));
@@ -1001,8 +1245,9 @@ int lb_sk_to_pk(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, uint8_t* out96) {
   if (!ctx || (n && (!sk32 || !out96))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (32 + 96) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void* d_k;
   LB_TRY(upload(ctx, ws, sk32, (size_t)n * 32, &d_k));
   uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
@@ -1016,8 +1261,9 @@ int lb_sign(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, const uint8_t* message
   if (!ctx || (n && (!sk32 || !messages || !out96))) return LB_ERR_INVALID_ARGUMENT;
   if (n == 0) return LB_OK;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
   LB_TRY(ensure_ws(ctx, (size_t)n * (32 + 32 + 96) + 8192));
-  Bump ws{ctx->d_ws, 0, ctx->ws_cap};
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   void *d_k, *d_m;
   LB_TRY(upload(ctx, ws, sk32, (size_t)n * 32, &d_k));
   LB_TRY(upload(ctx, ws, messages, (size_t)n * 32, &d_m));

@@ -125,7 +125,7 @@ LB_NOINL void miller_loop(fp12& f, const g1a& P, const g2a& Q) {
 LB_NOINL void fp12_exp_x(fp12& r, const fp12& a) {
   fp12 acc = a;
   for (int i = 62; i >= 0; i--) {
-    fp12_sqr(acc, acc);
+    fp12_cyc_sqr(acc, acc);
     if ((LB_X_ABS >> i) & 1ull) fp12_mul(acc, acc, a);
   }
   fp12_conj(r, acc);
@@ -160,7 +160,7 @@ LB_NOINL void final_exp(fp12& r, const fp12& f) {
   fp12_conj(t1, b);
   fp12_mul(c, c, t1);
   // r = c * f2^3
-  fp12_sqr(t0, f2);
+  fp12_cyc_sqr(t0, f2);
   fp12_mul(t0, t0, f2);
   fp12_mul(r, c, t0);
 }

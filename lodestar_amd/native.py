@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
     "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
-    "lb_last_stage_times", "lb_sk_to_pk", "lb_sign",
+    "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
 )
 
 
@@ -104,6 +104,9 @@ def load_library() -> ctypes.CDLL:
     lib.lb_batch_scalars.argtypes = [vp, vp, u32, u32, vp]
     lib.lb_g1_mul.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_g2_mul.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_verify_requests_device_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
+                                                    ctypes.POINTER(ctypes.c_uint64)]
+    lib.lb_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_Stats)]
     lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
@@ -204,6 +207,22 @@ class Device:
         rc = self.lib.lb_verify_requests_device(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
                                                 ctypes.byref(st))
         self._check(rc, "lb_verify_requests_device")
+        return st.device_ms
+
+    def verify_requests_device_async(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int,
+                                     d_pk_off: Optional[int], d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int,
+                                     d_valid: int, d_err: int, d_set_status: Optional[int] = None) -> int:
+        """Enqueue; returns a ticket for wait().  All arguments are device pointers."""
+        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed)
+        t = ctypes.c_uint64(0)
+        rc = self.lib.lb_verify_requests_device_async(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
+                                                      ctypes.byref(t))
+        self._check(rc, "lb_verify_requests_device_async")
+        return int(t.value)
+
+    def wait(self, ticket: int) -> float:
+        st = _Stats()
+        self._check(self.lib.lb_wait(self._h, ticket, ctypes.byref(st)), "lb_wait")
         return st.device_ms
 
     def verify_same_message(self, pubkeys: Sequence[bytes], signatures: Sequence[bytes], message: bytes,
