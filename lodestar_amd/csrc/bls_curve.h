@@ -214,14 +214,13 @@ LB_DEV void jac_add_aff_impl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   r = o;
 }
 
-// G1 point ops inline; G2 point ops out of line (an inlined Fp2 group law
-// pushes the per-set kernels to 512 VGPRs = one wave per SIMD).
+// G1 point ops always inline; G2 point ops follow LB_TOWER (see bls_field.h).
 LB_DEV void jac_dbl(g1j& r, const g1j& p) { jac_dbl_impl(r, p); }
 LB_DEV void jac_add(g1j& r, const g1j& p, const g1j& q) { jac_add_impl(r, p, q); }
 LB_DEV void jac_add_aff(g1j& r, const g1j& p, const g1a& q) { jac_add_aff_impl(r, p, q); }
-LB_NOINL void jac_dbl(g2j& r, const g2j& p) { jac_dbl_impl(r, p); }
-LB_NOINL void jac_add(g2j& r, const g2j& p, const g2j& q) { jac_add_impl(r, p, q); }
-LB_NOINL void jac_add_aff(g2j& r, const g2j& p, const g2a& q) { jac_add_aff_impl(r, p, q); }
+LB_TOWER void jac_dbl(g2j& r, const g2j& p) { jac_dbl_impl(r, p); }
+LB_TOWER void jac_add(g2j& r, const g2j& p, const g2j& q) { jac_add_impl(r, p, q); }
+LB_TOWER void jac_add_aff(g2j& r, const g2j& p, const g2a& q) { jac_add_aff_impl(r, p, q); }
 
 template <class F>
 LB_DEV void jac_to_aff(aff<F>& r, const jac<F>& p) {

@@ -22,6 +22,17 @@
 
 #define LB_DEV __device__ __forceinline__
 #define LB_NOINL __device__ __noinline__
+// Tower-level routines (Fp6/Fp12 products, G2 group law, Miller loop, final
+// exponentiation) are inlined into the kernels by default: kernels then run at
+// one wave per SIMD with 256 VGPRs + 256 AGPRs and almost no scratch, instead
+// of spilling every call level's live state through the AMDGPU call ABI
+// (profiles/pmc_traffic.json: ~106 GB of spill traffic per Miller launch with
+// out-of-line tower routines).  Only fp_mul / fp_sqr stay out of line.
+#ifndef LB_TOWER_NOINLINE
+#define LB_TOWER LB_DEV
+#else
+#define LB_TOWER LB_NOINL
+#endif
 
 namespace lb {
 
@@ -544,7 +555,7 @@ LB_DEV void fp6_mul_v(fp6& r, const fp6& a) {
   r.c0 = t;
 }
 // Karatsuba (Devegili et al.): 6 Fp2 products
-LB_NOINL void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
+LB_TOWER void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
   fp2 t0, t1, t2, s, u;
   fp2_mul(t0, a.c0, b.c0);
   fp2_mul(t1, a.c1, b.c1);
@@ -650,7 +661,7 @@ LB_DEV void fp12_conj(fp12& r, const fp12& a) {
   fp6_neg(r.c1, a.c1);
 }
 // Karatsuba over Fp6: 3 Fp6 products = 18 Fp2 products
-LB_NOINL void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+LB_TOWER void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
   fp6 t0, t1, s, u;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -663,7 +674,7 @@ LB_NOINL void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
   fp6_add(r.c0, t0, t1);
 }
 // complex squaring: 2 Fp6 products
-LB_NOINL void fp12_sqr(fp12& r, const fp12& a) {
+LB_TOWER void fp12_sqr(fp12& r, const fp12& a) {
   fp6 t, s, u;
   fp6_mul(t, a.c0, a.c1);
   fp6_add(s, a.c0, a.c1);
@@ -704,7 +715,7 @@ LB_DEV void fp2_3a_p2b(fp2& r, const fp2& a, const fp2& b) {
   fp2_dbl(t, t);
   fp2_add(r, t, a);
 }
-LB_NOINL void fp12_cyc_sqr(fp12& r, const fp12& f) {
+LB_TOWER void fp12_cyc_sqr(fp12& r, const fp12& f) {
   fp2 Ax, Ay, Bx, By, Cx, Cy;
   fp4_sqr(Ax, Ay, f.c0.c0, f.c1.c1);
   fp4_sqr(Bx, By, f.c1.c0, f.c0.c2);
@@ -722,7 +733,7 @@ LB_NOINL void fp12_cyc_sqr(fp12& r, const fp12& f) {
 }
 
 // f * l, l = (l0 + l1 v) + (l4 v) w  (the Miller-loop line shape): 13 Fp2 products
-LB_NOINL void fp12_mul_line(fp12& r, const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
+LB_TOWER void fp12_mul_line(fp12& r, const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
   fp6 t0, t1, s;
   fp6_mul_01(t0, f.c0, l0, l1);
   fp6_mul_1(t1, f.c1, l4);

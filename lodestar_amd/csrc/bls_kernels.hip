@@ -36,6 +36,11 @@ using namespace lb;
 // Kernels
 // ============================================================================
 static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at high VGPR counts
+// min waves per SIMD for the heavy per-lane kernels: 1 = 512-register budget
+// (256 VGPR + 256 AGPR), which keeps the inlined tower arithmetic spill-free
+#ifndef LB_HEAVY_WAVES
+#define LB_HEAVY_WAVES 1
+#endif
 
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint8_t* __restrict__ single_flag) {
@@ -47,7 +52,7 @@ __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_
 
 // Signature.fromBytes(validate=true); for single-set requests also the
 // ZeroSignatureError of @chainsafe/bls Signature.verify.
-__global__ void __launch_bounds__(TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                      const uint32_t* __restrict__ sig_off,
                                                      const uint8_t* __restrict__ single_flag,
                                                      g2j* __restrict__ out_sig, uint8_t* __restrict__ status) {
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint
 }
 
 // hash_to_G2, first half: lane 2i+j maps u_j of message i (SSWU + 3-isogeny)
-__global__ void __launch_bounds__(TPB) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * n) return;
@@ -148,7 +153,7 @@ __global__ void __launch_bounds__(TPB) k_hash_half(uint32_t n, const uint8_t* __
   q[t] = r;
 }
 // hash_to_G2, second half: Q0 + Q1, clear cofactor, affine
-__global__ void __launch_bounds__(TPB) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(TPB) k_hash_finish(uint32_t n, const g2j* __re
 }
 
 // r_i sig_i
-__global__ void __launch_bounds__(TPB) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig) {
@@ -178,7 +183,7 @@ __global__ void __launch_bounds__(TPB) k_scalar_sig(uint32_t n, const uint8_t* _
 }
 
 // r_i pk_i (affine); core-verify pubkey subgroup check for single-set requests
-__global__ void __launch_bounds__(TPB) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
                                                    uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -203,7 +208,7 @@ __global__ void __launch_bounds__(TPB) k_scalar_pk(uint32_t n, const uint8_t* __
 }
 
 // S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
-__global__ void __launch_bounds__(TPB) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                   const g2j* __restrict__ rsig, g2a* __restrict__ S) {
   __shared__ g2j sh[TPB];
   const uint32_t k = blockIdx.x;
@@ -234,7 +239,7 @@ __global__ void __launch_bounds__(TPB) k_sum_tree(uint32_t n_req, const uint32_t
 }
 
 // f_S[k] = Miller(-g1, S_k)
-__global__ void __launch_bounds__(TPB) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_req) return;
   fp12 r;
@@ -251,7 +256,7 @@ __global__ void __launch_bounds__(TPB) k_miller_S(uint32_t n_req, const g2a* __r
 }
 
 // f_i = Miller(r_i pk_i, H(m_i))
-__global__ void __launch_bounds__(TPB) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
                                                      fp12* __restrict__ f) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -264,7 +269,7 @@ __global__ void __launch_bounds__(TPB) k_miller_sets(uint32_t n, const g1a* __re
 }
 
 // F_k = f_S[k] * prod f_i, request status and errors: one wave per request
-__global__ void __launch_bounds__(TPB) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    const fp12* __restrict__ f, const fp12* __restrict__ fS,
                                                    const uint8_t* __restrict__ sig_status,
                                                    const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(TPB) k_prod_tree(uint32_t n_req, const uint32_
   }
 }
 
-__global__ void __launch_bounds__(TPB) k_final(uint32_t n_req, const fp12* __restrict__ F,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_final(uint32_t n_req, const fp12* __restrict__ F,
                                                const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_req) return;
@@ -329,7 +334,7 @@ __global__ void __launch_bounds__(TPB) k_final(uint32_t n_req, const fp12* __res
 }
 
 // ---- hash_to_G2 in one lane (stage-level API) ------------------------------
-__global__ void __launch_bounds__(TPB) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t m[32];

@@ -92,7 +92,7 @@ LB_DEV void miller_add_step(g2proj& T, const fp2& xq, const fp2& yq, fp2& l0, fp
 }
 
 // f = f_{|x|,Q}(P), conjugated (x < 0).  P, Q affine, not infinity.
-LB_NOINL void miller_loop(fp12& f, const g1a& P, const g2a& Q) {
+LB_TOWER void miller_loop(fp12& f, const g1a& P, const g2a& Q) {
   g2proj T;
   T.X = Q.x;
   T.Y = Q.y;
@@ -122,7 +122,7 @@ LB_NOINL void miller_loop(fp12& f, const g1a& P, const g2a& Q) {
 }
 
 // a^x for the (negative) BLS parameter, a in the cyclotomic subgroup (so a^-1 = conj(a))
-LB_NOINL void fp12_exp_x(fp12& r, const fp12& a) {
+LB_TOWER void fp12_exp_x(fp12& r, const fp12& a) {
   fp12 acc = a;
   for (int i = 62; i >= 0; i--) {
     fp12_cyc_sqr(acc, acc);
@@ -132,7 +132,7 @@ LB_NOINL void fp12_exp_x(fp12& r, const fp12& a) {
 }
 
 // f^(3 (p^12 - 1)/r)
-LB_NOINL void final_exp(fp12& r, const fp12& f) {
+LB_TOWER void final_exp(fp12& r, const fp12& f) {
   fp12 t0, t1, f2, a, b, c;
   // easy part: f^(p^6 - 1) then ^(p^2 + 1)
   fp12_conj(t0, f);
