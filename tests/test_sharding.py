@@ -1,0 +1,91 @@
+"""Multi-GPU sharding logic on CPU: shard boundaries, in-process fan-out, and a
+world_size-2 torch.distributed (gloo) run whose verdicts equal the unsharded ones."""
+import os
+import random
+
+import pytest
+import torch.multiprocessing as mp
+
+from lodestar_amd.sharding import ShardedVerifier, shard_requests, verify_distributed
+
+
+class TableBackend:
+    """Deterministic stand-in for a GPU: a request is valid iff none of its
+    sets is marked bad (the verdict rule verify_requests implements)."""
+
+    def __init__(self):
+        self.seen = []
+
+    def verify_requests(self, requests):
+        self.seen.append([r[0]["id"] if r else None for r in requests])
+        return [bool(r) and all(not s["bad"] for s in r) for r in requests], \
+               [1 if any(s.get("empty_agg") for s in r) else 0 for r in requests]
+
+
+def make_requests(seed=0, n=37):
+    rnd = random.Random(seed)
+    reqs, k = [], 0
+    for _ in range(n):
+        size = rnd.choice([0, 1, 2, 5, 128, 3])
+        reqs.append([{"id": k + j, "bad": rnd.random() < 0.05, "empty_agg": rnd.random() < 0.01}
+                     for j in range(size)])
+        k += size
+    return reqs
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 4, 8])
+def test_shards_cover_every_request_once(shards):
+    sizes = [len(r) for r in make_requests(1)]
+    sh = shard_requests(sizes, shards)
+    assert len(sh) == shards
+    assert sh[0][0] == 0 and sh[-1][1] == len(sizes)
+    for (a, b), (c, d) in zip(sh, sh[1:]):
+        assert b == c and a <= b
+    total = sum(sizes)
+    for a, b in sh:  # balance: no shard above its fair share by more than one request
+        assert sum(sizes[a:b]) <= total / shards + max(sizes)
+
+
+def test_shard_more_shards_than_requests():
+    sh = shard_requests([3, 4], 8)
+    assert sum(b - a for a, b in sh) == 2
+
+
+def test_sharded_verifier_equals_single():
+    reqs = make_requests(2)
+    single = TableBackend().verify_requests(reqs)
+    backs = [TableBackend() for _ in range(4)]
+    assert ShardedVerifier(backs).verify_requests(reqs) == single
+    assert sum(len(b.seen) for b in backs) >= 1
+
+
+def _worker(rank, world, port, reqs, out_q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = TableBackend()
+    v, e = verify_distributed(reqs, b.verify_requests, rank, world)
+    out_q.put((rank, v, e, b.seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_verify_distributed_gloo_world2():
+    reqs = make_requests(3)
+    want = TableBackend().verify_requests(reqs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + random.Random(os.getpid()).randrange(2000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, reqs, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = shard_requests([len(r) for r in reqs], 2)
+    for rank, v, e, seen in res:
+        assert (v, e) == want
+        lo, hi = shards[rank]
+        assert len(seen[0]) == hi - lo  # each rank verified only its own shard

@@ -1,0 +1,199 @@
+"""BlsGpuVerifier scheduling semantics on CPU with a mock backend (the pattern
+of the reference's test/mocks/mockedBls.ts): chunking, buffering, priority,
+same-message flattening, rejection rules, close()."""
+import asyncio
+
+import pytest
+
+from lodestar_amd.native import EmptyAggregateError
+from lodestar_amd.verifier import (MAX_BUFFER_WAIT_MS, BlsGpuVerifier, PublicKey, QueueError, VerifySignatureOpts,
+                                   aggregate_set, chunkify_maximize_chunk_size, single_set)
+
+GOOD = b"\x01" * 96
+BAD = b"\x02" * 96
+PK = PublicKey(bytes(96))
+
+
+class MockBackend:
+    """valid iff every set carries GOOD; zero-pubkey aggregate -> error 1."""
+
+    def __init__(self):
+        self.dispatches = []
+        self.same_message_calls = []
+
+    def verify_requests(self, requests):
+        self.dispatches.append([len(r) for r in requests])
+        valid, errs = [], []
+        for r in requests:
+            empty = any(s.pubkeys is not None and len(s.pubkeys) == 0 for s in r)
+            errs.append(1 if empty else 0)
+            valid.append(bool(r) and all(s.signature == GOOD for s in r))
+        return valid, errs
+
+    def verify_same_message(self, pubkeys, signatures, message):
+        self.same_message_calls.append(len(signatures))
+        return [s == GOOD for s in signatures]
+
+
+def sets(n, bad=()):
+    return [single_set(PK, bytes([i % 256]) * 32, BAD if i in bad else GOOD) for i in range(n)]
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def test_chunkify_matches_reference():
+    assert [len(c) for c in chunkify_maximize_chunk_size(list(range(300)), 128)] == [150, 150]
+    assert [len(c) for c in chunkify_maximize_chunk_size(list(range(100)), 128)] == [100]
+
+
+def test_verify_all_valid_and_one_invalid():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        assert await v.verify_signature_sets(sets(3)) is True
+        assert await v.verify_signature_sets(sets(3, bad={1})) is False
+        await v.close()
+    run(main())
+
+
+def test_large_call_is_chunked_into_jobs_of_le_128():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        assert await v.verify_signature_sets(sets(300)) is True
+        assert sorted(x for d in b.dispatches for x in d) == [150, 150]
+        await v.close()
+    run(main())
+
+
+def test_batchable_calls_are_buffered_and_merged():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        opts = VerifySignatureOpts(batchable=True)
+        r = await asyncio.gather(v.verify_signature_sets(sets(3), opts), v.verify_signature_sets(sets(4), opts),
+                                 v.verify_signature_sets(sets(2, bad={0}), opts))
+        assert r == [True, True, False]
+        assert b.dispatches == [[3, 4, 2]]  # one package, three verdicts
+        await v.close()
+    run(main())
+
+
+def test_buffer_flushes_above_32_sigs_without_waiting():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        assert await v.verify_signature_sets(sets(33), VerifySignatureOpts(batchable=True))
+        assert loop.time() - t0 < MAX_BUFFER_WAIT_MS / 1000 / 2
+        await v.close()
+    run(main())
+
+
+def test_batchable_waits_for_buffer_timeout():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        assert await v.verify_signature_sets(sets(2), VerifySignatureOpts(batchable=True))
+        assert loop.time() - t0 >= MAX_BUFFER_WAIT_MS / 1000 * 0.9
+        await v.close()
+    run(main())
+
+
+def test_priority_jobs_run_first():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b], max_sets_per_dispatch=1)
+        v._idle = []  # hold dispatch until both are queued
+        f1 = asyncio.ensure_future(v.verify_signature_sets(sets(2)))
+        f2 = asyncio.ensure_future(v.verify_signature_sets(sets(5), VerifySignatureOpts(priority=True)))
+        await asyncio.sleep(0.01)
+        v._idle = [0]
+        v._run_job()
+        await asyncio.gather(f1, f2)
+        assert b.dispatches[0] == [5]
+        await v.close()
+    run(main())
+
+
+def test_empty_aggregate_rejects_the_job():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        with pytest.raises(EmptyAggregateError):
+            await v.verify_signature_sets([aggregate_set([], bytes(32), GOOD)])
+        await v.close()
+    run(main())
+
+
+def test_empty_sets_are_false_like_reference():
+    """chunkify([]) -> [[]] -> one job of 0 sets -> maybeBatch throws "Empty
+    signature set" -> caught -> false (index.ts:191-213, maybeBatch.ts:31-33)."""
+    async def main():
+        v = BlsGpuVerifier(backends=[MockBackend()])
+        assert await v.verify_signature_sets([]) is False
+        await v.close()
+    run(main())
+
+
+def test_same_message_flattens_chunks():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        pairs = [(PK, GOOD)] * 299 + [(PK, BAD)]
+        out = await v.verify_signature_sets_same_message(pairs, bytes(32))
+        assert out == [True] * 299 + [False]
+        assert sorted(b.same_message_calls) == [150, 150]  # chunkify(300, 128)
+        assert await v.verify_signature_sets_same_message([], bytes(32)) == []
+        await v.close()
+    run(main())
+
+
+def test_verify_on_main_thread_is_synchronous():
+    async def main():
+        b = MockBackend()
+        v = BlsGpuVerifier(backends=[b])
+        assert await v.verify_signature_sets(sets(2), VerifySignatureOpts(verify_on_main_thread=True))
+        assert b.dispatches == [[2]]
+        await v.close()
+    run(main())
+
+
+def test_close_rejects_queued_jobs_and_new_work():
+    async def main():
+        v = BlsGpuVerifier(backends=[MockBackend()])
+        fut = asyncio.ensure_future(v.verify_signature_sets(sets(2), VerifySignatureOpts(batchable=True)))
+        await asyncio.sleep(0)
+        await v.close()
+        with pytest.raises(QueueError):
+            await fut
+        with pytest.raises(QueueError):
+            await v.verify_signature_sets(sets(1))
+    run(main())
+
+
+def test_can_accept_work():
+    async def main():
+        v = BlsGpuVerifier(backends=[MockBackend()])
+        assert v.can_accept_work()
+        v._idle = []
+        assert not v.can_accept_work()
+        v._idle = [0]
+        await v.close()
+    run(main())
+
+
+def test_multiple_backends_share_load():
+    async def main():
+        bs = [MockBackend(), MockBackend()]
+        v = BlsGpuVerifier(backends=bs, max_sets_per_dispatch=128)
+        r = await asyncio.gather(*[v.verify_signature_sets(sets(128)) for _ in range(6)])
+        assert all(r)
+        assert all(len(b.dispatches) > 0 for b in bs)
+        await v.close()
+    run(main())
