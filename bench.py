@@ -111,10 +111,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
+        dist.init_process_group("gloo")  # barrier + max-over-ranks only; no data-path collective
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)  # one process per GPU; ranks > devices only when rehearsing
+    torch.cuda.set_device(gpu)
     from lodestar_amd.native import Device
-    dev = Device(local)
+    dev = Device(gpu)
 
     n = a.sets
     seed = hashlib.sha256(b"lodestar-mi355x-bench").digest()
@@ -122,7 +124,7 @@ def main():
     sks, pks, msgs, sigs = make_workload(dev, n, rank * n, seed)
     t_gen = time.time() - t_gen
 
-    cuda = torch.device("cuda", local)
+    cuda = torch.device("cuda", gpu)
     d_pk = torch.from_numpy(np.frombuffer(b"".join(pks), np.uint8).copy()).to(cuda)
     d_msg = torch.from_numpy(np.frombuffer(b"".join(msgs), np.uint8).copy()).to(cuda)
     d_sig = torch.from_numpy(np.frombuffer(b"".join(sigs), np.uint8).copy()).to(cuda)
