@@ -9,7 +9,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liblodestar_bls.so")
-SOURCES = ["bls_kernels.hip", "bls_field.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h", "gen_constants.py"]
+# one translation unit per stage group, compiled in parallel and linked into one .so
+UNITS = ["k_final.hip", "k_pairing.hip", "k_aux.hip", "k_hash.hip", "k_miller.hip", "k_scalar.hip", "k_sets.hip",
+         "k_prod.hip", "bls_host.hip"]
+HEADERS = ["bls_kernels.h", "bls_field.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h", "gen_constants.py"]
+SOURCES = UNITS + HEADERS + ["bls_all.hip"]
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
 HEADER = os.path.join(ROOT, "include", "lodestar_bls.h")
 ARCH = os.environ.get("LB_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -28,19 +33,48 @@ def gen_constants() -> str:
     return out
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC"]
+
+
 def hipcc_cmd(out: str, extra=()) -> list:
-    return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-            "-o", out, os.path.join(CSRC, "bls_kernels.hip"), *extra]
+    """Single-TU build of the whole library (op-counting variant)."""
+    return [HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-shared", "-o", out, os.path.join(CSRC, "bls_all.hip"), *extra]
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def _unit_deps_mtime(unit: str) -> float:
+    paths = [os.path.join(CSRC, unit)] + [os.path.join(CSRC, h) for h in HEADERS] + [HEADER]
+    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
+    """Compile every unit for gfx950 (in parallel, each unit only when stale) and link the .so."""
     gen_constants()
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_source_mtime():
         return LIB
-    cmd = hipcc_cmd(LIB + ".tmp")
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    objs, todo = [], []
+    for u in UNITS:
+        o = os.path.join(OBJ_DIR, os.path.splitext(u)[0] + ".o")
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < _unit_deps_mtime(u):
+            todo.append([HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-c", "-o", o, os.path.join(CSRC, u)])
+    jobs = jobs or max(1, min(len(todo), os.cpu_count() or 1, 16))
+    procs = []
+    for cmd in todo:
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((cmd, subprocess.Popen(cmd)))
+        while sum(p.poll() is None for _, p in procs) >= jobs:
+            procs[0][1].wait() if procs[0][1].poll() is None else None
+            import time
+            time.sleep(0.2)
+    failed = [c for c, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError("hipcc failed: " + " | ".join(" ".join(c) for c in failed))
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+        print(" ".join(link), flush=True)
+    subprocess.check_call(link)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

@@ -25,457 +25,9 @@
 #include <string>
 #include <vector>
 
-#include "../../include/lodestar_bls.h"
-#include "bls_pairing.h"
+#include "bls_kernels.h"
 
 using namespace lb;
-
-#define LB_ST_ZERO_SIGNATURE 6
-
-// ============================================================================
-// Kernels
-// ============================================================================
-static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at high VGPR counts
-// min waves per SIMD for the heavy per-lane kernels: 1 = 512-register budget
-// (256 VGPR + 256 AGPR), which keeps the inlined tower arithmetic spill-free
-#ifndef LB_HEAVY_WAVES
-#define LB_HEAVY_WAVES 1
-#endif
-
-__global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                   uint8_t* __restrict__ single_flag) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  const uint32_t a = req_off[k], b = req_off[k + 1];
-  for (uint32_t i = a; i < b; i++) single_flag[i] = (b - a == 1) ? 1 : 0;
-}
-
-// Signature.fromBytes(validate=true); for single-set requests also the
-// ZeroSignatureError of @chainsafe/bls Signature.verify.
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
-                                                     const uint32_t* __restrict__ sig_off,
-                                                     const uint8_t* __restrict__ single_flag,
-                                                     g2j* __restrict__ out_sig, uint8_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t a = sig_off[i], b = sig_off[i + 1];
-  g2a s;
-  uint8_t st = g2_deserialize(s, sigs + a, b - a);
-  g2j sj;
-  jac_set_inf(sj);
-  if (st == LB_ST_OK) {
-    jac_from_aff(sj, s);
-    if (!g2_in_subgroup(sj)) st = LB_ST_NOT_IN_GROUP;
-    else if (single_flag && single_flag[i] && s.inf) st = LB_ST_ZERO_SIGNATURE;
-  }
-  out_sig[i] = sj;
-  status[i] = st;
-}
-
-// Sets with exactly one pubkey (the common case): one lane per set.
-__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
-                                                        const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
-                                                        uint8_t* __restrict__ pk_status) {
-  const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
-  if (set >= n_sets) return;
-  const uint32_t a = pk_off ? pk_off[set] : set, b = pk_off ? pk_off[set + 1] : set + 1;
-  if (b - a > 1) return;  // aggregate: k_pubkeys_agg
-  g1j acc;
-  jac_set_inf(acc);
-  uint8_t st = LB_ST_EMPTY_AGGREGATE;
-  if (b == a + 1) {
-    g1a p;
-    st = g1_deserialize(p, pks + (size_t)a * 96, 96);
-    if (st == LB_ST_OK) {
-      jac_from_aff(acc, p);
-      if (p.inf) st = LB_ST_PK_INFINITY;
-    } else {
-      st = LB_ST_BAD_ENCODING;
-    }
-  }
-  out_pk[set] = acc;
-  pk_status[set] = st;
-}
-
-// Sets with >= 2 pubkeys (PublicKey.aggregate, chain/bls/utils.ts:13): one
-// wave per set, grid-stride over sets; lanes decode strided, LDS tree sum.
-__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
-                                                     const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
-                                                     uint8_t* __restrict__ pk_status) {
-  __shared__ g1j sh[TPB];
-  __shared__ uint32_t bad;
-  if (!pk_off) return;
-  for (uint32_t set = blockIdx.x; set < n_sets; set += gridDim.x) {
-    const uint32_t a = pk_off[set], b = pk_off[set + 1];
-    if (b - a <= 1) continue;  // uniform across the block
-    if (threadIdx.x == 0) bad = 0;
-    __syncthreads();
-    g1j acc;
-    jac_set_inf(acc);
-    for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
-      g1a p;
-      const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
-      if (st != LB_ST_OK) {
-        atomicOr(&bad, 1u);
-      } else {
-        jac_add_aff(acc, acc, p);
-      }
-    }
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = TPB / 2; s > 0; s >>= 1) {
-      if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-        g1j o = sh[threadIdx.x + s];
-        g1j m = sh[threadIdx.x];
-        jac_add(m, m, o);
-        sh[threadIdx.x] = m;
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      out_pk[set] = sh[0];
-      pk_status[set] = bad ? LB_ST_BAD_ENCODING : jac_is_inf(sh[0]) ? LB_ST_PK_INFINITY : LB_ST_OK;
-    }
-    __syncthreads();
-  }
-}
-
-// hash_to_G2, first half: lane 2i+j maps u_j of message i (SSWU + 3-isogeny)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
-                                                   g2j* __restrict__ q) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * n) return;
-  uint8_t m[32];
-  const uint8_t* src = msgs + (size_t)(t >> 1) * 32;
-  for (int k = 0; k < 32; k++) m[k] = src[k];
-  g2j r;
-  hash_to_g2_half(r, m, (int)(t & 1));
-  q[t] = r;
-}
-// hash_to_G2, second half: Q0 + Q1, clear cofactor, affine
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
-  hash_to_g2_finish(h, q0, q1);
-  g2a ha;
-  jac_to_aff(ha, h);
-  out_h[i] = ha;
-}
-
-// r_i sig_i
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
-                                                    const g2j* __restrict__ sig,
-                                                    const uint8_t* __restrict__ sig_status,
-                                                    g2j* __restrict__ rsig) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2j rs;
-  jac_set_inf(rs);
-  if (sig_status[i] == LB_ST_OK) {
-    uint8_t sd[32];
-    for (int k = 0; k < 32; k++) sd[k] = seed[k];
-    const uint64_t r = batch_scalar(sd, i);
-    g2j s = sig[i];
-    jac_mul_u64(rs, s, r);
-  }
-  rsig[i] = rs;
-}
-
-// r_i pk_i (affine); core-verify pubkey subgroup check for single-set requests
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
-                                                   const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
-                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t st = pk_status[i];
-  g1j p = pk[i];
-  if (st == LB_ST_OK && single_flag[i] && !g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
-  g1a pa;
-  fp_zero(pa.x);
-  fp_zero(pa.y);
-  pa.inf = true;
-  if (st == LB_ST_OK) {
-    uint8_t sd[32];
-    for (int k = 0; k < 32; k++) sd[k] = seed[k];
-    const uint64_t r = batch_scalar(sd, i);
-    g1j rp;
-    jac_mul_u64(rp, p, r);
-    jac_to_aff(pa, rp);
-  }
-  rpk[i] = pa;
-  pk_status[i] = st;
-}
-
-// S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S) {
-  __shared__ g2j sh[TPB];
-  const uint32_t k = blockIdx.x;
-  if (k >= n_req) return;
-  const uint32_t a = req_off[k], b = req_off[k + 1];
-  g2j acc;
-  jac_set_inf(acc);
-  for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
-    g2j t = rsig[i];
-    jac_add(acc, acc, t);
-  }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = TPB / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-      g2j m = sh[threadIdx.x], o = sh[threadIdx.x + s];
-      jac_add(m, m, o);
-      sh[threadIdx.x] = m;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    g2j tot = sh[0];
-    g2a sa;
-    jac_to_aff(sa, tot);
-    S[k] = sa;
-  }
-}
-
-// f_S[k] = Miller(-g1, S_k)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  fp12 r;
-  fp12_one(r);
-  g2a q = S[k];
-  if (!q.inf) {
-    g1a g;
-    fp_set(g.x, LB_G1_X);
-    fp_set(g.y, LB_G1_NEG_Y);
-    g.inf = false;
-    miller_loop(r, g, q);
-  }
-  fS[k] = r;
-}
-
-// f_i = Miller(r_i pk_i, H(m_i))
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
-                                                     fp12* __restrict__ f) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fp12 r;
-  fp12_one(r);
-  g1a p = rpk[i];
-  g2a q = h[i];
-  if (!p.inf && !q.inf) miller_loop(r, p, q);
-  f[i] = r;
-}
-
-// F_k = f_S[k] * prod f_i, request status and errors: one wave per request
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                   const fp12* __restrict__ f, const fp12* __restrict__ fS,
-                                                   const uint8_t* __restrict__ sig_status,
-                                                   const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
-                                                   uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err) {
-  __shared__ fp12 sh[TPB];
-  __shared__ uint32_t bad, err_empty, err_pk;
-  const uint32_t k = blockIdx.x;
-  if (k >= n_req) return;
-  const uint32_t a = req_off[k], b = req_off[k + 1];
-  if (threadIdx.x == 0) {
-    bad = (a == b) ? 1u : 0u;
-    err_empty = 0;
-    err_pk = 0;
-  }
-  __syncthreads();
-  fp12 acc;
-  fp12_one(acc);
-  bool first = true;
-  for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
-    const uint8_t ss = sig_status[i], ps = pk_status[i];
-    if (ss != LB_ST_OK || ps != LB_ST_OK) atomicOr(&bad, 1u);
-    if (ps == LB_ST_EMPTY_AGGREGATE) atomicOr(&err_empty, 1u);
-    if (ps == LB_ST_BAD_ENCODING) atomicOr(&err_pk, 1u);
-    fp12 t = f[i];
-    if (first) {
-      acc = t;
-      first = false;
-    } else {
-      fp12_mul(acc, acc, t);
-    }
-  }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = TPB / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-      fp12 m = sh[threadIdx.x], o = sh[threadIdx.x + s];
-      fp12_mul(m, m, o);
-      sh[threadIdx.x] = m;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    fp12 tot = sh[0], s = fS[k];
-    fp12_mul(tot, tot, s);
-    F[k] = tot;
-    req_bad[k] = bad ? 1 : 0;
-    req_err[k] = err_empty ? LB_REQ_EMPTY_AGGREGATE : err_pk ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
-  }
-}
-
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_final(uint32_t n_req, const fp12* __restrict__ F,
-                                               const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
-  if (req_bad[k]) {
-    valid[k] = 0;
-    return;
-  }
-  fp12 acc = F[k], r;
-  final_exp(r, acc);
-  valid[k] = fp12_is_one(r) ? 1 : 0;
-}
-
-// ---- hash_to_G2 in one lane (stage-level API) ------------------------------
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t m[32];
-  for (int k = 0; k < 32; k++) m[k] = msgs[(size_t)i * 32 + k];
-  g2j h;
-  hash_to_g2(h, m);
-  g2a ha;
-  jac_to_aff(ha, h);
-  out_h[i] = ha;
-}
-
-// ---- generic point sums (one workgroup, LDS tree) ------------------------
-template <class F>
-__global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out) {
-  __shared__ jac<F> sh[256];
-  jac<F> acc;
-  jac_set_inf(acc);
-  for (uint32_t i = threadIdx.x; i < n; i += 256) {
-    jac<F> t = in[i];
-    jac_add(acc, acc, t);
-  }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      jac<F> m = sh[threadIdx.x], o = sh[threadIdx.x + s];
-      jac_add(m, m, o);
-      sh[threadIdx.x] = m;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = sh[0];
-}
-
-__global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g1j p = in[i];
-  g1a a;
-  jac_to_aff(a, p);
-  g1_serialize(out96 + (size_t)i * 96, a);
-}
-__global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* __restrict__ out192) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2j p = in[i];
-  g2a a;
-  jac_to_aff(a, p);
-  g2_serialize(out192 + (size_t)i * 192, a);
-}
-__global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2a a = in[i];
-  g2_serialize(out192 + (size_t)i * 192, a);
-}
-
-// ---- stage-level kernels for parity tests ---------------------------------
-__global__ void k_pairing(uint32_t n, const uint8_t* __restrict__ g1b, const uint8_t* __restrict__ g2b,
-                          uint8_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g1a p;
-  g2a q;
-  const uint8_t s1 = g1_deserialize(p, g1b + (size_t)i * 96, 96);
-  const uint8_t s2 = g2_deserialize(q, g2b + (size_t)i * 192, 192);
-  fp12 f, r;
-  fp12_one(f);
-  if (s1 == LB_ST_OK && s2 == LB_ST_OK && !p.inf && !q.inf) miller_loop(f, p, q);
-  final_exp(r, f);
-  uint8_t* o = out + (size_t)i * 576;
-  const fp2* c[6] = {&r.c0.c0, &r.c0.c1, &r.c0.c2, &r.c1.c0, &r.c1.c1, &r.c1.c2};
-  for (int k = 0; k < 6; k++) {
-    fp_write_be(o + 96 * k, c[k]->c0);
-    fp_write_be(o + 96 * k + 48, c[k]->c1);
-  }
-}
-__global__ void k_scalars(const uint8_t* __restrict__ seed, uint32_t first, uint32_t n, uint64_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t sd[32];
-  for (int k = 0; k < 32; k++) sd[k] = seed[k];
-  out[i] = batch_scalar(sd, first + i);
-}
-__global__ void k_g1_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
-                         uint8_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g1a a;
-  g1_deserialize(a, in + (size_t)i * 96, 96);
-  g1j p, r;
-  jac_from_aff(p, a);
-  jac_mul_u64(r, p, k[i]);
-  jac_to_aff(a, r);
-  g1_serialize(out + (size_t)i * 96, a);
-}
-__global__ void k_g2_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
-                         uint8_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2a a;
-  g2_deserialize(a, in + (size_t)i * 192, 192);
-  g2j p, r;
-  jac_from_aff(p, a);
-  jac_mul_u64(r, p, k[i]);
-  jac_to_aff(a, r);
-  g2_serialize(out + (size_t)i * 192, a);
-}
-
-// ---- synthetic data generation (bench / tests): SecretKey.toPublicKey, sign --
-__global__ void __launch_bounds__(TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32,
-                                                  uint8_t* __restrict__ out96) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t k[32];
-  for (int b = 0; b < 32; b++) k[b] = sk32[(size_t)i * 32 + b];
-  g1j g, r;
-  fp_set(g.X, LB_G1_X);
-  fp_set(g.Y, LB_G1_Y);
-  fp_one(g.Z);
-  jac_mul_be32(r, g, k);
-  g1a a;
-  jac_to_aff(a, r);
-  g1_serialize(out96 + (size_t)i * 96, a);
-}
-__global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sk32,
-                                              const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t k[32], m[32];
-  for (int b = 0; b < 32; b++) {
-    k[b] = sk32[(size_t)i * 32 + b];
-    m[b] = msgs[(size_t)i * 32 + b];
-  }
-  g2j h, r;
-  hash_to_g2(h, m);
-  jac_mul_be32(r, h, k);
-  g2a a;
-  jac_to_aff(a, r);
-  g2_compress(out96 + (size_t)i * 96, a);
-}
 
 #ifdef LB_COUNT_OPS
 static unsigned long long opcount_read_reset() {

@@ -1,0 +1,77 @@
+// Shared declarations of the verification kernels (defined in k_*.hip, one
+// translation unit per stage group so the build compiles them in parallel;
+// bls_all.hip is the single-TU build used for the op-counting variant).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/lodestar_bls.h"
+#include "bls_pairing.h"
+
+#include "bls_pairing.h"
+
+
+#define LB_ST_ZERO_SIGNATURE 6
+
+// ============================================================================
+// Kernels
+// ============================================================================
+static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at high VGPR counts
+// min waves per SIMD for the heavy per-lane kernels: 1 = 512-register budget
+// (256 VGPR + 256 AGPR), which keeps the inlined tower arithmetic spill-free
+#ifndef LB_HEAVY_WAVES
+#define LB_HEAVY_WAVES 1
+#endif
+
+namespace lb {
+__global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   uint8_t* __restrict__ single_flag);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint32_t* __restrict__ sig_off,
+                                                     const uint8_t* __restrict__ single_flag,
+                                                     g2j* __restrict__ out_sig, uint8_t* __restrict__ status);
+__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                        const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                        uint8_t* __restrict__ pk_status);
+__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                     const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                     uint8_t* __restrict__ pk_status);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                   g2j* __restrict__ q);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+                                                    const g2j* __restrict__ sig,
+                                                    const uint8_t* __restrict__ sig_status,
+                                                    g2j* __restrict__ rsig);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+                                                   const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
+                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+                                                     fp12* __restrict__ f);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   const fp12* __restrict__ f, const fp12* __restrict__ fS,
+                                                   const uint8_t* __restrict__ sig_status,
+                                                   const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
+                                                   uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_final(uint32_t n_req, const fp12* __restrict__ F,
+                                               const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h);
+template <class F>
+__global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out);
+__global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96);
+__global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* __restrict__ out192);
+__global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192);
+__global__ void k_pairing(uint32_t n, const uint8_t* __restrict__ g1b, const uint8_t* __restrict__ g2b,
+                          uint8_t* __restrict__ out);
+__global__ void k_scalars(const uint8_t* __restrict__ seed, uint32_t first, uint32_t n, uint64_t* __restrict__ out);
+__global__ void k_g1_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out);
+__global__ void k_g2_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out);
+__global__ void __launch_bounds__(TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32,
+                                                  uint8_t* __restrict__ out96);
+__global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sk32,
+                                              const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96);
+}  // namespace lb

@@ -1,0 +1,122 @@
+// Helper kernels: point sums, serialization, stage-level parity kernels, synthetic signer.
+// Part of the MI355X BLS verification pipeline; see bls_host.hip for the DAG.
+#include "bls_kernels.h"
+
+namespace lb {
+
+// ---- generic point sums (one workgroup, LDS tree) ------------------------
+template <class F>
+__global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out) {
+  __shared__ jac<F> sh[256];
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    jac<F> t = in[i];
+    jac_add(acc, acc, t);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      jac<F> m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      jac_add(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sh[0];
+}
+
+__global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1j p = in[i];
+  g1a a;
+  jac_to_aff(a, p);
+  g1_serialize(out96 + (size_t)i * 96, a);
+}
+__global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* __restrict__ out192) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j p = in[i];
+  g2a a;
+  jac_to_aff(a, p);
+  g2_serialize(out192 + (size_t)i * 192, a);
+}
+__global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a a = in[i];
+  g2_serialize(out192 + (size_t)i * 192, a);
+}
+
+// ---- stage-level kernels for parity tests ---------------------------------
+__global__ void k_scalars(const uint8_t* __restrict__ seed, uint32_t first, uint32_t n, uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t sd[32];
+  for (int k = 0; k < 32; k++) sd[k] = seed[k];
+  out[i] = batch_scalar(sd, first + i);
+}
+__global__ void k_g1_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a a;
+  g1_deserialize(a, in + (size_t)i * 96, 96);
+  g1j p, r;
+  jac_from_aff(p, a);
+  jac_mul_u64(r, p, k[i]);
+  jac_to_aff(a, r);
+  g1_serialize(out + (size_t)i * 96, a);
+}
+__global__ void k_g2_mul(uint32_t n, const uint8_t* __restrict__ in, const uint64_t* __restrict__ k,
+                         uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a a;
+  g2_deserialize(a, in + (size_t)i * 192, 192);
+  g2j p, r;
+  jac_from_aff(p, a);
+  jac_mul_u64(r, p, k[i]);
+  jac_to_aff(a, r);
+  g2_serialize(out + (size_t)i * 192, a);
+}
+
+// ---- synthetic data generation (bench / tests): SecretKey.toPublicKey, sign --
+__global__ void __launch_bounds__(TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32,
+                                                  uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t k[32];
+  for (int b = 0; b < 32; b++) k[b] = sk32[(size_t)i * 32 + b];
+  g1j g, r;
+  fp_set(g.X, LB_G1_X);
+  fp_set(g.Y, LB_G1_Y);
+  fp_one(g.Z);
+  jac_mul_be32(r, g, k);
+  g1a a;
+  jac_to_aff(a, r);
+  g1_serialize(out96 + (size_t)i * 96, a);
+}
+__global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sk32,
+                                              const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t k[32], m[32];
+  for (int b = 0; b < 32; b++) {
+    k[b] = sk32[(size_t)i * 32 + b];
+    m[b] = msgs[(size_t)i * 32 + b];
+  }
+  g2j h, r;
+  hash_to_g2(h, m);
+  jac_mul_be32(r, h, k);
+  g2a a;
+  jac_to_aff(a, r);
+  g2_compress(out96 + (size_t)i * 96, a);
+}
+
+template __global__ void k_jac_sum<fp>(uint32_t, const jac<fp>* __restrict__, jac<fp>* __restrict__);
+template __global__ void k_jac_sum<fp2>(uint32_t, const jac<fp2>* __restrict__, jac<fp2>* __restrict__);
+
+}  // namespace lb

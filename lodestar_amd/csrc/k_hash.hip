@@ -1,0 +1,43 @@
+// hash_to_G2 stages (two lanes per message, then finish), and the one-lane variant.
+// Part of the MI355X BLS verification pipeline; see bls_host.hip for the DAG.
+#include "bls_kernels.h"
+
+namespace lb {
+
+// hash_to_G2, first half: lane 2i+j maps u_j of message i (SSWU + 3-isogeny)
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                   g2j* __restrict__ q) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n) return;
+  uint8_t m[32];
+  const uint8_t* src = msgs + (size_t)(t >> 1) * 32;
+  for (int k = 0; k < 32; k++) m[k] = src[k];
+  g2j r;
+  hash_to_g2_half(r, m, (int)(t & 1));
+  q[t] = r;
+}
+// hash_to_G2, second half: Q0 + Q1, clear cofactor, affine
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
+  hash_to_g2_finish(h, q0, q1);
+  g2a ha;
+  jac_to_aff(ha, h);
+  out_h[i] = ha;
+}
+
+// ---- hash_to_G2 in one lane (stage-level API) ------------------------------
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t m[32];
+  for (int k = 0; k < 32; k++) m[k] = msgs[(size_t)i * 32 + k];
+  g2j h;
+  hash_to_g2(h, m);
+  g2a ha;
+  jac_to_aff(ha, h);
+  out_h[i] = ha;
+}
+
+}  // namespace lb

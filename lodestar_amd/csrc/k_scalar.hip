@@ -1,0 +1,82 @@
+// Random-scalar stages: r_i sig_i, r_i pk_i, per-request sum S_k.
+// Part of the MI355X BLS verification pipeline; see bls_host.hip for the DAG.
+#include "bls_kernels.h"
+
+namespace lb {
+
+// r_i sig_i
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+                                                    const g2j* __restrict__ sig,
+                                                    const uint8_t* __restrict__ sig_status,
+                                                    g2j* __restrict__ rsig) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j rs;
+  jac_set_inf(rs);
+  if (sig_status[i] == LB_ST_OK) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    const uint64_t r = batch_scalar(sd, i);
+    g2j s = sig[i];
+    jac_mul_u64(rs, s, r);
+  }
+  rsig[i] = rs;
+}
+
+// r_i pk_i (affine); core-verify pubkey subgroup check for single-set requests
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+                                                   const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
+                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = pk_status[i];
+  g1j p = pk[i];
+  if (st == LB_ST_OK && single_flag[i] && !g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
+  g1a pa;
+  fp_zero(pa.x);
+  fp_zero(pa.y);
+  pa.inf = true;
+  if (st == LB_ST_OK) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    const uint64_t r = batch_scalar(sd, i);
+    g1j rp;
+    jac_mul_u64(rp, p, r);
+    jac_to_aff(pa, rp);
+  }
+  rpk[i] = pa;
+  pk_status[i] = st;
+}
+
+// S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S) {
+  __shared__ g2j sh[TPB];
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
+    g2j t = rsig[i];
+    jac_add(acc, acc, t);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+      g2j m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      jac_add(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    g2j tot = sh[0];
+    g2a sa;
+    jac_to_aff(sa, tot);
+    S[k] = sa;
+  }
+}
+
+}  // namespace lb

@@ -1,0 +1,105 @@
+// Per-set input stages: request flags, signature decode + G2 subgroup check, pubkey decode/aggregation.
+// Part of the MI355X BLS verification pipeline; see bls_host.hip for the DAG.
+#include "bls_kernels.h"
+
+namespace lb {
+
+__global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   uint8_t* __restrict__ single_flag) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  const uint32_t a = req_off[k], b = req_off[k + 1];
+  for (uint32_t i = a; i < b; i++) single_flag[i] = (b - a == 1) ? 1 : 0;
+}
+
+// Signature.fromBytes(validate=true); for single-set requests also the
+// ZeroSignatureError of @chainsafe/bls Signature.verify.
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint32_t* __restrict__ sig_off,
+                                                     const uint8_t* __restrict__ single_flag,
+                                                     g2j* __restrict__ out_sig, uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t a = sig_off[i], b = sig_off[i + 1];
+  g2a s;
+  uint8_t st = g2_deserialize(s, sigs + a, b - a);
+  g2j sj;
+  jac_set_inf(sj);
+  if (st == LB_ST_OK) {
+    jac_from_aff(sj, s);
+    if (!g2_in_subgroup(sj)) st = LB_ST_NOT_IN_GROUP;
+    else if (single_flag && single_flag[i] && s.inf) st = LB_ST_ZERO_SIGNATURE;
+  }
+  out_sig[i] = sj;
+  status[i] = st;
+}
+
+// Sets with exactly one pubkey (the common case): one lane per set.
+__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                        const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                        uint8_t* __restrict__ pk_status) {
+  const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
+  if (set >= n_sets) return;
+  const uint32_t a = pk_off ? pk_off[set] : set, b = pk_off ? pk_off[set + 1] : set + 1;
+  if (b - a > 1) return;  // aggregate: k_pubkeys_agg
+  g1j acc;
+  jac_set_inf(acc);
+  uint8_t st = LB_ST_EMPTY_AGGREGATE;
+  if (b == a + 1) {
+    g1a p;
+    st = g1_deserialize(p, pks + (size_t)a * 96, 96);
+    if (st == LB_ST_OK) {
+      jac_from_aff(acc, p);
+      if (p.inf) st = LB_ST_PK_INFINITY;
+    } else {
+      st = LB_ST_BAD_ENCODING;
+    }
+  }
+  out_pk[set] = acc;
+  pk_status[set] = st;
+}
+
+// Sets with >= 2 pubkeys (PublicKey.aggregate, chain/bls/utils.ts:13): one
+// wave per set, grid-stride over sets; lanes decode strided, LDS tree sum.
+__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
+                                                     const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
+                                                     uint8_t* __restrict__ pk_status) {
+  __shared__ g1j sh[TPB];
+  __shared__ uint32_t bad;
+  if (!pk_off) return;
+  for (uint32_t set = blockIdx.x; set < n_sets; set += gridDim.x) {
+    const uint32_t a = pk_off[set], b = pk_off[set + 1];
+    if (b - a <= 1) continue;  // uniform across the block
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    g1j acc;
+    jac_set_inf(acc);
+    for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
+      g1a p;
+      const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
+      if (st != LB_ST_OK) {
+        atomicOr(&bad, 1u);
+      } else {
+        jac_add_aff(acc, acc, p);
+      }
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = TPB / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+        g1j o = sh[threadIdx.x + s];
+        g1j m = sh[threadIdx.x];
+        jac_add(m, m, o);
+        sh[threadIdx.x] = m;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      out_pk[set] = sh[0];
+      pk_status[set] = bad ? LB_ST_BAD_ENCODING : jac_is_inf(sh[0]) ? LB_ST_PK_INFINITY : LB_ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace lb
