@@ -12,7 +12,8 @@ LIB = os.path.join(HERE, "liblodestar_bls.so")
 # one translation unit per stage group, compiled in parallel and linked into one .so
 UNITS = ["k_final.hip", "k_pairing.hip", "k_aux.hip", "k_hash.hip", "k_miller.hip", "k_scalar.hip", "k_sets.hip",
          "k_prod.hip", "bls_host.hip"]
-HEADERS = ["bls_kernels.h", "bls_field.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h", "gen_constants.py"]
+HEADERS = ["bls_kernels.h", "bls_field.h", "bls_fp_ps.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h",
+           "gen_constants.py", "gen_fp_asm.py"]
 SOURCES = UNITS + HEADERS + ["bls_all.hip"]
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 HEADER = os.path.join(ROOT, "include", "lodestar_bls.h")
@@ -26,11 +27,13 @@ def _newest_source_mtime() -> float:
 
 
 def gen_constants() -> str:
-    out = os.path.join(CSRC, "bls_constants.h")
-    gen = os.path.join(CSRC, "gen_constants.py")
-    if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(gen):
-        subprocess.check_call([sys.executable, gen, out])
-    return out
+    """Generated headers: curve constants and the product-scanning field multiply."""
+    for header, script in (("bls_constants.h", "gen_constants.py"), ("bls_fp_ps.h", "gen_fp_asm.py")):
+        out = os.path.join(CSRC, header)
+        gen = os.path.join(CSRC, script)
+        if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(gen):
+            subprocess.check_call([sys.executable, gen, out])
+    return os.path.join(CSRC, "bls_constants.h")
 
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC"]
