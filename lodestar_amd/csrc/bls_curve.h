@@ -268,6 +268,34 @@ LB_DEV void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
   r = acc;
 }
 
+// [a + b lambda]P for the batch-randomness scalar r = a + b lambda (mod r),
+// a, b = the 32-bit halves of the 64-bit DRBG output, lambda = -x^2, given
+// E = [lambda]P (phi(P) on G1, -psi^2(P) on G2; both cost a few products).
+// Straus-Shamir joint double-and-add over 32 bit pairs with the table
+// {O, P, E, P + E}: 32 doublings + 32 additions.  The plain 64-bit
+// double-and-add it replaces ran 64 doublings + 64 additions per wave, since a
+// wave executes an addition as soon as ONE of its lanes has the bit set.
+// The table lives in private memory (dynamic index): 288 B per G2 entry.
+template <class F>
+LB_DEV void jac_mul_glv(jac<F>& r, const jac<F>& p, const jac<F>& e, uint64_t raw) {
+  const uint32_t a = (uint32_t)raw, b = (uint32_t)(raw >> 32);
+  jac<F> tab[4];
+  jac_set_inf(tab[0]);
+  tab[1] = p;
+  tab[2] = e;
+  jac_add(tab[3], p, e);
+  jac<F> acc;
+  jac_set_inf(acc);
+#pragma unroll 1
+  for (int i = 31; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    const uint32_t sel = ((a >> i) & 1u) | (((b >> i) & 1u) << 1);
+    const jac<F> t = tab[sel];
+    jac_add(acc, acc, t);
+  }
+  r = acc;
+}
+
 // [k]P for a 32-byte big-endian scalar (secret keys: SecretKey.fromBytes is BE)
 template <class F>
 LB_DEV void jac_mul_be32(jac<F>& r, const jac<F>& p, const uint8_t k[32]) {
@@ -322,6 +350,20 @@ LB_DEV void g2_psi(g2j& r, const g2j& p) {
   fp2_conj(t, p.Y);
   fp2_mul_const(r.Y, t, LB_PSI_CY);
   fp2_conj(r.Z, p.Z);
+}
+
+// GLV endomorphisms with eigenvalue lambda = -x^2 (mod r) on G1 and G2:
+//   G1: phi(x, y) = (beta x, y)      (the map g1_in_subgroup checks)
+//   G2: -psi^2, since psi = [x] on G2 (the map g2_in_subgroup checks)
+LB_DEV void g1_glv_endo(g1j& r, const g1j& p) {
+  r = p;
+  fp_mul_const(r.X, p.X, LB_G1_BETA);
+}
+LB_DEV void g2_glv_endo(g2j& r, const g2j& p) {
+  g2j t;
+  g2_psi(t, p);
+  g2_psi(t, t);
+  jac_neg(r, t);
 }
 
 // G2 membership: psi(P) == [x]P = -[|x|]P  (Scott 2021; blst POINTonE2_in_G2).

@@ -163,9 +163,43 @@ LB_DEV void hash_to_field_fp2_2(fp2 u[2], const uint8_t msg[32]) {
   fp_from_64be_words(u[1].c1, ub + 48);
 }
 
-// Simplified SWU onto E2': y^2 = x^3 + A'x + B'  (RFC 9380 §6.6.2)
+// Square root in Fp2 when a square root s of the norm N(a) = a0^2 + a1^2 is
+// already known: one Fp exponentiation (fp2_sqrt's second half).  a must be a
+// square; which of the two roots comes out does not matter (callers fix the sign).
+LB_DEV void fp2_sqrt_with_norm_root(fp2& r, const fp2& a, const fp& s) {
+  if (fp_is_zero(a.c1)) {  // a in Fp (probability ~2^-381 on hashed input)
+    fp2 t;
+    fp2_sqrt(t, a);
+    r = t;
+    return;
+  }
+  fp half, t, c, x0, chk, a1c;
+  fp_set(half, LB_HALF);
+  fp_add(t, a.c0, s);
+  fp_mul(t, t, half);
+  fp_pow_p34(c, t);
+  fp_mul(x0, t, c);  // t^((p+1)/4)
+  fp_sqr(chk, x0);
+  fp_mul(a1c, a.c1, c);
+  fp_mul(a1c, a1c, half);
+  const bool direct = fp_eq(chk, t);
+  fp na1c;
+  fp_neg(na1c, a1c);
+  r.c0 = x0;
+  r.c1 = a1c;
+  fp_cmov(r.c0, na1c, !direct);
+  fp_cmov(r.c1, x0, !direct);
+}
+
+// Simplified SWU onto E2': y^2 = x^3 + A'x + B'  (RFC 9380 §6.6.2), branch-free.
+// With x2 = Z u^2 x1, g(x2) = Z^3 u^6 g(x1), so N(g(x2)) = N(Z)^3 N(u)^6 N(g(x1))
+// and N(Z)^3 is a non-square: ONE exponentiation t = N(g(x1))^((p-3)/4) gives
+// the square test of g(x1) and a square root of whichever norm is a square
+//   sqrt N(g(x1)) = N(g(x1)) t,   sqrt N(g(x2)) = N(u)^3 N(Z)^(3(p+1)/4) N(g(x1)) t,
+// and a second one (fp2_sqrt_with_norm_root) finishes the Fp2 root.  Every lane
+// of a wave runs the same instructions (the gx1 / gx2 choice is a select).
 LB_DEV void map_to_curve_sswu(g2a& out, const fp2& u) {
-  fp2 A, B, Z, tv1, tv2, x1, gx1, x, y, t;
+  fp2 A, B, Z, tv1, tv2, x1, x2, gx1, gx2, x, gx, y, t;
   fp2_set(A, LB_SSWU_A);
   fp2_set(B, LB_SSWU_B);
   fp2_set(Z, LB_SSWU_Z);
@@ -173,32 +207,52 @@ LB_DEV void map_to_curve_sswu(g2a& out, const fp2& u) {
   fp2_mul(tv1, Z, tv1);  // Z u^2
   fp2_sqr(tv2, tv1);
   fp2_add(tv2, tv2, tv1);  // Z^2 u^4 + Z u^2
-  if (fp2_is_zero(tv2)) {
-    fp2_set(x1, LB_SSWU_B_OVER_ZA);
-  } else {
-    fp2_inv(t, tv2);
-    fp one;
-    fp_one(one);
-    fp_add(t.c0, t.c0, one);
-    fp2_mul_const(x1, t, LB_SSWU_MINUS_B_OVER_A);
-  }
-  // gx1 = x1^3 + A x1 + B
+  const bool exceptional = fp2_is_zero(tv2);
+  fp2_inv(t, tv2);  // inv(0) = 0
+  fp one;
+  fp_one(one);
+  fp_add(t.c0, t.c0, one);
+  fp2_mul_const(x1, t, LB_SSWU_MINUS_B_OVER_A);
+  fp2 bza;
+  fp2_set(bza, LB_SSWU_B_OVER_ZA);
+  fp2_cmov(x1, bza, exceptional);
+  // gx1 = x1^3 + A x1 + B, x2 = Z u^2 x1, gx2 = x2^3 + A x2 + B
   fp2_sqr(gx1, x1);
   fp2_add(gx1, gx1, A);
   fp2_mul(gx1, gx1, x1);
   fp2_add(gx1, gx1, B);
-  if (fp2_sqrt(y, gx1)) {
-    x = x1;
-  } else {
-    fp2 gx2;
-    fp2_mul(x, tv1, x1);
-    fp2_sqr(gx2, x);
-    fp2_add(gx2, gx2, A);
-    fp2_mul(gx2, gx2, x);
-    fp2_add(gx2, gx2, B);
-    fp2_sqrt(y, gx2);  // guaranteed square when gx1 is not
-  }
-  if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
+  fp2_mul(x2, tv1, x1);
+  fp2_sqr(gx2, x2);
+  fp2_add(gx2, gx2, A);
+  fp2_mul(gx2, gx2, x2);
+  fp2_add(gx2, gx2, B);
+  // norms and the shared exponentiation
+  fp n1, e, chk, s1, s2, nu, nu3, c1;
+  fp_sqr(n1, gx1.c0);
+  fp_sqr(e, gx1.c1);
+  fp_add(n1, n1, e);
+  fp_pow_p34(e, n1);
+  fp_sqr(chk, e);
+  fp_mul(chk, chk, n1);
+  const bool sq1 = fp_eq(chk, one) || fp_is_zero(n1);
+  fp_mul(s1, n1, e);
+  fp_sqr(nu, u.c0);
+  fp_sqr(e, u.c1);
+  fp_add(nu, nu, e);
+  fp_sqr(nu3, nu);
+  fp_mul(nu3, nu3, nu);
+  fp_set(c1, LB_SSWU_NZ3_SQRT);
+  fp_mul(s2, nu3, c1);
+  fp_mul(s2, s2, s1);
+  x = x1;
+  gx = gx1;
+  fp_cmov(s2, s1, sq1);
+  fp2_cmov(x, x2, !sq1);
+  fp2_cmov(gx, gx2, !sq1);
+  fp2_sqrt_with_norm_root(y, gx, s2);
+  fp2 ny;
+  fp2_neg(ny, y);
+  fp2_cmov(y, ny, fp2_sgn0(u) != fp2_sgn0(y));
   out.x = x;
   out.y = y;
   out.inf = false;
@@ -316,7 +370,10 @@ LB_DEV void hash_to_g2(g2j& r, const uint8_t msg[32]) {
 }
 
 // Deterministic batch randomness (SURVEY.md §8c "Batch
-// randomness"): r_i = LE64(SHA-256(seed[32] || LE32(i))[0..8]), 0 -> 1.
+// randomness"): w_i = LE64(SHA-256(seed[32] || LE32(i))[0..8]), 0 -> 1.
+// The batch scalar is r_i = (w_i mod 2^32) + (w_i >> 32) lambda (mod r),
+// lambda = -x^2: 2^64 distinct values like blst's 64-bit scalars, but applied
+// as a 2 x 32-bit GLV multiplication (jac_mul_glv).
 LB_DEV uint64_t batch_scalar(const uint8_t seed[32], uint32_t idx) {
   uint32_t st[8];
   sha256_init(st);

@@ -4,7 +4,7 @@
 
 namespace lb {
 
-// r_i sig_i
+// r_i sig_i  (r_i = a_i + b_i lambda, jac_mul_glv)
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
@@ -17,8 +17,9 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, 
     uint8_t sd[32];
     for (int k = 0; k < 32; k++) sd[k] = seed[k];
     const uint64_t r = batch_scalar(sd, i);
-    g2j s = sig[i];
-    jac_mul_u64(rs, s, r);
+    g2j s = sig[i], e;
+    g2_glv_endo(e, s);
+    jac_mul_glv(rs, s, e, r);
   }
   rsig[i] = rs;
 }
@@ -40,8 +41,9 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, c
     uint8_t sd[32];
     for (int k = 0; k < 32; k++) sd[k] = seed[k];
     const uint64_t r = batch_scalar(sd, i);
-    g1j rp;
-    jac_mul_u64(rp, p, r);
+    g1j rp, e;
+    g1_glv_endo(e, p);
+    jac_mul_glv(rp, p, e, r);
     jac_to_aff(pa, rp);
   }
   rpk[i] = pa;

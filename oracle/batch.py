@@ -25,10 +25,29 @@ BATCHABLE_MIN_PER_CHUNK = 16        # worker.ts:17
 MAX_SIGNATURE_SETS_PER_JOB = 128    # index.ts:57
 
 
-def batch_scalar(seed: bytes, i: int) -> int:
+# GLV eigenvalue shared by phi on G1 and -psi^2 on G2 (the maps the subgroup
+# checks use): lambda = -x^2 mod r
+GLV_LAMBDA = (-(O.X_PARAM * O.X_PARAM)) % O.R
+
+
+def batch_scalar_raw(seed: bytes, i: int) -> int:
+    """64-bit DRBG output w_i = LE64(SHA-256(seed || LE32(i))[0..8]), 0 -> 1
+    (what the device's lb_batch_scalars returns)."""
     d = hashlib.sha256(bytes(seed) + int(i).to_bytes(4, "little")).digest()
     v = int.from_bytes(d[:8], "little")
     return v if v else 1
+
+
+def batch_scalar(seed: bytes, i: int) -> int:
+    """Batch scalar r_i = (w_i mod 2^32) + (w_i >> 32) * lambda (mod r).
+
+    Like blst's 8 random bytes per set (maybeBatch.ts:19 -> mul_n_aggregate)
+    this takes 2^64 distinct values (a + b lambda with a, b < 2^32 never
+    collide: the lattice {(a, b): a + b lambda = 0 mod r} has no vector shorter
+    than ~2^64), so the small-exponent batch test keeps its 2^-64 soundness;
+    the split lets the device multiply with two 32-bit halves (GLV)."""
+    w = batch_scalar_raw(seed, i)
+    return ((w & 0xFFFFFFFF) + (w >> 32) * GLV_LAMBDA) % O.R
 
 
 class BlsThrow(Exception):

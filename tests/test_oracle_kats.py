@@ -122,8 +122,25 @@ def test_g2_subgroup_check_psi_equivalence():
 
 def test_batch_scalar_drbg():
     seed = bytes(range(32))
-    v = OB.batch_scalar(seed, 5)
-    assert v == int.from_bytes(hashlib.sha256(seed + (5).to_bytes(4, "little")).digest()[:8], "little")
+    w = OB.batch_scalar_raw(seed, 5)
+    assert w == int.from_bytes(hashlib.sha256(seed + (5).to_bytes(4, "little")).digest()[:8], "little")
+    r = OB.batch_scalar(seed, 5)
+    assert r == ((w & 0xFFFFFFFF) + (w >> 32) * OB.GLV_LAMBDA) % O.R
+
+
+def test_glv_eigenvalues():
+    """lambda = -x^2 is the eigenvalue of phi on G1 and of -psi^2 on G2 (the
+    endomorphisms the device's jac_mul_glv uses)."""
+    lam = OB.GLV_LAMBDA
+    assert (lam * lam + lam + 1) % O.R == 0
+    P = O.g1_mul(O.G1, 12345)
+    # the two primitive cube roots of unity mod p; one of them is the device's beta
+    g = next(c for c in range(2, 100) if pow(c, (O.P - 1) // 3, O.P) != 1)
+    w = pow(g, (O.P - 1) // 3, O.P)
+    lam_P = O.g1_mul(P, lam)
+    assert sum((P[0] * b % O.P, P[1]) == lam_P for b in (w, w * w % O.P)) == 1
+    Q = O.g2_mul(O.G2, 6789)
+    assert O.E2.neg(O.psi(O.psi(Q))) == O.g2_mul(Q, lam)
 
 
 def test_chunkify_maximize_chunk_size():
