@@ -92,8 +92,8 @@ def _oracle_verify_batch(batch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=65536)
     ap.add_argument("--per-request", type=int, default=128)
     ap.add_argument("--latency-reps", type=int, default=10)

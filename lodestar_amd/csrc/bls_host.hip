@@ -74,6 +74,13 @@ struct lb_ctx {
   uint64_t next_ticket = 1;
   std::string err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
+  // Miller organisation: one pair per lane (k_miller_sets, lowest latency) for
+  // small calls; stored lines + multi-pair accumulation (k_lines/k_miller_acc)
+  // from lines_min_sets up.  LB_MILLER=lane|lines forces one.
+  int miller_mode = 0;  // 0 auto, 1 lane, 2 lines
+  uint32_t lines_min_sets = 8192;
+  int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
+  int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
   // timing of the last completed verify call
   int n_stages = 0;
   float stage_ms[Slot::kMaxStages] = {};
@@ -194,7 +201,11 @@ int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
 // as a two-stream DAG inside the slot:
 //   A: flags -> pubkeys -> r_i pk_i -> [evPK] -> decode sigs -> r_i sig_i -> S_k (tree)
 //      -> Miller(-g1, S_k) -> [wait B] -> per-request product (tree) -> final exp
-//   B: hash_to_G2 (two lanes per message) -> [wait evPK] -> Miller(r_i pk_i, H_i)
+//   B: hash_to_G2 (two lanes per message) -> [wait evPK] -> lines of (r_i pk_i, H_i)
+// with the Miller values accumulated per request from the stored lines
+// (k_miller_acc, several pairs per lane sharing the Fp12 squarings); the
+// original one-pair-per-lane Miller (k_miller_sets + k_prod_tree) remains
+// selectable with LB_MILLER=lane for comparison.
 int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
                  const uint8_t* d_pks, const uint32_t* d_pk_off, const uint8_t* d_msgs, const uint8_t* d_sigs,
                  const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
@@ -206,7 +217,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2a* d_h = ws.take<g2a>(ns);
   g1j* d_pk = ws.take<g1j>(ns);
   g1a* d_rpk = ws.take<g1a>(ns);
-  fp12* d_f = ws.take<fp12>(ns);
+  const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets);
+  fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);
+  uint32_t* d_lines = by_lines ? ws.take<uint32_t>((size_t)ns * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
   uint8_t* d_pk_st = ws.take<uint8_t>(ns);
   uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
@@ -232,7 +245,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
-  if (n_sets)
+  if (n_sets && by_lines) {
+    if (ctx->lines_waves == 1)
+      LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1a*)d_rpk,
+               (const g2a*)d_h, d_lines);
+    else
+      LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1a*)d_rpk,
+               (const g2a*)d_h, d_lines);
+  }
+  else if (n_sets)
     LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1a*)d_rpk, (const g2a*)d_h,
              d_f);
   if (n_sets) {
@@ -244,15 +265,29 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S);
   LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
   LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
-  LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, (const fp12*)d_fS,
-           (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
+  if (by_lines) {
+    const uint32_t rpw = TPB / ctx->acc_lpr, grid = (n_req + rpw - 1) / rpw;
+#define LB_ACC_STAGE(L)                                                                                       \
+  LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, n_req, d_req_off, n_sets, (const uint32_t*)d_lines, \
+           (const fp12*)d_fS, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err)
+    if (ctx->acc_lpr == 16)
+      LB_ACC_STAGE(16);
+    else if (ctx->acc_lpr == 32)
+      LB_ACC_STAGE(32);
+    else
+      LB_ACC_STAGE(64);
+#undef LB_ACC_STAGE
+  } else
+    LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, (const fp12*)d_fS,
+             (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
   LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
   return LB_OK;
 }
 
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
-  size_t per_set = sizeof(g2j) * 4 + sizeof(g2a) + sizeof(g1j) + sizeof(g1a) + sizeof(fp12) + 3 + 16 * 256 / 64;
+  size_t per_set = sizeof(g2j) * 4 + sizeof(g2a) + sizeof(g1j) + sizeof(g1a) + sizeof(fp12) + 3 + 16 * 256 / 64 +
+                   (size_t)LB_MILLER_LINES * 72 * 4;
   size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64;
   return ns * per_set + (size_t)n_req * per_req + 64 * 256;
 }
@@ -326,6 +361,12 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_SLOTS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
+  }
+  if (const char* e = getenv("LB_MILLER")) ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : 0;
+  if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("LB_ACC_LPR")) {
+    const int v = atoi(e);
+    if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;
   }
   for (int s = 0; s < lb_ctx::kMaxSlots; s++)
     ctx->streams_per_slot[s] = ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;

@@ -22,6 +22,7 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #define LB_HEAVY_WAVES 1
 #endif
 
+
 namespace lb {
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint8_t* __restrict__ single_flag);
@@ -74,4 +75,16 @@ __global__ void __launch_bounds__(TPB) k_sk_to_pk(uint32_t n, const uint8_t* __r
                                                   uint8_t* __restrict__ out96);
 __global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sk32,
                                               const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96);
+template <int WAVES>
+__global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pairs, uint32_t base,
+                                                               const g1a* __restrict__ P, const g2a* __restrict__ Q,
+                                                               uint32_t* __restrict__ lines);
+template <int LPR>
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                                    uint32_t n_pairs, const uint32_t* __restrict__ lines,
+                                                                    const fp12* __restrict__ fS,
+                                                                    const uint8_t* __restrict__ sig_status,
+                                                                    const uint8_t* __restrict__ pk_status,
+                                                                    fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
+                                                                    uint8_t* __restrict__ req_err);
 }  // namespace lb

@@ -34,4 +34,114 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n,
   f[i] = r;
 }
 
+// Lines of pairs [base, base + n) of the verification's pair list (n_pairs
+// total): pair base + i is (P[i], Q[i]), or (-g1, Q[i]) when P is null.
+template <int WAVES>
+__global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pairs, uint32_t base,
+                                                               const g1a* __restrict__ P, const g2a* __restrict__ Q,
+                                                               uint32_t* __restrict__ lines) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a p;
+  if (P) {
+    p = P[i];
+  } else {
+    fp_set(p.x, LB_G1_X);
+    fp_set(p.y, LB_G1_NEG_Y);
+    p.inf = false;
+  }
+  const g2a q = Q[i];
+  miller_lines(p, q, lines, n_pairs, base + i);
+}
+
+// Per request k: F_k = f_S[k] * prod_{i in request} Miller(r_i pk_i, H_i), from
+// the stored lines.  LB_ACC_LPR lanes per request (64 / LB_ACC_LPR requests per
+// wave); lane l accumulates the set pairs a + l, a + l + LPR, ... into ONE f,
+// so the Fp12 squaring of each loop step is shared by ~128 / LPR pairs; the
+// lane values are then multiplied in an LDS tree.  Also reduces the request's
+// set statuses (verdict / rejection flags) as k_prod_tree did.
+template <int LPR>
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                                    uint32_t n_pairs, const uint32_t* __restrict__ lines,
+                                                                    const fp12* __restrict__ fS,
+                                                                    const uint8_t* __restrict__ sig_status,
+                                                                    const uint8_t* __restrict__ pk_status,
+                                                                    fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
+                                                                    uint8_t* __restrict__ req_err) {
+  constexpr uint32_t RPW = TPB / LPR;  // requests per workgroup
+  __shared__ fp12 sh[TPB];
+  __shared__ uint32_t bad[RPW], err_empty[RPW], err_pk[RPW];
+  const uint32_t sub = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  const uint32_t k = blockIdx.x * RPW + sub;
+  const bool live = k < n_req;
+  const uint32_t a = live ? req_off[k] : 0, b = live ? req_off[k + 1] : 0;
+  if (lane == 0) {
+    bad[sub] = (a == b) ? 1u : 0u;
+    err_empty[sub] = 0;
+    err_pk[sub] = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = a + lane; i < b; i += LPR) {
+    const uint8_t ss = sig_status[i], ps = pk_status[i];
+    if (ss != LB_ST_OK || ps != LB_ST_OK) atomicOr(&bad[sub], 1u);
+    if (ps == LB_ST_EMPTY_AGGREGATE) atomicOr(&err_empty[sub], 1u);
+    if (ps == LB_ST_BAD_ENCODING) atomicOr(&err_pk[sub], 1u);
+  }
+  fp12 f;
+  fp12_one(f);
+  fp2 l0, l1, l4;
+  int j = 0;
+#pragma unroll 1
+  for (int bit = 62; bit >= 0; bit--) {
+    if (bit < 62) fp12_sqr(f, f);
+#pragma unroll 1
+    for (uint32_t i = a + lane; i < b; i += LPR) {
+      line_get(lines, n_pairs, i, j, l0, l1, l4);
+      fp12_mul_line(f, f, l0, l1, l4);
+    }
+    j++;
+    if ((LB_X_ABS >> bit) & 1ull) {
+#pragma unroll 1
+      for (uint32_t i = a + lane; i < b; i += LPR) {
+        line_get(lines, n_pairs, i, j, l0, l1, l4);
+        fp12_mul_line(f, f, l0, l1, l4);
+      }
+      j++;
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+  sh[threadIdx.x] = f;
+  __syncthreads();
+  for (uint32_t s = (uint32_t)LPR / 2; s > 0; s >>= 1) {
+    if (lane < s) {
+      fp12 m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      fp12_mul(m, m, o);
+      sh[threadIdx.x] = m;
+    }
+    __syncthreads();
+  }
+  if (live && lane == 0) {
+    fp12 tot = sh[threadIdx.x], s = fS[k];
+    fp12_mul(tot, tot, s);
+    F[k] = tot;
+    req_bad[k] = bad[sub] ? 1 : 0;
+    req_err[k] = err_empty[sub] ? LB_REQ_EMPTY_AGGREGATE : err_pk[sub] ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+  }
+}
+
+// tuning variants selected at run time (LB_LINES_WAVES, LB_ACC_LPR)
+#define LB_INST_LINES(W)                                                                                       \
+  template __global__ void k_lines<W>(uint32_t, uint32_t, uint32_t, const g1a* __restrict__, const g2a* __restrict__, \
+                                      uint32_t* __restrict__);
+LB_INST_LINES(1)
+LB_INST_LINES(2)
+#define LB_INST_ACC(L)                                                                                           \
+  template __global__ void k_miller_acc<L>(uint32_t, const uint32_t* __restrict__, uint32_t,                    \
+                                           const uint32_t* __restrict__, const fp12* __restrict__,              \
+                                           const uint8_t* __restrict__, const uint8_t* __restrict__,            \
+                                           fp12* __restrict__, uint8_t* __restrict__, uint8_t* __restrict__);
+LB_INST_ACC(64)
+LB_INST_ACC(32)
+LB_INST_ACC(16)
+
 }  // namespace lb
