@@ -239,6 +239,42 @@ LB_DEV void jac_to_aff(aff<F>& r, const jac<F>& p) {
   r.inf = false;
 }
 
+// Affine forms of a G1 and a G2 point with ONE shared Fp inversion
+// (Montgomery's trick over the pair): with t = Z1 N(Z2),
+//   1/Z1 = N(Z2)/t,  1/Z2 = conj(Z2) Z1/t.
+// Saves one of the two ~460-product exponentiations per verified set (the
+// pipeline needs r_i pk_i and H(m_i) affine for the Miller loop).
+LB_DEV void jac_pair_to_aff(g1a& pa, g2a& qa, const g1j& p, const g2j& q) {
+  const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  fp one, z1, n2, e, t, ti, z1i, n2i, zi2, zi3;
+  fp_one(one);
+  z1 = p.Z;
+  fp_cmov(z1, one, pi);
+  fp_sqr(n2, q.Z.c0);
+  fp_sqr(e, q.Z.c1);
+  fp_add(n2, n2, e);
+  fp_cmov(n2, one, qi);
+  fp_mul(t, z1, n2);
+  fp_inv(ti, t);
+  fp_mul(z1i, ti, n2);
+  fp_mul(n2i, ti, z1);
+  // G1
+  fp_sqr(zi2, z1i);
+  fp_mul(zi3, zi2, z1i);
+  fp_mul(pa.x, p.X, zi2);
+  fp_mul(pa.y, p.Y, zi3);
+  pa.inf = pi;
+  // G2: 1/Z2 = conj(Z2) / N(Z2)
+  fp2 z2i, w2, w3;
+  fp2_conj(z2i, q.Z);
+  fp2_mul_fp(z2i, z2i, n2i);
+  fp2_sqr(w2, z2i);
+  fp2_mul(w3, w2, z2i);
+  fp2_mul(qa.x, q.X, w2);
+  fp2_mul(qa.y, q.Y, w3);
+  qa.inf = qi;
+}
+
 template <class F>
 LB_DEV bool jac_eq(const jac<F>& p, const jac<F>& q) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);

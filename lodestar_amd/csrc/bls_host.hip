@@ -214,9 +214,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2j* d_sig = ws.take<g2j>(ns);
   g2j* d_rsig = ws.take<g2j>(ns);
   g2j* d_q = ws.take<g2j>(2 * (size_t)ns);
-  g2a* d_h = ws.take<g2a>(ns);
+  g2j* d_h = ws.take<g2j>(ns);
   g1j* d_pk = ws.take<g1j>(ns);
-  g1a* d_rpk = ws.take<g1a>(ns);
+  g1j* d_rpk = ws.take<g1j>(ns);
   const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets);
   fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);
   uint32_t* d_lines = by_lines ? ws.take<uint32_t>((size_t)ns * LB_MILLER_LINES * 72) : nullptr;
@@ -247,14 +247,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
   if (n_sets && by_lines) {
     if (ctx->lines_waves == 1)
-      LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1a*)d_rpk,
-               (const g2a*)d_h, d_lines);
+      LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1j*)d_rpk,
+               (const g2j*)d_h, d_lines);
     else
-      LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1a*)d_rpk,
-               (const g2a*)d_h, d_lines);
+      LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1j*)d_rpk,
+               (const g2j*)d_h, d_lines);
   }
   else if (n_sets)
-    LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1a*)d_rpk, (const g2a*)d_h,
+    LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1j*)d_rpk, (const g2j*)d_h,
              d_f);
   if (n_sets) {
     LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
@@ -286,7 +286,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
 
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
-  size_t per_set = sizeof(g2j) * 4 + sizeof(g2a) + sizeof(g1j) + sizeof(g1a) + sizeof(fp12) + 3 + 16 * 256 / 64 +
+  size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
                    (size_t)LB_MILLER_LINES * 72 * 4;
   size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64;
   return ns * per_set + (size_t)n_req * per_req + 64 * 256;

@@ -38,18 +38,18 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint
                                                      uint8_t* __restrict__ pk_status);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h);
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
-                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk);
+                                                   uint8_t* __restrict__ pk_status, g1j* __restrict__ rpk);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                   const g2j* __restrict__ rsig, g2a* __restrict__ S);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1j* __restrict__ rpk, const g2j* __restrict__ h,
                                                      fp12* __restrict__ f);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    const fp12* __restrict__ f, const fp12* __restrict__ fS,
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(TPB) k_sign(uint32_t n, const uint8_t* __restr
                                               const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96);
 template <int WAVES>
 __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pairs, uint32_t base,
-                                                               const g1a* __restrict__ P, const g2a* __restrict__ Q,
+                                                               const g1j* __restrict__ P, const g2j* __restrict__ Q,
                                                                uint32_t* __restrict__ lines);
 template <int LPR>
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,

@@ -16,15 +16,14 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, c
   hash_to_g2_half(r, m, (int)(t & 1));
   q[t] = r;
 }
-// hash_to_G2, second half: Q0 + Q1, clear cofactor, affine
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2a* __restrict__ out_h) {
+// hash_to_G2, second half: Q0 + Q1, clear cofactor (Jacobian out: the
+// affine conversion shares its inversion with r_i pk_i, jac_pair_to_aff)
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
   hash_to_g2_finish(h, q0, q1);
-  g2a ha;
-  jac_to_aff(ha, h);
-  out_h[i] = ha;
+  out_h[i] = h;
 }
 
 // ---- hash_to_G2 in one lane (stage-level API) ------------------------------

@@ -22,35 +22,30 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req
 }
 
 // f_i = Miller(r_i pk_i, H(m_i))
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1a* __restrict__ rpk, const g2a* __restrict__ h,
+__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1j* __restrict__ rpk, const g2j* __restrict__ h,
                                                      fp12* __restrict__ f) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fp12 r;
   fp12_one(r);
-  g1a p = rpk[i];
-  g2a q = h[i];
+  g1a p;
+  g2a q;
+  jac_pair_to_aff(p, q, rpk[i], h[i]);
   if (!p.inf && !q.inf) miller_loop(r, p, q);
   f[i] = r;
 }
 
 // Lines of pairs [base, base + n) of the verification's pair list (n_pairs
-// total): pair base + i is (P[i], Q[i]), or (-g1, Q[i]) when P is null.
+// total): pair base + i is (P[i], Q[i]) (Jacobian in, one shared inversion).
 template <int WAVES>
 __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pairs, uint32_t base,
-                                                               const g1a* __restrict__ P, const g2a* __restrict__ Q,
+                                                               const g1j* __restrict__ P, const g2j* __restrict__ Q,
                                                                uint32_t* __restrict__ lines) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1a p;
-  if (P) {
-    p = P[i];
-  } else {
-    fp_set(p.x, LB_G1_X);
-    fp_set(p.y, LB_G1_NEG_Y);
-    p.inf = false;
-  }
-  const g2a q = Q[i];
+  g2a q;
+  jac_pair_to_aff(p, q, P[i], Q[i]);
   miller_lines(p, q, lines, n_pairs, base + i);
 }
 
@@ -131,7 +126,7 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_r
 
 // tuning variants selected at run time (LB_LINES_WAVES, LB_ACC_LPR)
 #define LB_INST_LINES(W)                                                                                       \
-  template __global__ void k_lines<W>(uint32_t, uint32_t, uint32_t, const g1a* __restrict__, const g2a* __restrict__, \
+  template __global__ void k_lines<W>(uint32_t, uint32_t, uint32_t, const g1j* __restrict__, const g2j* __restrict__, \
                                       uint32_t* __restrict__);
 LB_INST_LINES(1)
 LB_INST_LINES(2)

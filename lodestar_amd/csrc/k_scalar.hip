@@ -24,29 +24,27 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, 
   rsig[i] = rs;
 }
 
-// r_i pk_i (affine); core-verify pubkey subgroup check for single-set requests
+// r_i pk_i (Jacobian; made affine together with H(m_i), jac_pair_to_aff);
+// core-verify pubkey subgroup check for single-set requests
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
-                                                   uint8_t* __restrict__ pk_status, g1a* __restrict__ rpk) {
+                                                   uint8_t* __restrict__ pk_status, g1j* __restrict__ rpk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st = pk_status[i];
   g1j p = pk[i];
   if (st == LB_ST_OK && single_flag[i] && !g1_in_subgroup(p)) st = LB_ST_NOT_IN_GROUP;
-  g1a pa;
-  fp_zero(pa.x);
-  fp_zero(pa.y);
-  pa.inf = true;
+  g1j rp;
+  jac_set_inf(rp);
   if (st == LB_ST_OK) {
     uint8_t sd[32];
     for (int k = 0; k < 32; k++) sd[k] = seed[k];
     const uint64_t r = batch_scalar(sd, i);
-    g1j rp, e;
+    g1j e;
     g1_glv_endo(e, p);
     jac_mul_glv(rp, p, e, r);
-    jac_to_aff(pa, rp);
   }
-  rpk[i] = pa;
+  rpk[i] = rp;
   pk_status[i] = st;
 }
 

@@ -23,6 +23,26 @@ def device():
     dev.close()
 
 
+@pytest.fixture(scope="session", params=["lane", "lines"])
+def device_modes(request):
+    """A context per Miller organisation: one pair per lane (k_miller_sets) and
+    stored lines + multi-pair accumulation (k_lines / k_miller_acc), which the
+    library otherwise picks only for calls of >= 8192 sets."""
+    import os
+    from lodestar_amd.native import Device
+    old = os.environ.get("LB_MILLER")
+    os.environ["LB_MILLER"] = request.param
+    try:
+        dev = Device(0)
+    finally:
+        if old is None:
+            os.environ.pop("LB_MILLER", None)
+        else:
+            os.environ["LB_MILLER"] = old
+    yield dev
+    dev.close()
+
+
 def load_golden(name):
     import json
     with open(os.path.join(GOLDEN, name)) as f:

@@ -119,9 +119,9 @@ def test_aggregate_signatures_golden(device):
 
 # ---- verdict scenarios (maybeBatch / worker semantics) -----------------------------------
 @pytest.mark.parametrize("idx", range(len(VEC["verify_requests"])))
-def test_verify_requests_scenarios(device, idx):
+def test_verify_requests_scenarios(device_modes, idx):
     sc = VEC["verify_requests"][idx]
-    res = run_requests(device, sc["requests"])
+    res = run_requests(device_modes, sc["requests"])
     errors = sc.get("errors", [0] * len(sc["expect"]))
     assert list(res.errors) == errors, sc["name"]
     for e, v, err in zip(sc["expect"], res.valid, errors):
@@ -159,8 +159,9 @@ def test_sign_matches_oracle_random(device):
         assert s == O.g2_to_bytes(O.sign(k, m))
 
 
-def test_random_batches_vs_oracle(device):
+def test_random_batches_vs_oracle(device_modes):
     """Random mixes of valid / wrong-message / malformed sets: verdicts equal oracle.batch."""
+    device = device_modes
     rnd = random.Random(1234)
     n = 24
     sks = [interop_sk_be(i) for i in range(n)]
