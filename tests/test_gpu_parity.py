@@ -248,3 +248,72 @@ def test_c3_sync_aggregate_512(device):
                                  np.array([0, n, 2 * n], np.uint32), np.frombuffer(msg * 2, np.uint8), blob, offs,
                                  bytes(32))
     assert list(res.valid) == [1, 0]
+
+
+# ---- mixed block-import / gossip workloads vs the C oracle (configs C4 / C5 shapes) ----------
+def _mixed_workload(device, n_keys=512, n_sets=1500, seed=5):
+    """Single sets, committee aggregates (2..64 pubkeys, same message, 192-byte
+    aggregated signature), and injected failures: wrong message, malformed
+    signatures (Buffer.alloc(96, 10), 32 zero bytes), infinite signature,
+    bad pubkey bytes, empty aggregate.  Requests of 1..128 sets."""
+    rnd = random.Random(seed)
+    sks = [interop_sk_be(i) for i in range(n_keys)]
+    pks = device.sk_to_pk(sks)
+    # plan the sets, then sign everything in one device call
+    plan, msgs = [], []
+    for j in range(n_sets):
+        msgs.append(hashlib.sha256(b"mixed" + j.to_bytes(4, "little")).digest())
+        plan.append(rnd.sample(range(n_keys), rnd.randint(2, 64)) if rnd.random() < 0.15 else [rnd.randrange(n_keys)])
+    flat_sig = device.sign([sks[m] for p in plan for m in p], [msgs[j] for j, p in enumerate(plan) for _ in p])
+    set_pks, sigs, at = [], [], 0
+    for p in plan:
+        part = flat_sig[at:at + len(p)]
+        at += len(p)
+        set_pks.append([pks[m] for m in p])
+        if len(p) == 1:
+            sigs.append(part[0])
+        else:
+            msig, bad = device.aggregate_signatures(part)
+            assert bad == -1
+            sigs.append(msig)
+    for j in rnd.sample(range(n_sets), 40):
+        kind = rnd.randrange(6)
+        if kind == 0:
+            msgs[j] = bytes(32)
+        elif kind == 1:
+            sigs[j] = bytes([10]) * 96
+        elif kind == 2:
+            sigs[j] = bytes(32)
+        elif kind == 3:
+            sigs[j] = bytes([0xC0]) + bytes(95)
+        elif kind == 4:
+            set_pks[j] = [bytes(rnd.getrandbits(8) for _ in range(96))]
+        else:
+            set_pks[j] = []
+    req_off = [0]
+    while req_off[-1] < n_sets:
+        req_off.append(min(n_sets, req_off[-1] + rnd.choice([1, 1, 2, 3, 16, 64, 128])))
+    flat, pk_off = [], [0]
+    for s in set_pks:
+        flat += s
+        pk_off.append(len(flat))
+    blob, offs = pack_blobs(sigs)
+    return (np.array(req_off, np.uint32), np.frombuffer(b"".join(flat), np.uint8), np.array(pk_off, np.uint32),
+            np.frombuffer(b"".join(msgs), np.uint8), blob, offs)
+
+
+@pytest.fixture(scope="module")
+def mixed_workload(device):
+    return _mixed_workload(device)
+
+
+def test_mixed_workload_vs_c_oracle(device_modes, mixed_workload):
+    """GPU verdicts and rejection codes == the C oracle's, request by request."""
+    from oracle import c_oracle as C
+    args = mixed_workload
+    seed = hashlib.sha256(b"mixed-seed").digest()
+    res = device_modes.verify_requests(*args, seed)
+    valid, err = C.verify_requests(*args, seed, threads=16)
+    assert list(res.errors) == list(err)
+    assert list(res.valid) == list(valid)
+    assert 0 < int(valid.sum()) < len(valid)  # the injections hit some requests, not all
