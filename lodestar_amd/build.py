@@ -49,9 +49,12 @@ def _unit_deps_mtime(unit: str) -> float:
     return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, lib: str = LIB, obj_dir: str = OBJ_DIR,
+          extra=()) -> str:
     """Compile every unit for gfx950 (in parallel, each unit only when stale) and link the .so."""
     gen_constants()
+    LIB = lib  # noqa: N806
+    OBJ_DIR = obj_dir  # noqa: N806
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_source_mtime():
         return LIB
     os.makedirs(OBJ_DIR, exist_ok=True)
@@ -60,7 +63,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         o = os.path.join(OBJ_DIR, os.path.splitext(u)[0] + ".o")
         objs.append(o)
         if force or not os.path.exists(o) or os.path.getmtime(o) < _unit_deps_mtime(u):
-            todo.append([HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-c", "-o", o, os.path.join(CSRC, u)])
+            todo.append([HIPCC, f"--offload-arch={ARCH}", *FLAGS, *extra, "-c", "-o", o, os.path.join(CSRC, u)])
     jobs = jobs or max(1, min(len(todo), os.cpu_count() or 1, 16))
     procs = []
     for cmd in todo:
@@ -80,6 +83,14 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     subprocess.check_call(link)
     os.replace(LIB + ".tmp", LIB)
     return LIB
+
+
+def build_variant(name: str, extra, verbose: bool = False) -> str:
+    """Same library with extra compile flags, under build/variants/NAME/ (select it
+    at run time with LB_LIBRARY=<path>); for tuning experiments only."""
+    d = os.path.join(ROOT, "build", "variants", name)
+    return build(verbose=verbose, lib=os.path.join(d, "liblodestar_bls.so"), obj_dir=os.path.join(d, "obj"),
+                 extra=tuple(extra))
 
 
 def build_opcount(out_dir: str) -> str:

@@ -21,12 +21,36 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #ifndef LB_HEAVY_WAVES
 #define LB_HEAVY_WAVES 1
 #endif
+// Per-stage occupancy (min waves per SIMD, i.e. a 512 / W register budget),
+// measured on MI355X (profiles/occupancy_r01.log): the per-set stages run
+// faster at 2 waves/SIMD despite some spilling (a lone wave issues
+// v_mad_u64_u32 at ~60% of the SIMD's rate); the per-request tails (one lane
+// per request, a long serial chain) and the Miller accumulation keep the
+// spill-free 1-wave budget.
+#ifndef LB_W_HASH
+#define LB_W_HASH 2
+#endif
+#ifndef LB_W_MAP  // k_hash_half (SHA-256 + SSWU + isogeny, small live state)
+#define LB_W_MAP 4
+#endif
+#ifndef LB_W_DECODE
+#define LB_W_DECODE 2
+#endif
+#ifndef LB_W_SCALAR
+#define LB_W_SCALAR 2
+#endif
+#ifndef LB_W_ACC
+#define LB_W_ACC 1
+#endif
+#ifndef LB_W_TAIL
+#define LB_W_TAIL 1
+#endif
 
 
 namespace lb {
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint8_t* __restrict__ single_flag);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                      const uint32_t* __restrict__ sig_off,
                                                      const uint8_t* __restrict__ single_flag,
                                                      g2j* __restrict__ out_sig, uint8_t* __restrict__ status);
@@ -36,27 +60,27 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const u
 __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
                                                      const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                      uint8_t* __restrict__ pk_status);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+__global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
                                                    uint8_t* __restrict__ pk_status, g1j* __restrict__ rpk);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                   const g2j* __restrict__ rsig, g2a* __restrict__ S);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1j* __restrict__ rpk, const g2j* __restrict__ h,
                                                      fp12* __restrict__ f);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    const fp12* __restrict__ f, const fp12* __restrict__ fS,
                                                    const uint8_t* __restrict__ sig_status,
                                                    const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
                                                    uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err);
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_final(uint32_t n_req, const fp12* __restrict__ F,
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_final(uint32_t n_req, const fp12* __restrict__ F,
                                                const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h);
 template <class F>
@@ -80,7 +104,7 @@ __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pai
                                                                const g1j* __restrict__ P, const g2j* __restrict__ Q,
                                                                uint32_t* __restrict__ lines);
 template <int LPR>
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                                     uint32_t n_pairs, const uint32_t* __restrict__ lines,
                                                                     const fp12* __restrict__ fS,
                                                                     const uint8_t* __restrict__ sig_status,

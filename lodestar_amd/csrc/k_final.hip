@@ -4,7 +4,7 @@
 
 namespace lb {
 
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_final(uint32_t n_req, const fp12* __restrict__ F,
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_final(uint32_t n_req, const fp12* __restrict__ F,
                                                const uint8_t* __restrict__ req_bad, uint8_t* __restrict__ valid) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_req) return;

@@ -5,7 +5,7 @@
 namespace lb {
 
 // hash_to_G2, first half: lane 2i+j maps u_j of message i (SSWU + 3-isogeny)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
+__global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * n) return;
@@ -18,7 +18,7 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_half(uint32_t n, c
 }
 // hash_to_G2, second half: Q0 + Q1, clear cofactor (Jacobian out: the
 // affine conversion shares its inversion with r_i pk_i, jac_pair_to_aff)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h) {
+__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;

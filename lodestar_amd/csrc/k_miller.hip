@@ -5,7 +5,7 @@
 namespace lb {
 
 // f_S[k] = Miller(-g1, S_k)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_req) return;
   fp12 r;
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pai
 // lane values are then multiplied in an LDS tree.  Also reduces the request's
 // set statuses (verdict / rejection flags) as k_prod_tree did.
 template <int LPR>
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                                     uint32_t n_pairs, const uint32_t* __restrict__ lines,
                                                                     const fp12* __restrict__ fS,
                                                                     const uint8_t* __restrict__ sig_status,

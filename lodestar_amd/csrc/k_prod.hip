@@ -5,7 +5,7 @@
 namespace lb {
 
 // F_k = f_S[k] * prod f_i, request status and errors: one wave per request
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_prod_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    const fp12* __restrict__ f, const fp12* __restrict__ fS,
                                                    const uint8_t* __restrict__ sig_status,
                                                    const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,

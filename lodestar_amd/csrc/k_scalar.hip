@@ -5,7 +5,7 @@
 namespace lb {
 
 // r_i sig_i  (r_i = a_i + b_i lambda, jac_mul_glv)
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig) {
@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_sig(uint32_t n, 
 
 // r_i pk_i (Jacobian; made affine together with H(m_i), jac_pair_to_aff);
 // core-verify pubkey subgroup check for single-set requests
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
                                                    uint8_t* __restrict__ pk_status, g1j* __restrict__ rpk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_scalar_pk(uint32_t n, c
 }
 
 // S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                   const g2j* __restrict__ rsig, g2a* __restrict__ S) {
   __shared__ g2j sh[TPB];
   const uint32_t k = blockIdx.x;

@@ -14,7 +14,7 @@ __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_
 
 // Signature.fromBytes(validate=true); for single-set requests also the
 // ZeroSignatureError of @chainsafe/bls Signature.verify.
-__global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                      const uint32_t* __restrict__ sig_off,
                                                      const uint8_t* __restrict__ single_flag,
                                                      g2j* __restrict__ out_sig, uint8_t* __restrict__ status) {

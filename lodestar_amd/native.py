@@ -51,7 +51,9 @@ class BadPubkeyError(LodestarBlsError):
 
 
 def library_path() -> str:
-    return os.path.join(_HERE, _LIB_NAME)
+    # LB_LIBRARY: an alternative build of the same library (tuning experiments,
+    # lodestar_amd/build.py build_variant); never a CPU fallback
+    return os.environ.get("LB_LIBRARY") or os.path.join(_HERE, _LIB_NAME)
 
 
 class _RequestBatch(ctypes.Structure):
