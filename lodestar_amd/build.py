@@ -11,9 +11,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liblodestar_bls.so")
 # one translation unit per stage group, compiled in parallel and linked into one .so
 UNITS = ["k_final.hip", "k_pairing.hip", "k_aux.hip", "k_hash.hip", "k_miller.hip", "k_scalar.hip", "k_sets.hip",
-         "k_prod.hip", "bls_host.hip"]
+         "k_prod.hip", "k_tail.hip", "bls_host.hip"]
 HEADERS = ["bls_kernels.h", "bls_field.h", "bls_fp_ps.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h",
-           "gen_constants.py", "gen_fp_asm.py"]
+           "bls_wc12.h", "bls_wc12_tables.h", "gen_constants.py", "gen_fp_asm.py", "gen_wc12.py"]
 SOURCES = UNITS + HEADERS + ["bls_all.hip"]
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 HEADER = os.path.join(ROOT, "include", "lodestar_bls.h")
@@ -28,7 +28,8 @@ def _newest_source_mtime() -> float:
 
 def gen_constants() -> str:
     """Generated headers: curve constants and the product-scanning field multiply."""
-    for header, script in (("bls_constants.h", "gen_constants.py"), ("bls_fp_ps.h", "gen_fp_asm.py")):
+    for header, script in (("bls_constants.h", "gen_constants.py"), ("bls_fp_ps.h", "gen_fp_asm.py"),
+                           ("bls_wc12_tables.h", "gen_wc12.py")):
         out = os.path.join(CSRC, header)
         gen = os.path.join(CSRC, script)
         if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(gen):

@@ -8,4 +8,5 @@
 #include "k_final.hip"
 #include "k_pairing.hip"
 #include "k_aux.hip"
+#include "k_tail.hip"
 #include "bls_host.hip"

@@ -8,14 +8,16 @@
 // worker verifyManySignatureSets -> verifySignatureSetsMaybeBatch,
 // packages/beacon-node/src/chain/bls/multithread/worker.ts:30-108,
 // chain/bls/maybeBatch.ts:16-46):
-//   k_req_flags     per request : 1-set requests need core-verify checks
-//   k_decode_sigs   per set     : Signature.fromBytes(validate=true)
-//   k_pubkeys       per set (WG): PublicKey.fromBytes + PublicKey.aggregate
-//   k_hash          per set     : hash_to_G2(signing root)
-//   k_scalar        per set     : r_i pk_i (affine), r_i sig_i
-//   k_sum_req       per request : S_k = sum r_i sig_i
-//   k_miller        per pair    : f = Miller(r_i pk_i, H_i), Miller(-g1, S_k)
-//   k_final         per request : prod f, final exponentiation, == 1
+//   k_req_flags       per request : 1-set requests need core-verify checks
+//   k_decode_sigs     per set     : Signature.fromBytes(validate=true)
+//   k_pubkeys_*       per set     : PublicKey.fromBytes + PublicKey.aggregate
+//   k_hash_half/finish per message: hash_to_G2(signing root), two lanes per message
+//   k_scalar_pk/sig   per set     : r_i pk_i, r_i sig_i (GLV, 2 x 32-bit)
+//   k_sum_tree        per request : S_k = sum r_i sig_i
+//   k_lines + k_miller_acc        : Miller(r_i pk_i, H_i) from stored lines, several
+//     (or k_miller_sets + k_prod_tree) pairs per lane, product per request
+//   k_lines_S + k_tail per request: Miller(-g1, S_k), final exponentiation, == 1,
+//                                   one wave per request (wave-cooperative Fp12)
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -81,6 +83,9 @@ struct lb_ctx {
   uint32_t lines_min_sets = 8192;
   int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
   int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
+  // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
+  // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
+  bool tail_wave = true;
   // timing of the last completed verify call
   int n_stages = 0;
   float stage_ms[Slot::kMaxStages] = {};
@@ -219,7 +224,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g1j* d_rpk = ws.take<g1j>(ns);
   const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets);
   fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);
-  uint32_t* d_lines = by_lines ? ws.take<uint32_t>((size_t)ns * LB_MILLER_LINES * 72) : nullptr;
+  const bool tail_wave = ctx->tail_wave;
+  // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
+  const uint32_t n_pairs = n_sets + n_req;
+  uint32_t* d_lines = (by_lines || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
   uint8_t* d_pk_st = ws.take<uint8_t>(ns);
   uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
@@ -247,10 +255,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
   if (n_sets && by_lines) {
     if (ctx->lines_waves == 1)
-      LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1j*)d_rpk,
+      LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
     else
-      LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_sets, 0u, (const g1j*)d_rpk,
+      LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
   }
   else if (n_sets)
@@ -263,13 +271,17 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_sig_st, d_rsig);
   }
   LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S);
-  LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
+  if (tail_wave)
+    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines);
+  else
+    LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
+  const fp12* fS_in = tail_wave ? nullptr : (const fp12*)d_fS;
   LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
   if (by_lines) {
     const uint32_t rpw = TPB / ctx->acc_lpr, grid = (n_req + rpw - 1) / rpw;
 #define LB_ACC_STAGE(L)                                                                                       \
-  LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, n_req, d_req_off, n_sets, (const uint32_t*)d_lines, \
-           (const fp12*)d_fS, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err)
+  LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, n_req, d_req_off, n_pairs, (const uint32_t*)d_lines, \
+           fS_in, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err)
     if (ctx->acc_lpr == 16)
       LB_ACC_STAGE(16);
     else if (ctx->acc_lpr == 32)
@@ -278,9 +290,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_ACC_STAGE(64);
 #undef LB_ACC_STAGE
   } else
-    LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, (const fp12*)d_fS,
+    LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, fS_in,
              (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
-  LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
+  if (tail_wave)
+    LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
+             (const uint8_t*)d_bad, d_valid);
+  else
+    LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
   return LB_OK;
 }
 
@@ -288,7 +304,7 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
                    (size_t)LB_MILLER_LINES * 72 * 4;
-  size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64;
+  size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
   return ns * per_set + (size_t)n_req * per_req + 64 * 256;
 }
 
@@ -363,6 +379,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
   }
   if (const char* e = getenv("LB_MILLER")) ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : 0;
+  if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);

@@ -116,8 +116,11 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
     __syncthreads();
   }
   if (live && lane == 0) {
-    fp12 tot = sh[threadIdx.x], s = fS[k];
-    fp12_mul(tot, tot, s);
+    fp12 tot = sh[threadIdx.x];
+    if (fS) {  // null: the tail kernel multiplies Miller(-g1, S_k) in (k_tail)
+      fp12 s = fS[k];
+      fp12_mul(tot, tot, s);
+    }
     F[k] = tot;
     req_bad[k] = bad[sub] ? 1 : 0;
     req_err[k] = err_empty[sub] ? LB_REQ_EMPTY_AGGREGATE : err_pk[sub] ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;

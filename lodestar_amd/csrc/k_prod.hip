@@ -48,8 +48,11 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_prod_tree(uint32_t n_req, co
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    fp12 tot = sh[0], s = fS[k];
-    fp12_mul(tot, tot, s);
+    fp12 tot = sh[0];
+    if (fS) {  // null: the tail kernel multiplies Miller(-g1, S_k) in (k_tail)
+      fp12 s = fS[k];
+      fp12_mul(tot, tot, s);
+    }
     F[k] = tot;
     req_bad[k] = bad ? 1 : 0;
     req_err[k] = err_empty ? LB_REQ_EMPTY_AGGREGATE : err_pk ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
