@@ -86,6 +86,9 @@ struct lb_ctx {
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
   // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
   bool tail_wave = true;
+  // merged check of the whole call first (one tail), per-request tails only
+  // when it fails; used from merge_min_req requests up (LB_MERGE_MIN, 0 = off)
+  uint32_t merge_min_req = 8;
   // timing of the last completed verify call
   int n_stages = 0;
   float stage_ms[Slot::kMaxStages] = {};
@@ -226,7 +229,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);
   const bool tail_wave = ctx->tail_wave;
   // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
-  const uint32_t n_pairs = n_sets + n_req;
+  const bool merged = tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req;
+  const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
   uint32_t* d_lines = (by_lines || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
   uint8_t* d_pk_st = ws.take<uint8_t>(ns);
@@ -235,6 +239,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   fp12* d_fS = ws.take<fp12>(n_req);
   fp12* d_F = ws.take<fp12>(n_req);
   uint8_t* d_bad = ws.take<uint8_t>(n_req);
+  g2a* d_Sall = ws.take<g2a>(1);
+  fp12* d_Fall = ws.take<fp12>(1);
+  uint8_t* d_mflag = ws.take<uint8_t>(2);  // [0] merged check passed, [1] constant 0 (req_bad of the merged pair)
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
@@ -271,9 +278,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_sig_st, d_rsig);
   }
   LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S);
-  if (tail_wave)
-    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines);
-  else
+  if (tail_wave && !merged)
+    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines,
+             (const uint8_t*)nullptr);
+  else if (!tail_wave)
     LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
   const fp12* fS_in = tail_wave ? nullptr : (const fp12*)d_fS;
   LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
@@ -292,9 +300,22 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   } else
     LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, fS_in,
              (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
-  if (tail_wave)
+  if (merged) {
+    // merged check: one tail for the whole call; per-request tails only if it fails
+    LB_HIP(hipMemsetAsync(d_mflag, 0, 2, sl.st[0]));
+    LB_STAGE("merge", 0, k_merge, 1u, TPB, n_req, (const g2a*)d_S, (const fp12*)d_F, (const uint8_t*)d_bad, d_Sall,
+             d_Fall);
+    LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+             (const uint8_t*)nullptr);
+    LB_STAGE("tail_all", 0, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+             (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
+    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines,
+             (const uint8_t*)d_mflag);
     LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
-             (const uint8_t*)d_bad, d_valid);
+             (const uint8_t*)d_bad, d_valid, (const uint8_t*)d_mflag);
+  } else if (tail_wave)
+    LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
+             (const uint8_t*)d_bad, d_valid, (const uint8_t*)nullptr);
   else
     LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
   return LB_OK;
@@ -305,7 +326,7 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
                    (size_t)LB_MILLER_LINES * 72 * 4;
   size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
-  return ns * per_set + (size_t)n_req * per_req + 64 * 256;
+  return ns * per_set + (size_t)(n_req + 1) * per_req + 64 * 256;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -380,6 +401,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   }
   if (const char* e = getenv("LB_MILLER")) ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : 0;
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
+  if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);

@@ -112,10 +112,16 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
                                                                     fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
                                                                     uint8_t* __restrict__ req_err);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_lines_S(uint32_t n_req, uint32_t n_pairs, uint32_t base,
-                                                          const g2a* __restrict__ S, uint32_t* __restrict__ lines);
+                                                          const g2a* __restrict__ S, uint32_t* __restrict__ lines,
+                                                          const uint8_t* __restrict__ skip);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_t n_pairs, uint32_t base,
                                                        const uint32_t* __restrict__ lines,
                                                        const fp12* __restrict__ F,
                                                        const uint8_t* __restrict__ req_bad,
-                                                       uint8_t* __restrict__ valid);
+                                                       uint8_t* __restrict__ valid,
+                                                       const uint8_t* __restrict__ skip);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
+                                                        const fp12* __restrict__ F,
+                                                        const uint8_t* __restrict__ req_bad,
+                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all);
 }  // namespace lb

@@ -9,10 +9,12 @@
 namespace lb {
 
 // lines of the pairs (-g1, S_k), k < n_req, stored as pairs base + k
+// (skip: optional flag; nonzero -> nothing to do, the merged check passed)
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_lines_S(uint32_t n_req, uint32_t n_pairs, uint32_t base,
-                                                          const g2a* __restrict__ S, uint32_t* __restrict__ lines) {
+                                                          const g2a* __restrict__ S, uint32_t* __restrict__ lines,
+                                                          const uint8_t* __restrict__ skip) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_req) return;
+  if (k >= n_req || (skip && *skip)) return;
   g1a p;
   fp_set(p.x, LB_G1_X);
   fp_set(p.y, LB_G1_NEG_Y);
@@ -21,17 +23,20 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_lines_S(uint32_t n_req, uint
   miller_lines(p, q, lines, n_pairs, (size_t)base + k);
 }
 
-// one workgroup (one wave) per request: valid[k] = final_exp(F_k * Miller(-g1, S_k)) == 1
+// one workgroup (one wave) per request: valid[k] = final_exp(F_k * Miller(-g1, S_k)) == 1.
+// skip (optional): nonzero when the merged check of the whole call passed ->
+// valid[k] = !req_bad[k] without any arithmetic.
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_t n_pairs, uint32_t base,
                                                        const uint32_t* __restrict__ lines,
                                                        const fp12* __restrict__ F,
                                                        const uint8_t* __restrict__ req_bad,
-                                                       uint8_t* __restrict__ valid) {
+                                                       uint8_t* __restrict__ valid,
+                                                       const uint8_t* __restrict__ skip) {
   __shared__ wc_smem S;
   const uint32_t k = blockIdx.x;
   if (k >= n_req) return;
-  if (req_bad[k]) {  // uniform per workgroup
-    if (threadIdx.x == 0) valid[k] = 0;
+  if (req_bad[k] || (skip && *skip)) {  // uniform per workgroup
+    if (threadIdx.x == 0) valid[k] = req_bad[k] ? 0 : 1;
     return;
   }
   wc_init_gammas(S);
@@ -40,6 +45,50 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_
   wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
   wc_final_exp(S, WC_F, WC_F);
   if (threadIdx.x == 0) valid[k] = wc_is_one(S, WC_F) ? 1 : 0;
+}
+
+// Merged check of a whole call (the worker's merged batch, worker.ts:41-96):
+// S_all = sum S_k and F_all = prod F_k over the requests not already false.
+// One wave; the tail kernel then verifies (F_all, S_all) once, and the
+// per-request tails only run if that merged check fails.
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
+                                                        const fp12* __restrict__ F,
+                                                        const uint8_t* __restrict__ req_bad,
+                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all) {
+  __shared__ g2j shs[TPB];
+  __shared__ fp12 shf[TPB];
+  g2j acc;
+  jac_set_inf(acc);
+  fp12 f;
+  fp12_one(f);
+  for (uint32_t k = threadIdx.x; k < n_req; k += TPB) {
+    if (req_bad[k]) continue;
+    const g2a s = S[k];
+    if (!s.inf) jac_add_aff(acc, acc, s);
+    fp12 t = F[k];
+    fp12_mul(f, f, t);
+  }
+  shs[threadIdx.x] = acc;
+  shf[threadIdx.x] = f;
+  __syncthreads();
+  for (int st = TPB / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      g2j m = shs[threadIdx.x], o = shs[threadIdx.x + st];
+      jac_add(m, m, o);
+      shs[threadIdx.x] = m;
+      fp12 a = shf[threadIdx.x], b = shf[threadIdx.x + st];
+      fp12_mul(a, a, b);
+      shf[threadIdx.x] = a;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    g2j tot = shs[0];
+    g2a sa;
+    jac_to_aff(sa, tot);
+    S_all[0] = sa;
+    F_all[0] = shf[0];
+  }
 }
 
 }  // namespace lb
