@@ -187,6 +187,7 @@ def main():
             step(0, 1, a.per_request)
             lat.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.median(lat)) if lat else None
+    lat_stages = {name: round(ms, 3) for name, ms in dev.last_stage_times()} if lat else None
 
     if rank != 0:
         if world > 1:
@@ -203,7 +204,8 @@ def main():
         oc = json.load(open(counts_path))
         st = oc["stages"].get(dom)
         if st:
-            mads = st["fp_mul_per_set"] * n * oc["mads_per_fp_mul"]
+            per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
+            mads = per_set * n
             achieved = mads / (stage_ms[dom] * 1e-3) / 1e12
             peak = PEAK_MAD_PER_S / 1e12
             traffic = None
@@ -240,6 +242,7 @@ def main():
                                f"{a.per_request} sets, verifySignatureSetsMaybeBatch semantics",
                    "sets_per_gpu": n, "sets_per_request": a.per_request, "parallelism": f"shard{world}"},
         "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
+        "p50_stage_ms": lat_stages,
         "all_valid": ok,
         "overlap": "sync" if a.sync else f"{nbuf} calls in flight (lb_verify_requests_device_async)",
         "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},

@@ -86,9 +86,16 @@ int lb_device_count(void);
  *   - any signature that fails Signature.fromBytes(validate=true) -> false
  *   - infinite (aggregated) pubkey -> false
  *   - 1 set: core verify (pubkey G1 check, infinite signature -> false)
- *   - >= 2 sets: random-scalar batch verification with 64-bit scalars drawn
- *     from the deterministic DRBG  r_i = LE64(SHA-256(seed || LE32(i))[0..8]),
- *     i = the set's index in this call, 0 -> 1.
+ *   - >= 2 sets: random-scalar batch verification with 2^64 possible scalars
+ *     per set, drawn from the deterministic DRBG
+ *       w_i = LE64(SHA-256(seed || LE32(i))[0..8]) (0 -> 1),
+ *       r_i = (w_i mod 2^32) + (w_i >> 32) * lambda (mod r), lambda = -x^2,
+ *     i = the set's index in this call (blst draws 8 random bytes per set; the
+ *     lambda split lets the GPU multiply with two 32-bit halves, GLV).
+ *   Requests that are not already false are first checked together (one merged
+ *   product, the worker's merged batch, worker.ts:41-96); each request is
+ *   re-verified alone only when the merged check fails, so a merged failure
+ *   never changes any request's verdict.
  * Set i's pubkeys are pubkeys[pk_offsets[i] .. pk_offsets[i+1]) (96-byte
  * uncompressed each); more than one -> aggregated on the GPU (the reference
  * aggregates on the main thread before dispatch).

@@ -35,49 +35,122 @@ enum : int {
 struct wc_smem {
   fp slot[WC_NSLOTS][12];
   fp prod[64];
-  uint32_t flag;
+  fp part[64];
+  // the op programs, copied from constant memory once per kernel: every lane
+  // walks its own term list, and lane-divergent constant/global loads on that
+  // path would put a memory round trip under every term
+  wc_desc ops[LB_WC_NOPS];
+  uint16_t term[LB_WC_NTERMS];  // coef << 8 | code
 };
 
-LB_DEV void wc_acc(fp& acc, const fp& v, int c) {
-  if (c > 0) {
-    for (int t = 0; t < c; t++) fp_add(acc, acc, v);
+LB_DEV void wc_init_tables(wc_smem& S) {
+  for (int t = threadIdx.x; t < LB_WC_NTERMS; t += blockDim.x)
+    S.term[t] = (uint16_t)((uint8_t)LB_WC_COEF[t] << 8 | LB_WC_CODE[t]);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(LB_WC_OPS);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(S.ops);
+  for (int t = threadIdx.x; t < (int)(sizeof(S.ops) / 4); t += blockDim.x) dst[t] = src[t];
+  __syncthreads();
+}
+
+// ---- lazy accumulation: a lane sums up to 8 (|coef|-weighted) terms as a
+// plain 12-limb integer (every term is v or p - v, both <= p, so the sum stays
+// < 8p < 2^384), then reduces once with conditional subtractions of 4p, 2p, p.
+static constexpr uint32_t WC_P2[12] = LB_P2_LIMBS;
+static constexpr uint32_t WC_P4[12] = LB_P4_LIMBS;
+
+struct lz {
+  uint32_t l[12];
+};
+LB_DEV void lz_zero(lz& a) {
+#pragma unroll
+  for (int j = 0; j < 12; j++) a.l[j] = 0;
+}
+// a += c v  (c > 0)  or  a += |c| (p - v)  (c < 0)
+LB_DEV void lz_term(lz& a, const fp& v, int c) {
+  uint32_t t[12];
+  if (c < 0) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) t[j] = __builtin_subc(P_[j], v.l[j], br, &br);
+    c = -c;
   } else {
-    for (int t = 0; t < -c; t++) fp_sub(acc, acc, v);
+#pragma unroll
+    for (int j = 0; j < 12; j++) t[j] = v.l[j];
   }
+  for (int k = 0; k < c; k++) {
+    uint32_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) a.l[j] = __builtin_addc(a.l[j], t[j], cy, &cy);
+  }
+}
+// a -= m if a >= m
+LB_DEV void lz_csub(lz& a, const uint32_t* m) {
+  uint32_t s[12], br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) s[j] = __builtin_subc(a.l[j], m[j], br, &br);
+#pragma unroll
+  for (int j = 0; j < 12; j++) a.l[j] = br ? a.l[j] : s[j];
+}
+// sum of the terms [t0, t1) (values val(code)) into r, reduced to < 2p
+// (operands of fp_mul: x y < 4p^2 < p R) or to < p (canonical outputs)
+template <class Val>
+LB_DEV void lz_sum(fp& r, const uint16_t* term, int t0, int t1, Val val, bool canonical) {
+  lz a;
+  lz_zero(a);
+  int w = 0;
+  for (int t = t0; t < t1; t++) {
+    const uint16_t tm = term[t];
+    const int c = (int8_t)(tm >> 8);
+    lz_term(a, val(tm & 255), c);
+    w += c < 0 ? -c : c;
+  }
+  if (w > 4) lz_csub(a, WC_P4);
+  if (w > 2) lz_csub(a, WC_P2);
+  if (canonical && w > 1) lz_csub(a, P_);
+#pragma unroll
+  for (int j = 0; j < 12; j++) r.l[j] = a.l[j];
 }
 
 // dst = op(a, b).  Every lane of the workgroup (TPB = 64) must call it.
-// In-place (dst == a or b) is safe: all reads finish before the barrier that
-// precedes the writes.
-LB_DEV void wc_apply(wc_smem& S, int op, int dst, int a, int b) {
-  const wc_desc& d = LB_WC_OPS[op];
+//   1. lane k < K: x_k, y_k = lazy sums of operand coefficients; P_k = x_k y_k
+//   2. lane c < NC: partial sum of one output chunk (products and operands)
+//   3. lane o < 12: output o = sum of its chunks (canonical)
+// In-place (dst == a or b) is safe: phase 3 reads only the partial sums.
+// Out of line: ~500 call sites per final exponentiation would otherwise
+// inline into a kernel far larger than the instruction cache.
+LB_NOINL void wc_apply(wc_smem& S, int op, int dst, int a, int b) {
+  const wc_desc& d = S.ops[op];
   const int lane = threadIdx.x;
   const fp* A = S.slot[a];
   const fp* B = d.square ? S.slot[a] : S.slot[b];
   if (lane < d.K) {
     fp x, y;
-    fp_zero(x);
-    fp_zero(y);
     const int x0 = d.xoff[lane], y0 = d.yoff[lane], y1 = lane + 1 < d.K ? d.xoff[lane + 1] : d.yoff[d.K];
-    for (int t = x0; t < y0; t++) wc_acc(x, A[LB_WC_CODE[t] & 63], LB_WC_COEF[t]);
-    for (int t = y0; t < y1; t++) wc_acc(y, B[LB_WC_CODE[t] & 63], LB_WC_COEF[t]);
+    lz_sum(x, S.term, x0, y0, [&](int code) -> const fp& { return A[code & 63]; }, false);
+    lz_sum(y, S.term, y0, y1, [&](int code) -> const fp& { return B[code & 63]; }, false);
     fp p;
     fp_mul(p, x, y);
     S.prod[lane] = p;
   }
   __syncthreads();
-  fp o;
-  if (lane < 12) {
-    fp_zero(o);
-    for (int t = d.ooff[lane]; t < d.ooff[lane + 1]; t++) {
-      const uint8_t code = LB_WC_CODE[t];
-      const int idx = code & 63, kind = code >> 6;
-      const fp& v = kind == 0 ? A[idx] : kind == 1 ? S.slot[b][idx] : S.prod[idx];
-      wc_acc(o, v, LB_WC_COEF[t]);
-    }
+  if (lane < d.NC) {
+    const fp* Bo = S.slot[b];
+    fp part;
+    lz_sum(part, S.term, d.coff[lane], d.coff[lane + 1],
+           [&](int code) -> const fp& {
+             const int idx = code & 63, kind = code >> 6;
+             return kind == 0 ? A[idx] : kind == 1 ? Bo[idx] : S.prod[idx];
+           },
+           true);
+    S.part[lane] = part;
   }
   __syncthreads();
-  if (lane < 12) S.slot[dst][lane] = o;
+  if (lane < 12) {
+    const int c0 = d.cs[lane], c1 = d.cs[lane + 1];
+    fp o = S.part[c0];
+    for (int c = c0 + 1; c < c1; c++) fp_add(o, o, S.part[c]);
+    S.slot[dst][lane] = o;
+  }
   __syncthreads();
 }
 
@@ -141,17 +214,22 @@ LB_DEV void wc_exp_x(wc_smem& S, int dst, int src) {
   wc_apply(S, LB_WC_CONJ, dst, WC_ACC, WC_ACC);
 }
 
+// out = in^-1 for 12 Fp coefficients in LDS; out of line so its register
+// pressure (one lane, once per final exponentiation) stays out of the kernel
+LB_NOINL void wc_fp12_inv_lane(fp* out, const fp* in) {
+  fp12 f, fi;
+  fp* pf = &f.c0.c0.c0;
+  for (int i = 0; i < 12; i++) pf[i] = in[i];
+  fp12_inv(fi, f);
+  const fp* o = &fi.c0.c0.c0;
+  for (int i = 0; i < 12; i++) out[i] = o[i];
+}
+
 // slot dst = f^(3 (p^12 - 1)/r) for f in slot src (== final_exp in bls_pairing.h)
 LB_DEV void wc_final_exp(wc_smem& S, int dst, int src) {
   // easy part: f^(p^6 - 1) = conj(f) / f: the Fp12 inversion runs in lane 0
   wc_apply(S, LB_WC_CONJ, WC_T0, src, src);
-  if (threadIdx.x == 0) {
-    fp12 f, fi;
-    wc_store(f, S, src);
-    fp12_inv(fi, f);
-    fp* o = &fi.c0.c0.c0;
-    for (int i = 0; i < 12; i++) S.slot[WC_T1][i] = o[i];
-  }
+  if (threadIdx.x == 0) wc_fp12_inv_lane(S.slot[WC_T1], S.slot[src]);
   __syncthreads();
   wc_apply(S, LB_WC_MUL, WC_T0, WC_T0, WC_T1);
   wc_apply(S, LB_WC_FROB2, WC_T1, WC_T0, WC_G2);

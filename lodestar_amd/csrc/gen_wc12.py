@@ -267,6 +267,23 @@ def enc_terms(form, allowed):
     return out
 
 
+CHUNK = 8  # max sum |c| of one lane's lazily accumulated terms (< 8p < 2^384)
+
+
+def chunks(term_list):
+    """Split an output's terms into runs with sum |c| <= CHUNK."""
+    out, cur, w = [], [], 0
+    for c, code in term_list:
+        if cur and w + abs(c) > CHUNK:
+            out.append(cur)
+            cur, w = [], 0
+        cur.append((c, code))
+        w += abs(c)
+    if cur:
+        out.append(cur)
+    return out
+
+
 def main():
     path = sys.argv[1] if len(sys.argv) > 1 else "bls_wc12_tables.h"
     terms = []  # flat (coef, code)
@@ -277,20 +294,29 @@ def main():
         P, out = fn()
         K = len(P.prods)
         assert K <= 64
-        xoff, yoff, ooff = [], [], []
+        xoff, yoff = [], []
         for x, y in P.prods:
             xoff.append(len(terms))
-            terms += enc_terms(x, {"A"})
+            tx = enc_terms(x, {"A"})
+            assert sum(abs(c) for c, _ in tx) <= CHUNK
+            terms += tx
             yoff.append(len(terms))
-            terms += enc_terms(y, {"A"} if P.square else {"B"})
+            ty = enc_terms(y, {"A"} if P.square else {"B"})
+            assert sum(abs(c) for c, _ in ty) <= CHUNK
+            terms += ty
         yoff.append(len(terms))  # sentinel after the last product's y terms
-        flat = out.flat()
-        for o in flat:
-            ooff.append(len(terms))
-            terms += enc_terms(o, {"A", "B", "P"})
-        ooff.append(len(terms))
-        descs.append((name, K, P.square, xoff, yoff, ooff))
-        stats.append("%s: %d products, max out terms %d" % (name, K, max(ooff[i + 1] - ooff[i] for i in range(12))))
+        coff, cs = [], []
+        for o in out.flat():
+            cs.append(len(coff))
+            for ch in chunks(enc_terms(o, {"A", "B", "P"})):
+                coff.append(len(terms))
+                terms += ch
+        cs.append(len(coff))
+        coff.append(len(terms))
+        nc = len(coff) - 1
+        assert nc <= 64, (name, nc)
+        descs.append((name, K, P.square, xoff, yoff, nc, coff, cs))
+        stats.append("%s: %d products, %d output chunks" % (name, K, nc))
     assert len(terms) < 65536
     lines.append("// " + "; ".join(stats))
     lines.append("#define LB_WC_NTERMS %d" % len(terms))
@@ -298,15 +324,19 @@ def main():
         len(terms), ", ".join(str(c) for c, _ in terms)))
     lines.append("__device__ __constant__ const uint8_t LB_WC_CODE[%d] = {%s};" % (
         len(terms), ", ".join(str(x) for _, x in terms)))
-    lines.append("struct wc_desc {\n  uint8_t K, square;\n  uint16_t xoff[64], yoff[65], ooff[13];\n};")
-    for i, (name, K, sq, xoff, yoff, ooff) in enumerate(descs):
-        lines.append("#define LB_WC_%s %d" % (name, i))
+    lines.append("// per op: K products (lane k: x terms [xoff[k], yoff[k]), y terms up to the next xoff /\n"
+                 "// yoff[K]); NC output chunks (lane c: terms [coff[c], coff[c+1]), sum |coef| <= 8);\n"
+                 "// output o = sum of chunks [cs[o], cs[o+1])")
+    lines.append("struct wc_desc {\n  uint8_t K, square, NC, pad;\n  uint16_t xoff[64], yoff[65], coff[65], cs[13];\n};")
+    for i, d in enumerate(descs):
+        lines.append("#define LB_WC_%s %d" % (d[0], i))
+    lines.append("#define LB_WC_NOPS %d" % len(descs))
     body = []
-    for name, K, sq, xoff, yoff, ooff in descs:
-        xo = xoff + [0] * (64 - len(xoff))
-        yo = yoff + [0] * (65 - len(yoff))
-        body.append("{%d, %d, {%s}, {%s}, {%s}}" % (K, int(sq), ", ".join(map(str, xo)), ", ".join(map(str, yo)),
-                                                    ", ".join(map(str, ooff))))
+    for name, K, sq, xoff, yoff, nc, coff, cs in descs:
+        pad = lambda v, n: v + [0] * (n - len(v))  # noqa: E731
+        body.append("{%d, %d, %d, 0, {%s}, {%s}, {%s}, {%s}}" % (
+            K, int(sq), nc, ", ".join(map(str, pad(xoff, 64))), ", ".join(map(str, pad(yoff, 65))),
+            ", ".join(map(str, pad(coff, 65))), ", ".join(map(str, cs))))
     lines.append("__device__ __constant__ const wc_desc LB_WC_OPS[%d] = {\n  %s};" % (len(descs), ",\n  ".join(body)))
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")

@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_
     if (threadIdx.x == 0) valid[k] = req_bad[k] ? 0 : 1;
     return;
   }
+  wc_init_tables(S);
   wc_init_gammas(S);
   wc_miller_from_lines(S, WC_FS, lines, n_pairs, (size_t)base + k);
   wc_load12(S, WC_F, F[k]);

@@ -18,14 +18,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT_DIR = os.path.join(ROOT, "tools", "opcount_build")
-MADS_PER_FPMUL = 288  # 12x12 limb products + 12x12 reduction products (CIOS, 32-bit limbs)
+MADS_PER_FPMUL = 288  # 12x12 limb products + 12x12 reduction products (bls_fp_ps.h)
+MADS_PER_FPSQR = 224  # 66 cross (+2 doubled lone cross) + 12 squares + 144 reduction products
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--run", action="store_true")
-    ap.add_argument("--sets", type=int, default=256)
+    ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--per-request", type=int, default=128)
     a = ap.parse_args()
     from lodestar_amd import build as b
@@ -34,6 +35,8 @@ def main():
     if not a.run:
         return
     import numpy as np
+    # the bench's organisation (stored lines + multi-pair accumulation, merged check)
+    os.environ["LB_MILLER"] = "lines"
     from lodestar_amd import native
     native.library_path = lambda: os.path.join(OUT_DIR, "liblodestar_bls_count.so")
     native._lib = None
@@ -57,11 +60,17 @@ def main():
     k = lib.lb_opcount_stages(dev._h, buf, 16)
     n_req = len(req) - 1
     per = {}
+    tot_mul = tot_sqr = 0
     for i in range(k):
-        per[names[i]] = {"fp_mul_total": int(buf[i]), "fp_mul_per_set": buf[i] / n}
-    total = sum(int(buf[i]) for i in range(k))
+        muls, sqrs = int(buf[i]) & 0xFFFFFFFF, int(buf[i]) >> 32
+        tot_mul += muls
+        tot_sqr += sqrs
+        per[names[i]] = {"fp_mul_total": muls, "fp_sqr_total": sqrs, "fp_mul_per_set": (muls + sqrs) / n,
+                         "mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n}
     out = {"sets": n, "requests": n_req, "sets_per_request": a.per_request, "mads_per_fp_mul": MADS_PER_FPMUL,
-           "stages": per, "fp_mul_per_set_total": total / n, "mads_per_set_total": total / n * MADS_PER_FPMUL}
+           "mads_per_fp_sqr": MADS_PER_FPSQR, "organisation": "LB_MILLER=lines, merged check",
+           "stages": per, "fp_mul_per_set_total": (tot_mul + tot_sqr) / n,
+           "mads_per_set_total": (tot_mul * MADS_PER_FPMUL + tot_sqr * MADS_PER_FPSQR) / n}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "op_counts.json"), "w") as f:
         json.dump(out, f, indent=1)
