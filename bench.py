@@ -215,6 +215,12 @@ def main():
             roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
                     "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
                     "algorithmic_mads_per_launch": mads}
+            if "mads_per_set_total" in oc:
+                # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
+                pipe = value * oc["mads_per_set_total"] / 1e12
+                roof["pipeline_achieved"] = round(pipe, 4)
+                roof["pipeline_frac"] = round(pipe / peak, 5)
+                roof["mads_per_set"] = round(oc["mads_per_set_total"])
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         # the box's CPU share is 16 threads per GPU (os.cpu_count() shows the whole host)

@@ -1,0 +1,62 @@
+"""Summarise tools/pmc.sh passes into profiles/pmc_traffic.json (per pipeline
+stage: kernel, counters averaged per launch, HBM bytes per launch).
+
+hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE and
+WRITE_SIZE are KiB from the L2's memory-side request counters; on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced reads
+(/opt/skills/guides/MI355X_MICROARCH.md, HBM section), hence the factor 2
+(an upper bound for narrower accesses).
+
+usage: python tools/pmc_summarize.py PMC_DIR [OUT.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
+    "hash_half": "k_hash_half", "hash_finish": "k_hash_finish", "req_flags": "k_req_flags",
+    "pubkeys": "k_pubkeys_single", "scalar_pk": "k_scalar_pk", "lines": "k_lines",
+    "decode_sigs": "k_decode_sigs", "scalar_sig": "k_scalar_sig", "sum_tree": "k_sum_tree",
+    "miller_acc": "k_miller_acc", "merge": "k_merge", "lines_S": "k_lines_S", "tail": "k_tail",
+}
+
+
+def kernel_key(name):
+    """'void lb::k_lines<1>(unsigned int, ...)' -> 'k_lines'"""
+    n = name.split("(")[0].replace("void ", "").replace("lb::", "").strip()
+    return n.split("<")[0]
+
+
+def main():
+    d = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                                              "pmc_traffic.json")
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-launch values]
+    full = {}
+    for f in glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = kernel_key(row["Kernel_Name"])
+            full[k] = row["Kernel_Name"]
+            vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    res = {"_note": __doc__.strip().split("\n\n")[1].replace("\n", " ")}
+    for stage, prefix in STAGE_OF.items():
+        if prefix not in vals:
+            continue
+        k = prefix
+        c = {n: sum(v) / len(v) for n, v in vals[k].items()}
+        ent = {"kernel": full[k].split("(")[0], "counters": {n: round(x, 3) for n, x in c.items()}}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            ent["hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+        if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c and c["SQ_WAVES"]:
+            ent["valu_insts_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"])
+        res[stage] = ent
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
