@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--sets", type=int, default=65536)
     ap.add_argument("--per-request", type=int, default=128)
     ap.add_argument("--latency-reps", type=int, default=10)
+    ap.add_argument("--iso-reps", type=int, default=3,
+                    help="sync calls after the timed region whose stage times price the dominant kernel")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
@@ -178,6 +180,15 @@ def main():
         elapsed = float(t.item())
     ok = all(bool(v.cpu().numpy().all()) for v in d_valid) and not any(bool(e.cpu().numpy().any()) for e in d_err)
 
+    # the same call, one at a time: per-kernel durations without other calls'
+    # kernels sharing the CUs (the roofline of the dominant kernel is priced on these)
+    iso = {}
+    for k in range(a.iso_reps):
+        step(k)
+        for name, ms in dev.last_stage_times():
+            iso.setdefault(name, []).append(ms)
+    iso_ms = {k: float(np.median(v)) for k, v in iso.items()}
+
     # p50 latency of one 128-set batch (one request)
     lat = []
     if a.latency_reps > 0:
@@ -199,14 +210,15 @@ def main():
     # roofline over the dominant kernel
     roof = None
     counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
-    dom = max((k for k in stage_ms if k not in ("start", "h2d", "d2h")), key=lambda k: stage_ms[k])
+    timing = iso_ms if iso_ms else stage_ms
+    dom = max((k for k in timing if k not in ("start", "h2d", "d2h")), key=lambda k: timing[k])
     if os.path.exists(counts_path):
         oc = json.load(open(counts_path))
         st = oc["stages"].get(dom)
         if st:
             per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
             mads = per_set * n
-            achieved = mads / (stage_ms[dom] * 1e-3) / 1e12
+            achieved = mads / (timing[dom] * 1e-3) / 1e12
             peak = PEAK_MAD_PER_S / 1e12
             traffic = None
             pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -214,7 +226,14 @@ def main():
                 traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
             roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
                     "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
-                    "algorithmic_mads_per_launch": mads}
+                    "algorithmic_mads_per_launch": mads,
+                    "launch_ms": round(timing[dom], 3),
+                    "timing": "median of %d one-at-a-time calls after the timed region (HIP events on the "
+                              "kernel's stream)" % a.iso_reps if iso_ms else "timed region, calls overlapped"}
+            if iso_ms and dom in stage_ms:
+                # the same kernel while other calls' kernels share the CUs (timed region)
+                roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
+                roof["in_pipeline_frac"] = round(mads / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
             if "mads_per_set_total" in oc:
                 # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
                 pipe = value * oc["mads_per_set_total"] / 1e12
@@ -252,6 +271,7 @@ def main():
         "all_valid": ok,
         "overlap": "sync" if a.sync else f"{nbuf} calls in flight (lb_verify_requests_device_async)",
         "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+        "iso_stage_ms": {k: round(v, 3) for k, v in iso_ms.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
         "datagen_s": round(t_gen, 2),

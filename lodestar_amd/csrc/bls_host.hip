@@ -76,11 +76,13 @@ struct lb_ctx {
   uint64_t next_ticket = 1;
   std::string err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
-  // Miller organisation: one pair per lane (k_miller_sets, lowest latency) for
-  // small calls; stored lines + multi-pair accumulation (k_lines/k_miller_acc)
-  // from lines_min_sets up.  LB_MILLER=lane|lines forces one.
-  int miller_mode = 0;  // 0 auto, 1 lane, 2 lines
+  // Miller organisation: stored lines + one wave per pair (k_lines/k_pair_wc,
+  // lowest latency) up to wave_max_sets; one pair per lane (k_miller_sets)
+  // below lines_min_sets; stored lines + multi-pair accumulation per request
+  // (k_lines/k_miller_acc, highest throughput) from there.  LB_MILLER=wave|lane|lines forces one.
+  int miller_mode = 0;  // 0 auto, 1 lane, 2 lines, 3 wave
   uint32_t lines_min_sets = 8192;
+  uint32_t wave_max_sets = 1024;
   int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
   int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
@@ -226,12 +228,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g1j* d_pk = ws.take<g1j>(ns);
   g1j* d_rpk = ws.take<g1j>(ns);
   const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets);
-  fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);
+  const bool by_wave =
+      !by_lines && (ctx->miller_mode == 3 || (ctx->miller_mode == 0 && n_sets <= ctx->wave_max_sets));
+  fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);  // per-set Miller values (lane / wave modes)
   const bool tail_wave = ctx->tail_wave;
   // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
   const bool merged = tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req;
   const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
-  uint32_t* d_lines = (by_lines || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
+  uint32_t* d_lines =
+      (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
   uint8_t* d_pk_st = ws.take<uint8_t>(ns);
   uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
@@ -260,7 +265,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
-  if (n_sets && by_lines) {
+  if (n_sets && (by_lines || by_wave)) {
     if (ctx->lines_waves == 1)
       LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
@@ -268,7 +273,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_STAGE("lines", 1, k_lines<2>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
   }
-  else if (n_sets)
+  if (n_sets && by_wave)
+    LB_STAGE("miller_wave", 1, k_pair_wc, n_sets, TPB, n_sets, n_pairs, (const uint32_t*)d_lines, d_f);
+  else if (n_sets && !by_lines)
     LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1j*)d_rpk, (const g2j*)d_h,
              d_f);
   if (n_sets) {
@@ -399,7 +406,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
     const int v = atoi(e);
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
   }
-  if (const char* e = getenv("LB_MILLER")) ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : 0;
+  if (const char* e = getenv("LB_MILLER"))
+    ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : strcmp(e, "wave") == 0 ? 3 : 0;
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;

@@ -120,6 +120,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_
                                                        const uint8_t* __restrict__ req_bad,
                                                        uint8_t* __restrict__ valid,
                                                        const uint8_t* __restrict__ skip);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t n_pairs,
+                                                          const uint32_t* __restrict__ lines, fp12* __restrict__ f);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,

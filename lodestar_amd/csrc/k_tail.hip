@@ -48,6 +48,19 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_
   if (threadIdx.x == 0) valid[k] = wc_is_one(S, WC_F) ? 1 : 0;
 }
 
+// Miller value of each set pair from its stored lines, one wave per pair
+// (wave-cooperative; the latency path for small calls, where one lane per pair
+// would run a ~6.5k-product chain)
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t n_pairs,
+                                                          const uint32_t* __restrict__ lines, fp12* __restrict__ f) {
+  __shared__ wc_smem S;
+  const uint32_t q = blockIdx.x;
+  if (q >= n) return;
+  wc_init_tables(S);
+  wc_miller_from_lines(S, WC_FS, lines, n_pairs, q);
+  if (threadIdx.x < 12) (&f[q].c0.c0.c0)[threadIdx.x] = S.slot[WC_FS][threadIdx.x];
+}
+
 // Merged check of a whole call (the worker's merged batch, worker.ts:41-96):
 // S_all = sum S_k and F_all = prod F_k over the requests not already false.
 // One wave; the tail kernel then verifies (F_all, S_all) once, and the

@@ -23,11 +23,12 @@ def device():
     dev.close()
 
 
-@pytest.fixture(scope="session", params=["lane", "lines"])
+@pytest.fixture(scope="session", params=["lane", "lines", "wave"])
 def device_modes(request):
-    """A context per Miller organisation: one pair per lane (k_miller_sets) and
-    stored lines + multi-pair accumulation (k_lines / k_miller_acc), which the
-    library otherwise picks only for calls of >= 8192 sets."""
+    """A context per Miller organisation: one pair per lane (k_miller_sets),
+    stored lines + multi-pair accumulation (k_lines / k_miller_acc, which the
+    library otherwise picks only for calls of >= 8192 sets) and stored lines +
+    one wave per pair (k_lines / k_pair_wc, picked for calls of <= 1024 sets)."""
     import os
     from lodestar_amd.native import Device
     old = os.environ.get("LB_MILLER")
