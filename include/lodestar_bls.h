@@ -111,6 +111,11 @@ typedef struct {
   const uint8_t* signatures;       /* concatenated signature bytes                           */
   const uint32_t* sig_offsets;     /* n_sets + 1 byte offsets into signatures                */
   const uint8_t* seed;             /* 32 bytes of batch randomness seed                      */
+  /* Optional (NULL => use `pubkeys`): pk_offsets[n_sets] (or n_sets) u32 validator
+   * indices into the context's device-resident pubkey table (lb_pubkey_table_append);
+   * `pubkeys` is then ignored and may be NULL.  An index >= the table size makes
+   * its request LB_REQ_BAD_PUBKEY (the reference would index index2pubkey out of range). */
+  const uint32_t* pubkey_indices;
 } lb_request_batch;
 
 typedef struct {
@@ -169,6 +174,35 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys, uint8_
  * encoding.  *out_bad_index = index of the first invalid signature or -1. */
 int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* signatures, const uint32_t* sig_offsets,
                             uint8_t* out192, int32_t* out_bad_index);
+
+/* ---- device-resident pubkey table ----------------------
+ * Mirror of the beacon node's index2pubkey cache
+ * (state-transition/src/cache/pubkeyCache.ts:56-77 syncPubkeys, held in
+ * epochCache.ts:765): validators' pubkeys are decoded ONCE into HBM (affine,
+ * Montgomery form, ~100 B per key; 2M validators ~200 MB of the 288 GB), so
+ * aggregate sets ship 4-byte validator indices instead of 96-byte points and
+ * the main-thread aggregation (chain/bls/utils.ts:13, jobItem.ts:80) moves to
+ * the GPU.
+ *
+ * Append n keys (pk_len = 48 compressed, as the state holds them, or 96
+ * uncompressed) at indices [size, size + n).  Decode semantics are those of
+ * PublicKey.fromBytes without validation (syncPubkeys: "Do not do any
+ * validation here"): a key that fails to decode makes the whole call fail with
+ * LB_ERR_INVALID_ARGUMENT, nothing is appended and *out_bad_index (optional)
+ * names the first bad key, else -1.  Waits for calls in flight. */
+int lb_pubkey_table_append(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys, uint32_t pk_len, int32_t* out_bad_index);
+/* Number of keys in the table. */
+int lb_pubkey_table_size(const lb_ctx* ctx, uint32_t* out_n);
+/* Table entries [first, first + n) re-encoded as 96-byte uncompressed points. */
+int lb_pubkey_table_read(lb_ctx* ctx, uint32_t first, uint32_t n, uint8_t* out96);
+/* Truncate the table to n keys (n <= size). */
+int lb_pubkey_table_truncate(lb_ctx* ctx, uint32_t n);
+/* lb_aggregate_pubkeys over table entries: sum of table[indices[0..n)] ->
+ * 96-byte uncompressed (committee aggregation from validator indices).
+ * n == 0 -> LB_ERR_INVALID_ARGUMENT (EMPTY_AGGREGATE_ARRAY); an index out of
+ * range -> *out_status = LB_SET_BAD_ENCODING. */
+int lb_aggregate_pubkeys_indexed(lb_ctx* ctx, uint32_t n, const uint32_t* indices, uint8_t* out96,
+                                 uint8_t* out_status);
 
 /* ---- stage-level entry points (parity tests against the CPU oracle) ----- */
 /* hash_to_G2(msg_i) -> 192-byte uncompressed affine encoding each */

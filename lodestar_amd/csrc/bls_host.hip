@@ -91,6 +91,9 @@ struct lb_ctx {
   // merged check of the whole call first (one tail), per-request tails only
   // when it fails; used from merge_min_req requests up (LB_MERGE_MIN, 0 = off)
   uint32_t merge_min_req = 8;
+  // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
+  g1a* d_table = nullptr;
+  uint32_t table_n = 0, table_cap = 0;
   // timing of the last completed verify call
   int n_stages = 0;
   float stage_ms[Slot::kMaxStages] = {};
@@ -217,7 +220,7 @@ int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
 // original one-pair-per-lane Miller (k_miller_sets + k_prod_tree) remains
 // selectable with LB_MILLER=lane for comparison.
 int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
-                 const uint8_t* d_pks, const uint32_t* d_pk_off, const uint8_t* d_msgs, const uint8_t* d_sigs,
+                 const uint8_t* d_pks, const uint32_t* d_pk_off, const uint32_t* d_pk_idx, const uint8_t* d_msgs, const uint8_t* d_sigs,
                  const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
                  uint8_t* d_set_status, Bump& ws) {
   const uint32_t ns = n_sets ? n_sets : 1;
@@ -258,9 +261,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   }
   LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
   if (n_sets) {
-    LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
+    const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
+    LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
     if (d_pk_off)
-      LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, 2048u, TPB, n_sets, d_pks, d_pk_off, d_pk, d_pk_st);
+      LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, 2048u, TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
     LB_STAGE("scalar_pk", 0, k_scalar_pk, blocks_for(n_sets), TPB, n_sets, d_seed, (const g1j*)d_pk,
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
@@ -338,7 +342,7 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
   if (!b || !b->request_offsets || !b->messages || !b->signatures || !b->sig_offsets || !b->seed ||
-      (b->n_sets && !b->pubkeys)) {
+      (b->n_sets && !b->pubkeys && !b->pubkey_indices)) {
     ctx->err = "null pointer in lb_request_batch";
     return LB_ERR_INVALID_ARGUMENT;
   }
@@ -458,6 +462,7 @@ int lb_destroy(lb_ctx* ctx) {
     for (int i = 0; i < ctx->streams_per_slot[s]; i++)
       if (sl.st[i]) (void)hipStreamDestroy(sl.st[i]);
   }
+  if (ctx->d_table) (void)hipFree(ctx->d_table);
   delete ctx;
   return LB_OK;
 }
@@ -491,7 +496,8 @@ static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   LB_TRY(begin_call(ctx, sl));
   if (b->n_requests)
-    LB_TRY(run_pipeline(ctx, sl, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets, b->messages,
+    LB_TRY(run_pipeline(ctx, sl, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets,
+                        b->pubkey_indices, b->messages,
                         b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err, d_set_status, ws));
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
@@ -579,10 +585,11 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
       }
   }
   const size_t n_pk = pk_off ? pk_off[ns] : ns;
+  const bool by_index = b->pubkey_indices != nullptr;
   const size_t sig_bytes = b->sig_offsets[ns];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = pk_off ? sizeof(uint32_t) * (ns + 1) : 0,
-               sz_pk = n_pk * 96, sz_msg = (size_t)ns * 32, sz_sigo = sizeof(uint32_t) * (ns + 1),
+               sz_pk = n_pk * (by_index ? sizeof(uint32_t) : 96), sz_msg = (size_t)ns * 32, sz_sigo = sizeof(uint32_t) * (ns + 1),
                sz_sig = sig_bytes, sz_seed = 32;
   const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
   const size_t out_bytes = al(nr) * 2 + al(ns ? ns : 1);
@@ -599,7 +606,7 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   };
   stage(b->request_offsets, sz_req);
   if (pk_off) stage(pk_off, sz_pko);
-  stage(b->pubkeys, sz_pk);
+  stage(by_index ? (const void*)b->pubkey_indices : (const void*)b->pubkeys, sz_pk);
   stage(b->messages, sz_msg);
   stage(b->sig_offsets, sz_sigo);
   stage(b->signatures, sz_sig);
@@ -623,7 +630,8 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
   const uint8_t* d_sig = (const uint8_t*)dptr(sz_sig);
   const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
-  LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, d_pks, d_pko, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
+  LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? nullptr : d_pks, d_pko,
+                      by_index ? (const uint32_t*)d_pks : nullptr, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
   char* h_out = h + in_bytes;
   LB_HIP(hipMemcpyAsync(h_out, d_valid, nr, hipMemcpyDeviceToHost, sl.st[0]));
   LB_HIP(hipMemcpyAsync(h_out + al(nr), d_err, nr, hipMemcpyDeviceToHost, sl.st[0]));
@@ -711,8 +719,125 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint8_t* o
   g1j* d_pk = ws.take<g1j>(1);
   uint8_t* d_st = ws.take<uint8_t>(1);
   uint8_t* d_out = ws.take<uint8_t>(96);
-  LB_LAUNCH(k_pubkeys_single, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
-  LB_LAUNCH(k_pubkeys_agg, 1, TPB, 1u, (const uint8_t*)d_p, (const uint32_t*)d_off, d_pk, d_st);
+  const PkSource src{(const uint8_t*)d_p, nullptr, nullptr, 0};
+  LB_LAUNCH(k_pubkeys_single, 1, TPB, 1u, src, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_pubkeys_agg, 1, TPB, 1u, src, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_g1_serialize, 1, TPB, 1u, (const g1j*)d_pk, d_out);
+  uint8_t st = 0;
+  LB_HIP(hipMemcpyAsync(out96, d_out, 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipMemcpyAsync(&st, d_st, 1, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  if (st == LB_ST_PK_INFINITY) st = LB_ST_OK;  // an infinite aggregate is a valid encoding (0x40...)
+  if (out_status) *out_status = st;
+  return LB_OK;
+}
+
+// ---- device-resident pubkey table (index2pubkey mirror) ------------------------
+int lb_pubkey_table_append(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint32_t pk_len, int32_t* out_bad_index) {
+  if (!ctx || (n && !pks) || (pk_len != 48 && pk_len != 96)) return LB_ERR_INVALID_ARGUMENT;
+  if (out_bad_index) *out_bad_index = -1;
+  if (n == 0) return LB_OK;
+  if ((uint64_t)ctx->table_n + n > 0x7fffffffu) {
+    ctx->err = "pubkey table full";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));  // calls in flight read the table
+  const uint32_t need = ctx->table_n + n;
+  if (need > ctx->table_cap) {
+    uint64_t cap = (uint64_t)ctx->table_cap * 2;
+    if (cap < need) cap = need;
+    if (cap < 4096) cap = 4096;
+    if (cap > 0x7fffffffu) cap = 0x7fffffffu;
+    g1a* d = nullptr;
+    if (hipMalloc(&d, sizeof(g1a) * cap) != hipSuccess) {
+      ctx->err = "hipMalloc pubkey table failed";
+      return LB_ERR_OUT_OF_MEMORY;
+    }
+    if (ctx->table_n)
+      LB_HIP(hipMemcpyAsync(d, ctx->d_table, sizeof(g1a) * ctx->table_n, hipMemcpyDeviceToDevice, ctx->stream));
+    LB_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_table) LB_HIP(hipFree(ctx->d_table));
+    ctx->d_table = d;
+    ctx->table_cap = (uint32_t)cap;
+  }
+  // decode straight into the table tail, in chunks that bound the staging workspace;
+  // table_n only advances once every key decoded
+  const uint32_t chunk = 1u << 20;
+  std::vector<uint8_t> st;
+  for (uint32_t first = 0; first < n; first += chunk) {
+    const uint32_t m = n - first < chunk ? n - first : chunk;
+    LB_TRY(ensure_ws(ctx, (size_t)m * (pk_len + 1) + 4096));
+    Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+    void* d_in;
+    LB_TRY(upload(ctx, ws, pks + (size_t)first * pk_len, (size_t)m * pk_len, &d_in));
+    uint8_t* d_st = ws.take<uint8_t>(m);
+    LB_LAUNCH(k_table_decode, blocks_for(m), TPB, m, (const uint8_t*)d_in, pk_len, ctx->d_table + ctx->table_n + first,
+              d_st);
+    st.resize(m);
+    LB_HIP(hipMemcpyAsync(st.data(), d_st, m, hipMemcpyDeviceToHost, ctx->stream));
+    LB_HIP(hipStreamSynchronize(ctx->stream));
+    for (uint32_t i = 0; i < m; i++)
+      if (st[i] != LB_ST_OK) {
+        if (out_bad_index) *out_bad_index = (int32_t)(first + i);
+        ctx->err = "pubkey fails PublicKey.fromBytes (bad encoding / not on curve)";
+        return LB_ERR_INVALID_ARGUMENT;
+      }
+  }
+  ctx->table_n = need;
+  return LB_OK;
+}
+
+int lb_pubkey_table_size(const lb_ctx* ctx, uint32_t* out_n) {
+  if (!ctx || !out_n) return LB_ERR_INVALID_ARGUMENT;
+  *out_n = ctx->table_n;
+  return LB_OK;
+}
+
+int lb_pubkey_table_truncate(lb_ctx* ctx, uint32_t n) {
+  if (!ctx || n > ctx->table_n) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  ctx->table_n = n;
+  return LB_OK;
+}
+
+int lb_pubkey_table_read(lb_ctx* ctx, uint32_t first, uint32_t n, uint8_t* out96) {
+  if (!ctx || (n && !out96) || (uint64_t)first + n > ctx->table_n) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  LB_TRY(ensure_ws(ctx, (size_t)n * 96 + 4096));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
+  LB_LAUNCH(k_g1a_serialize, blocks_for(n), TPB, n, (const g1a*)(ctx->d_table + first), d_out);
+  LB_HIP(hipMemcpyAsync(out96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_aggregate_pubkeys_indexed(lb_ctx* ctx, uint32_t n, const uint32_t* indices, uint8_t* out96,
+                                 uint8_t* out_status) {
+  if (!ctx || !out96 || (n && !indices)) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) {
+    ctx->err = "EMPTY_AGGREGATE_ARRAY";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  LB_TRY(ensure_ws(ctx, (size_t)n * 4 + 8192));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  void* d_idx;
+  LB_TRY(upload(ctx, ws, indices, (size_t)n * 4, &d_idx));
+  uint32_t off[2] = {0, n};
+  void* d_off;
+  LB_TRY(upload(ctx, ws, off, sizeof(off), &d_off));
+  g1j* d_pk = ws.take<g1j>(1);
+  uint8_t* d_st = ws.take<uint8_t>(1);
+  uint8_t* d_out = ws.take<uint8_t>(96);
+  const PkSource src{nullptr, (const uint32_t*)d_idx, ctx->d_table, ctx->table_n};
+  LB_LAUNCH(k_pubkeys_single, 1, TPB, 1u, src, (const uint32_t*)d_off, d_pk, d_st);
+  LB_LAUNCH(k_pubkeys_agg, 1, TPB, 1u, src, (const uint32_t*)d_off, d_pk, d_st);
   LB_LAUNCH(k_g1_serialize, 1, TPB, 1u, (const g1j*)d_pk, d_out);
   uint8_t st = 0;
   LB_HIP(hipMemcpyAsync(out96, d_out, 96, hipMemcpyDeviceToHost, ctx->stream));

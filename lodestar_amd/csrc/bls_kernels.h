@@ -48,18 +48,45 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 
 
 namespace lb {
+// Where a set's pubkeys come from: the call's 96-byte uncompressed encodings
+// (the worker wire format, chain/bls/multithread/worker.ts:110-116) or the
+// device-resident pubkey table addressed by validator index (the index2pubkey
+// mirror, state-transition/src/cache/pubkeyCache.ts:56-77; lb_pubkey_table_*).
+struct PkSource {
+  const uint8_t* bytes;   // pk_offsets[n_sets] x 96 B (when index == nullptr)
+  const uint32_t* index;  // pk_offsets[n_sets] validator indices, or nullptr
+  const g1a* table;       // decoded affine table entries
+  uint32_t table_n;
+};
+// Pubkey k of the call; an index outside the table is a bad pubkey (LB_REQ_BAD_PUBKEY).
+LB_DEV uint8_t pk_load(g1a& p, const PkSource& s, uint32_t k) {
+  if (s.index) {
+    const uint32_t j = s.index[k];
+    if (j >= s.table_n) {
+      p.inf = true;
+      return LB_ST_BAD_ENCODING;
+    }
+    p = s.table[j];
+    return LB_ST_OK;
+  }
+  return g1_deserialize(p, s.bytes + (size_t)k * 96, 96);
+}
+
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint8_t* __restrict__ single_flag);
 __global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                      const uint32_t* __restrict__ sig_off,
                                                      const uint8_t* __restrict__ single_flag,
                                                      g2j* __restrict__ out_sig, uint8_t* __restrict__ status);
-__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, PkSource pks,
                                                         const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                         uint8_t* __restrict__ pk_status);
-__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource pks,
                                                      const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                      uint8_t* __restrict__ pk_status);
+__global__ void __launch_bounds__(TPB) k_table_decode(uint32_t n, const uint8_t* __restrict__ in, uint32_t len,
+                                                      g1a* __restrict__ out, uint8_t* __restrict__ status);
+__global__ void k_g1a_serialize(uint32_t n, const g1a* __restrict__ in, uint8_t* __restrict__ out96);
 __global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
 __global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);

@@ -43,6 +43,25 @@ __global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* 
   jac_to_aff(a, p);
   g2_serialize(out192 + (size_t)i * 192, a);
 }
+// ---- device-resident pubkey table (index2pubkey mirror) ----------------------
+// syncPubkeys (state-transition/src/cache/pubkeyCache.ts:56-77) pushes
+// PublicKey.fromBytes(pubkey) per new validator: decode only (48-byte
+// compressed as the state holds it, or 96-byte uncompressed), no group check.
+__global__ void __launch_bounds__(TPB) k_table_decode(uint32_t n, const uint8_t* __restrict__ in, uint32_t len,
+                                                      g1a* __restrict__ out, uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a p;
+  status[i] = g1_deserialize(p, in + (size_t)i * len, len);
+  out[i] = p;
+}
+__global__ void k_g1a_serialize(uint32_t n, const g1a* __restrict__ in, uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a a = in[i];
+  g1_serialize(out96 + (size_t)i * 96, a);
+}
+
 __global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, co
 }
 
 // Sets with exactly one pubkey (the common case): one lane per set.
-__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, PkSource pks,
                                                         const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                         uint8_t* __restrict__ pk_status) {
   const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const u
   uint8_t st = LB_ST_EMPTY_AGGREGATE;
   if (b == a + 1) {
     g1a p;
-    st = g1_deserialize(p, pks + (size_t)a * 96, 96);
+    st = pk_load(p, pks, a);
     if (st == LB_ST_OK) {
       jac_from_aff(acc, p);
       if (p.inf) st = LB_ST_PK_INFINITY;
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, const u
 
 // Sets with >= 2 pubkeys (PublicKey.aggregate, chain/bls/utils.ts:13): one
 // wave per set, grid-stride over sets; lanes decode strided, LDS tree sum.
-__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource pks,
                                                      const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                      uint8_t* __restrict__ pk_status) {
   __shared__ g1j sh[TPB];
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, const uint
     jac_set_inf(acc);
     for (uint32_t k = a + threadIdx.x; k < b; k += TPB) {
       g1a p;
-      const uint8_t st = g1_deserialize(p, pks + (size_t)k * 96, 96);
+      const uint8_t st = pk_load(p, pks, k);
       if (st != LB_ST_OK) {
         atomicOr(&bad, 1u);
       } else {

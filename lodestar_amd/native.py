@@ -35,6 +35,8 @@ EXPORTED_SYMBOLS = (
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
     "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
+    "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
+    "lb_aggregate_pubkeys_indexed",
 )
 
 
@@ -68,6 +70,7 @@ class _RequestBatch(ctypes.Structure):
         ("signatures", ctypes.c_void_p),
         ("sig_offsets", ctypes.c_void_p),
         ("seed", ctypes.c_void_p),
+        ("pubkey_indices", ctypes.c_void_p),
     ]
 
 
@@ -110,6 +113,11 @@ def load_library() -> ctypes.CDLL:
                                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_Stats)]
     lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
+    lib.lb_pubkey_table_append.argtypes = [vp, u32, vp, u32, ctypes.POINTER(ctypes.c_int32)]
+    lib.lb_pubkey_table_size.argtypes = [vp, ctypes.POINTER(u32)]
+    lib.lb_pubkey_table_read.argtypes = [vp, u32, u32, vp]
+    lib.lb_pubkey_table_truncate.argtypes = [vp, u32]
+    lib.lb_aggregate_pubkeys_indexed.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
     for name in EXPORTED_SYMBOLS:
@@ -179,7 +187,9 @@ class Device:
     # -- hot path ------------------------------------------------------------
     def verify_requests(self, request_offsets: np.ndarray, pubkeys: np.ndarray, pk_offsets: Optional[np.ndarray],
                         messages: np.ndarray, sig_blob: np.ndarray, sig_offsets: np.ndarray, seed: bytes,
-                        batchable: Optional[np.ndarray] = None) -> VerifyResult:
+                        batchable: Optional[np.ndarray] = None,
+                        pk_indices: Optional[np.ndarray] = None) -> VerifyResult:
+        """pk_indices (u32 validator indices into the device pubkey table) replaces pubkeys when given."""
         request_offsets = np.ascontiguousarray(request_offsets, dtype=np.uint32)
         n_req = len(request_offsets) - 1
         n_sets = int(request_offsets[-1]) if n_req >= 0 else 0
@@ -190,8 +200,12 @@ class Device:
         pk_offsets = None if pk_offsets is None else np.ascontiguousarray(pk_offsets, dtype=np.uint32)
         seed_a = _u8(seed)
         assert len(seed_a) == 32
+        if pk_indices is not None:
+            pk_indices = np.ascontiguousarray(pk_indices, dtype=np.uint32)
+            if len(pk_indices) == 0:
+                pk_indices = np.zeros(1, np.uint32)
         b = _RequestBatch(n_req, n_sets, _ptr(request_offsets), _ptr(batchable), _ptr(pubkeys), _ptr(pk_offsets),
-                          _ptr(messages), _ptr(sig_blob), _ptr(sig_offsets), _ptr(seed_a))
+                          _ptr(messages), _ptr(sig_blob), _ptr(sig_offsets), _ptr(seed_a), _ptr(pk_indices))
         valid = np.zeros(max(n_req, 1), np.uint8)
         err = np.zeros(max(n_req, 1), np.uint8)
         sst = np.zeros(max(n_sets, 1), np.uint8)
@@ -202,9 +216,10 @@ class Device:
 
     def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
                                d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,
-                               d_set_status: Optional[int] = None) -> float:
+                               d_set_status: Optional[int] = None, d_pk_idx: Optional[int] = None) -> float:
         """All arguments are device pointers (ints).  Returns device_ms."""
-        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed)
+        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed,
+                          d_pk_idx)
         st = _Stats()
         rc = self.lib.lb_verify_requests_device(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
                                                 ctypes.byref(st))
@@ -213,9 +228,11 @@ class Device:
 
     def verify_requests_device_async(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int,
                                      d_pk_off: Optional[int], d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int,
-                                     d_valid: int, d_err: int, d_set_status: Optional[int] = None) -> int:
+                                     d_valid: int, d_err: int, d_set_status: Optional[int] = None,
+                                     d_pk_idx: Optional[int] = None) -> int:
         """Enqueue; returns a ticket for wait().  All arguments are device pointers."""
-        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed)
+        b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed,
+                          d_pk_idx)
         t = ctypes.c_uint64(0)
         rc = self.lib.lb_verify_requests_device_async(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
                                                       ctypes.byref(t))
@@ -265,6 +282,49 @@ class Device:
                                               ctypes.byref(bad))
         self._check(rc, "lb_aggregate_signatures")
         return out.tobytes(), int(bad.value)
+
+    # -- device-resident pubkey table (index2pubkey mirror) -------------------------
+    def pubkey_table_append(self, pubkeys: Sequence[bytes]) -> int:
+        """syncPubkeys: append keys (all 48-byte compressed or all 96-byte uncompressed);
+        returns the new table size.  Raises BadPubkeyError(index) if one fails to decode."""
+        n = len(pubkeys)
+        if n == 0:
+            return self.pubkey_table_size()
+        pk_len = len(pubkeys[0])
+        if any(len(p) != pk_len for p in pubkeys):
+            raise ValueError("pubkey_table_append expects keys of one encoding length")
+        blob = _u8(b"".join(pubkeys))
+        bad = ctypes.c_int32(-1)
+        rc = self.lib.lb_pubkey_table_append(self._h, n, _ptr(blob), pk_len, ctypes.byref(bad))
+        if rc == LB_ERR_INVALID_ARGUMENT and bad.value >= 0:
+            raise BadPubkeyError(f"pubkey {bad.value} fails to decode")
+        self._check(rc, "lb_pubkey_table_append")
+        return self.pubkey_table_size()
+
+    def pubkey_table_size(self) -> int:
+        n = ctypes.c_uint32(0)
+        self._check(self.lib.lb_pubkey_table_size(self._h, ctypes.byref(n)), "lb_pubkey_table_size")
+        return int(n.value)
+
+    def pubkey_table_read(self, first: int, n: int) -> List[bytes]:
+        out = np.zeros(max(n, 1) * 96, np.uint8)
+        self._check(self.lib.lb_pubkey_table_read(self._h, first, n, _ptr(out)), "lb_pubkey_table_read")
+        return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
+
+    def pubkey_table_truncate(self, n: int) -> None:
+        self._check(self.lib.lb_pubkey_table_truncate(self._h, n), "lb_pubkey_table_truncate")
+
+    def aggregate_pubkeys_indexed(self, indices: Sequence[int]) -> bytes:
+        if len(indices) == 0:
+            raise EmptyAggregateError("EMPTY_AGGREGATE_ARRAY")
+        idx = np.ascontiguousarray(indices, dtype=np.uint32)
+        out = np.zeros(96, np.uint8)
+        st = np.zeros(1, np.uint8)
+        rc = self.lib.lb_aggregate_pubkeys_indexed(self._h, len(idx), _ptr(idx), _ptr(out), _ptr(st))
+        self._check(rc, "lb_aggregate_pubkeys_indexed")
+        if st[0] != 0:
+            raise BadPubkeyError(SET_STATUS_NAMES.get(int(st[0]), str(st[0])))
+        return out.tobytes()
 
     # -- stage-level entry points (parity tests) ---------------------------------
     def hash_to_g2(self, messages: Sequence[bytes]) -> List[bytes]:

@@ -53,12 +53,19 @@ class SignatureSetType(str, enum.Enum):
 
 @dataclass
 class PublicKey:
-    """A validated G1 public key as its 96-byte uncompressed encoding (what
-    jobItemWorkReq ships to the worker, jobItem.ts:59 / index.ts:144)."""
-    uncompressed: bytes
+    """A G1 public key: its 96-byte uncompressed encoding (what jobItemWorkReq
+    ships to the worker, jobItem.ts:59 / index.ts:144) and/or its validator
+    index in the device-resident pubkey table (the index2pubkey mirror,
+    state-transition/src/cache/pubkeyCache.ts:56-77; see sync_pubkeys).  A
+    package whose keys all carry an index ships 4-byte indices instead of
+    points and is aggregated on the GPU from the table."""
+    uncompressed: bytes = b""
+    index: Optional[int] = None
 
     def __post_init__(self):
-        if len(self.uncompressed) != 96:
+        if self.index is None and len(self.uncompressed) != 96:
+            raise ValueError("PublicKey expects the 96-byte uncompressed encoding or a validator index")
+        if self.uncompressed and len(self.uncompressed) != 96:
             raise ValueError("PublicKey expects the 96-byte uncompressed encoding")
 
 
@@ -133,29 +140,51 @@ class DeviceBackend:
         self.seed_source = seed_source
         self.lock = threading.Lock()
 
+    def sync_pubkeys(self, pubkeys: Sequence[bytes]) -> int:
+        """syncPubkeys (pubkeyCache.ts:56-77): append validators' keys (48-byte
+        compressed, as the state holds them) to the device table; returns its size."""
+        with self.lock:
+            return self.dev.pubkey_table_append(list(pubkeys))
+
     def verify_requests(self, requests: List[List[SignatureSet]]) -> Tuple[List[bool], List[int]]:
-        pks, pk_off, msgs, sigs, req_off = [], [0], [], [], [0]
+        keys_all, pk_off, msgs, sigs, req_off = [], [0], [], [], [0]
         for req in requests:
             for s in req:
                 keys = [s.pubkey] if s.type == SignatureSetType.single else (s.pubkeys or [])
-                pks.extend(k.uncompressed for k in keys)
-                pk_off.append(len(pks))
+                keys_all.extend(keys)
+                pk_off.append(len(keys_all))
                 msgs.append(bytes(s.signing_root))
                 sigs.append(bytes(s.signature))
             req_off.append(len(msgs))
         blob, offs = pack_blobs(sigs)
+        # validator indices when every key has one (device table), else the encodings
+        by_index = bool(keys_all) and all(k.index is not None for k in keys_all)
+        idx = np.array([k.index for k in keys_all], np.uint32) if by_index else None
         with self.lock:
-            res = self.dev.verify_requests(np.array(req_off, np.uint32),
-                                           np.frombuffer(b"".join(pks) or b"\0", np.uint8),
-                                           np.array(pk_off, np.uint32),
+            pks = None if by_index else np.frombuffer(b"".join(self._key_bytes(keys_all)) or b"\0", np.uint8)
+            res = self.dev.verify_requests(np.array(req_off, np.uint32), pks, np.array(pk_off, np.uint32),
                                            np.frombuffer(b"".join(msgs) or b"\0", np.uint8), blob, offs,
-                                           self.seed_source())
+                                           self.seed_source(), pk_indices=idx)
         return [bool(v) for v in res.valid], [int(e) for e in res.errors]
+
+    def _key_bytes(self, keys: Sequence[PublicKey]) -> List[bytes]:
+        """96-byte encodings; index-only keys are read back from the device table
+        (mixed packages only).  An index outside the table -> an all-zero
+        encoding, which decodes as a bad pubkey (LB_REQ_BAD_PUBKEY)."""
+        size = None
+        out = []
+        for k in keys:
+            if k.uncompressed:
+                out.append(k.uncompressed)
+                continue
+            size = self.dev.pubkey_table_size() if size is None else size
+            out.append(self.dev.pubkey_table_read(k.index, 1)[0] if 0 <= k.index < size else bytes(96))
+        return out
 
     def verify_same_message(self, pubkeys: Sequence[PublicKey], signatures: Sequence[bytes],
                             message: bytes) -> List[bool]:
         with self.lock:
-            out, _ = self.dev.verify_same_message([p.uncompressed for p in pubkeys], list(signatures), message,
+            out, _ = self.dev.verify_same_message(self._key_bytes(pubkeys), list(signatures), message,
                                                   self.seed_source())
         return out
 
@@ -185,6 +214,14 @@ class BlsGpuVerifier:
         self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "prioritized_sig_sets": 0,
                         "jobs_started": 0, "dispatches": 0, "same_message_retry_jobs": 0,
                         "same_message_retry_sets": 0, "aggregated_pubkeys": 0}
+
+    def sync_pubkeys(self, pubkeys: Sequence[bytes]) -> int:
+        """Append validators' pubkeys to every GPU's device table (index2pubkey
+        mirror, pubkeyCache.ts:56-77); sets may then carry PublicKey(index=i)."""
+        sizes = [b.sync_pubkeys(pubkeys) for b in self.backends]
+        if len(set(sizes)) != 1:
+            raise RuntimeError(f"pubkey tables out of sync across devices: {sizes}")
+        return sizes[0]
 
     # ---- IBlsVerifier --------------------------------------------------------------
     def can_accept_work(self) -> bool:

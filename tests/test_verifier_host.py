@@ -197,3 +197,50 @@ def test_multiple_backends_share_load():
         assert all(len(b.dispatches) > 0 for b in bs)
         await v.close()
     run(main())
+
+
+# ---- index-addressed keys (device pubkey table) ------------------
+def test_public_key_index_or_bytes():
+    from lodestar_amd.verifier import PublicKey
+    assert PublicKey(index=3).index == 3
+    with pytest.raises(ValueError):
+        PublicKey()
+    with pytest.raises(ValueError):
+        PublicKey(b"\0" * 95, index=1)
+
+
+def test_device_backend_ships_indices_when_every_key_has_one():
+    import threading
+
+    import numpy as np
+
+    from lodestar_amd.native import VerifyResult
+    from lodestar_amd.verifier import DeviceBackend, PublicKey, aggregate_set, single_set
+
+    class FakeDev:
+        def __init__(self):
+            self.calls = []
+
+        def verify_requests(self, req_off, pks, pk_off, msgs, blob, offs, seed, pk_indices=None):
+            self.calls.append((pks, None if pk_indices is None else list(pk_indices), list(pk_off)))
+            n = len(req_off) - 1
+            return VerifyResult(np.ones(n, np.uint8), np.zeros(n, np.uint8), np.zeros(0, np.uint8), 0.0)
+
+        def pubkey_table_size(self):
+            return 10
+
+        def pubkey_table_read(self, first, n):
+            return [bytes([first]) * 96]
+
+    b = object.__new__(DeviceBackend)
+    b.dev, b.seed_source, b.lock = FakeDev(), (lambda: bytes(32)), threading.Lock()
+    s1 = single_set(PublicKey(index=4), bytes(32), bytes(96))
+    s2 = aggregate_set([PublicKey(index=1), PublicKey(index=2)], bytes(32), bytes(96))
+    b.verify_requests([[s1, s2]])
+    pks, idx, pk_off = b.dev.calls[-1]
+    assert pks is None and idx == [4, 1, 2] and pk_off == [0, 1, 3]
+    # mixed: index-only keys are materialised from the table, bytes shipped
+    s3 = single_set(PublicKey(bytes([7]) * 96), bytes(32), bytes(96))
+    b.verify_requests([[s1, s3]])
+    pks, idx, _ = b.dev.calls[-1]
+    assert idx is None and pks.tobytes() == bytes([4]) * 96 + bytes([7]) * 96
