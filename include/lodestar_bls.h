@@ -204,6 +204,21 @@ int lb_pubkey_table_truncate(lb_ctx* ctx, uint32_t n);
 int lb_aggregate_pubkeys_indexed(lb_ctx* ctx, uint32_t n, const uint32_t* indices, uint8_t* out96,
                                  uint8_t* out_status);
 
+/* ---- signing roots (the step before the verifier) --------
+ * computeSigningRoot(type, obj, domain) = hash_tree_root(SigningData{hash_tree_root(obj), domain})
+ * (state-transition/src/util/signingRoot.ts:7-13), SSZ merkleization on the GPU.
+ * domains: n x 32 bytes (domain_stride 32) or one shared domain (domain_stride 0).
+ *
+ * Attestations: data = n x 128-byte SSZ phase0.AttestationData (slot, index,
+ * beacon_block_root, source, target) -> n x 32-byte signing roots, as
+ * getAttestationDataSigningRoot (signatureSets/indexedAttestation.ts:10-19). */
+int lb_signing_roots_attestation(lb_ctx* ctx, uint32_t n, const uint8_t* data128, const uint8_t* domains,
+                                 uint32_t domain_stride, uint8_t* out32);
+/* Any container given as its m (1..16) field roots per object (n x m x 32 bytes;
+ * basic fields packed little-endian into a zero-padded chunk): merkleize, then SigningData. */
+int lb_signing_roots_chunks(lb_ctx* ctx, uint32_t n, uint32_t m, const uint8_t* chunks, const uint8_t* domains,
+                            uint32_t domain_stride, uint8_t* out32);
+
 /* ---- stage-level entry points (parity tests against the CPU oracle) ----- */
 /* hash_to_G2(msg_i) -> 192-byte uncompressed affine encoding each */
 int lb_hash_to_g2(lb_ctx* ctx, uint32_t n, const uint8_t* messages, uint8_t* out192);

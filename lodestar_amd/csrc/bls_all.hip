@@ -9,4 +9,5 @@
 #include "k_pairing.hip"
 #include "k_aux.hip"
 #include "k_tail.hip"
+#include "k_ssz.hip"
 #include "bls_host.hip"

@@ -848,6 +848,41 @@ int lb_aggregate_pubkeys_indexed(lb_ctx* ctx, uint32_t n, const uint32_t* indice
   return LB_OK;
 }
 
+// ---- signing roots -----------------------------------------------------------
+static int signing_roots(lb_ctx* ctx, uint32_t n, uint32_t m, const uint8_t* in, size_t in_per_obj,
+                         const uint8_t* domains, uint32_t dstride, uint8_t* out32) {
+  if (!ctx || (n && (!in || !domains || !out32)) || (dstride != 0 && dstride != 32)) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  const size_t n_dom = dstride ? n : 1;
+  LB_TRY(ensure_ws(ctx, (size_t)n * (in_per_obj + 32) + n_dom * 32 + 8192));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  void *d_in, *d_dom;
+  LB_TRY(upload(ctx, ws, in, (size_t)n * in_per_obj, &d_in));
+  LB_TRY(upload(ctx, ws, domains, n_dom * 32, &d_dom));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 32);
+  if (m == 0)
+    LB_LAUNCH(k_signing_root_att, blocks_for(n), TPB, n, (const uint8_t*)d_in, (const uint8_t*)d_dom, dstride, d_out);
+  else
+    LB_LAUNCH(k_signing_root_chunks, blocks_for(n), TPB, n, m, (const uint8_t*)d_in, (const uint8_t*)d_dom, dstride,
+              d_out);
+  LB_HIP(hipMemcpyAsync(out32, d_out, (size_t)n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+int lb_signing_roots_attestation(lb_ctx* ctx, uint32_t n, const uint8_t* data128, const uint8_t* domains,
+                                 uint32_t domain_stride, uint8_t* out32) {
+  return signing_roots(ctx, n, 0, data128, 128, domains, domain_stride, out32);
+}
+
+int lb_signing_roots_chunks(lb_ctx* ctx, uint32_t n, uint32_t m, const uint8_t* chunks, const uint8_t* domains,
+                            uint32_t domain_stride, uint8_t* out32) {
+  if (m < 1 || m > 16) return LB_ERR_INVALID_ARGUMENT;
+  return signing_roots(ctx, n, m, chunks, (size_t)m * 32, domains, domain_stride, out32);
+}
+
 int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const uint32_t* sig_off, uint8_t* out192,
                             int32_t* out_bad_index) {
   if (!ctx || !out192 || !out_bad_index || (n && (!sigs || !sig_off))) return LB_ERR_INVALID_ARGUMENT;

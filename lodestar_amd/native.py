@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
     "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
-    "lb_aggregate_pubkeys_indexed",
+    "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
 )
 
 
@@ -118,6 +118,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_pubkey_table_read.argtypes = [vp, u32, u32, vp]
     lib.lb_pubkey_table_truncate.argtypes = [vp, u32]
     lib.lb_aggregate_pubkeys_indexed.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_signing_roots_attestation.argtypes = [vp, u32, vp, vp, u32, vp]
+    lib.lb_signing_roots_chunks.argtypes = [vp, u32, u32, vp, vp, u32, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
     for name in EXPORTED_SYMBOLS:
@@ -325,6 +327,37 @@ class Device:
         if st[0] != 0:
             raise BadPubkeyError(SET_STATUS_NAMES.get(int(st[0]), str(st[0])))
         return out.tobytes()
+
+    # -- signing roots (computeSigningRoot, state-transition/src/util/signingRoot.ts:7-13) --
+    def signing_roots_attestation(self, data128: Sequence[bytes], domains) -> List[bytes]:
+        """n SSZ AttestationData (128 B each); domains: one 32-byte domain or a list of n."""
+        n = len(data128)
+        if n == 0:
+            return []
+        shared = isinstance(domains, (bytes, bytearray))
+        dom = _u8(bytes(domains) if shared else b"".join(domains))
+        d = _u8(b"".join(data128))
+        assert len(d) == 128 * n and len(dom) == (32 if shared else 32 * n)
+        out = np.zeros(32 * n, np.uint8)
+        self._check(self.lib.lb_signing_roots_attestation(self._h, n, _ptr(d), _ptr(dom), 0 if shared else 32,
+                                                          _ptr(out)), "lb_signing_roots_attestation")
+        return [out[32 * i:32 * (i + 1)].tobytes() for i in range(n)]
+
+    def signing_roots_chunks(self, field_roots: Sequence[Sequence[bytes]], domains) -> List[bytes]:
+        """n objects given as m field roots (32 B each, same m for all)."""
+        n = len(field_roots)
+        if n == 0:
+            return []
+        m = len(field_roots[0])
+        assert all(len(f) == m for f in field_roots)
+        shared = isinstance(domains, (bytes, bytearray))
+        dom = _u8(bytes(domains) if shared else b"".join(domains))
+        c = _u8(b"".join(b"".join(f) for f in field_roots))
+        assert len(c) == 32 * m * n
+        out = np.zeros(32 * n, np.uint8)
+        self._check(self.lib.lb_signing_roots_chunks(self._h, n, m, _ptr(c), _ptr(dom), 0 if shared else 32,
+                                                     _ptr(out)), "lb_signing_roots_chunks")
+        return [out[32 * i:32 * (i + 1)].tobytes() for i in range(n)]
 
     # -- stage-level entry points (parity tests) ---------------------------------
     def hash_to_g2(self, messages: Sequence[bytes]) -> List[bytes]:
