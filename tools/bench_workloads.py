@@ -174,7 +174,18 @@ def main():
     ok = all(bool(v.cpu().numpy().all()) and not bool(e.cpu().numpy().any()) for v, e in outs)
     res["device_indexed_inflight"] = {"sets_per_s": round(n * steps / el, 1), "ms_per_call": round(el / steps * 1e3, 3),
                                       "all_valid": ok}
-    out = {"workloads": "C3 + C4 shard (1/8 of 1M mixed sets)", "validators_in_table": nv,
+    # signing roots of the shard's attestations (the step before the verifier)
+    att = [rng.bytes(128) for _ in range(n)]
+    dom = rng.bytes(32)
+    dev.signing_roots_attestation(att, dom)
+    ts = []
+    for _ in range(a.reps):
+        t1 = time.perf_counter()
+        dev.signing_roots_attestation(att, dom)
+        ts.append(time.perf_counter() - t1)
+    ssz = {"attestation_signing_roots": n, "host_call_ms_p50": round(float(np.median(ts)) * 1e3, 3),
+           "roots_per_s": round(n / float(np.median(ts)), 1)}
+    out = {"workloads": "C3 + C4 shard (1/8 of 1M mixed sets)", "validators_in_table": nv, "ssz": ssz,
            "c3": c3,
            "c4_shard": {"sets": n, "requests": nr, "pubkeys": int(len(idx)), "singles": a.singles,
                         "aggregate_and_proofs": a.aggregates, "committee": a.committee, **res},
