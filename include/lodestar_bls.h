@@ -119,8 +119,9 @@ typedef struct {
 } lb_request_batch;
 
 typedef struct {
-  uint32_t batch_retries;      /* merged batchable groups that had to be retried (worker.ts:80) */
-  uint32_t batch_sigs_success; /* sets verified successfully inside merged groups (worker.ts:71) */
+  uint32_t batch_retries;      /* merged checks that failed, so requests were re-verified alone
+                                  (worker.ts:80; 0 or 1 per call, 0 below LB_MERGE_MIN requests) */
+  uint32_t batch_sigs_success; /* sets verified inside a passing merged check (worker.ts:71)   */
   double device_ms;            /* wall time of the device pipeline for this call              */
 } lb_verify_stats;
 

@@ -60,6 +60,7 @@ struct Slot {
   hipEvent_t wall0 = nullptr, wall1 = nullptr;
   bool busy = false;
   uint64_t ticket = 0;
+  uint32_t* h_stats = nullptr;  // pinned: [batch_retries, batch_sigs_success] of the call in flight
 };
 
 struct lb_ctx {
@@ -100,6 +101,7 @@ struct lb_ctx {
   const char* stage_name[Slot::kMaxStages] = {};
   unsigned long long stage_ops[Slot::kMaxStages] = {};
   float wall_ms = 0.f;
+  uint32_t batch_retries = 0, batch_sigs_success = 0;
 };
 
 namespace {
@@ -250,6 +252,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2a* d_Sall = ws.take<g2a>(1);
   fp12* d_Fall = ws.take<fp12>(1);
   uint8_t* d_mflag = ws.take<uint8_t>(2);  // [0] merged check passed, [1] constant 0 (req_bad of the merged pair)
+  uint32_t* d_mstats = ws.take<uint32_t>(2);
+  sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
@@ -324,6 +328,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_mflag);
     LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
              (const uint8_t*)d_bad, d_valid, (const uint8_t*)d_mflag);
+    hipLaunchKernelGGL(k_merge_stats, dim3(1), dim3(TPB), 0, sl.st[0], n_req, d_req_off, (const uint8_t*)d_bad,
+                       (const uint8_t*)d_mflag, d_mstats);
+    LB_HIP(hipGetLastError());
+    LB_HIP(hipMemcpyAsync(sl.h_stats, d_mstats, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st[0]));
   } else if (tail_wave)
     LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
              (const uint8_t*)d_bad, d_valid, (const uint8_t*)nullptr);
@@ -362,6 +370,8 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
     ctx->stage_ops[i] = sl.stage_ops[i];
   }
   LB_HIP(hipEventElapsedTime(&ctx->wall_ms, sl.wall0, sl.wall1));
+  ctx->batch_retries = sl.h_stats[0];
+  ctx->batch_sigs_success = sl.h_stats[1];
   sl.busy = false;
   return LB_OK;
 }
@@ -430,7 +440,9 @@ int lb_create(int device, lb_ctx** out_ctx) {
     for (int i = 0; ok && i < Slot::kMaxStages; i++)
       ok = hipEventCreate(&sl.ev0[i]) == hipSuccess && hipEventCreate(&sl.ev1[i]) == hipSuccess;
     ok = ok && hipEventCreate(&sl.wall0) == hipSuccess && hipEventCreate(&sl.wall1) == hipSuccess &&
-         hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc(&sl.h_stats, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+    if (ok) sl.h_stats[0] = sl.h_stats[1] = 0;
   }
   ctx->stream = ctx->slots[0].st[0];
   if (!ok) {
@@ -459,6 +471,7 @@ int lb_destroy(lb_ctx* ctx) {
     if (sl.wall0) (void)hipEventDestroy(sl.wall0);
     if (sl.wall1) (void)hipEventDestroy(sl.wall1);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.h_stats) (void)hipHostFree(sl.h_stats);
     for (int i = 0; i < ctx->streams_per_slot[s]; i++)
       if (sl.st[i]) (void)hipStreamDestroy(sl.st[i]);
   }
@@ -523,8 +536,8 @@ int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
     if (sl.busy && sl.ticket == ticket) LB_TRY(finish_slot(ctx, sl));
   }
   if (stats) {
-    stats->batch_retries = 0;
-    stats->batch_sigs_success = 0;
+    stats->batch_retries = ctx->batch_retries;
+    stats->batch_sigs_success = ctx->batch_sigs_success;
     stats->device_ms = ctx->wall_ms;
   }
   return LB_OK;
@@ -642,8 +655,8 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   memcpy(out_req_err, h_out + al(nr), nr);
   if (out_set_status && ns) memcpy(out_set_status, h_out + 2 * al(nr), ns);
   if (stats) {
-    stats->batch_retries = 0;
-    stats->batch_sigs_success = 0;
+    stats->batch_retries = ctx->batch_retries;
+    stats->batch_sigs_success = ctx->batch_sigs_success;
     stats->device_ms = ctx->wall_ms;
   }
   return LB_OK;

@@ -153,6 +153,9 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,
                                                         g2a* __restrict__ S_all, fp12* __restrict__ F_all);
+__global__ void __launch_bounds__(TPB) k_merge_stats(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                     const uint8_t* __restrict__ req_bad,
+                                                     const uint8_t* __restrict__ mflag, uint32_t* __restrict__ out);
 __global__ void __launch_bounds__(TPB) k_signing_root_att(uint32_t n, const uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ domains, uint32_t dstride,
                                                           uint8_t* __restrict__ out);

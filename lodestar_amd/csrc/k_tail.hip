@@ -65,6 +65,27 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t
 // S_all = sum S_k and F_all = prod F_k over the requests not already false.
 // One wave; the tail kernel then verifies (F_all, S_all) once, and the
 // per-request tails only run if that merged check fails.
+// The worker's bookkeeping of its merged batch (worker.ts:66-85): batchRetries
+// (1 when the merged check failed and requests were re-verified alone) and
+// batchSigsSuccess (sets verified inside a passing merged check).
+__global__ void __launch_bounds__(TPB) k_merge_stats(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                     const uint8_t* __restrict__ req_bad,
+                                                     const uint8_t* __restrict__ mflag, uint32_t* __restrict__ out) {
+  __shared__ uint32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  for (uint32_t k = threadIdx.x; k < n_req; k += TPB)
+    if (!req_bad[k]) c += req_off[k + 1] - req_off[k];
+  atomicAdd(&cnt, c);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool passed = mflag[0] != 0;
+    out[0] = passed ? 0u : 1u;
+    out[1] = passed ? cnt : 0u;
+  }
+}
+
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,

@@ -155,6 +155,8 @@ class VerifyResult:
     errors: np.ndarray         # uint8 per request (LB_REQ_*)
     set_status: np.ndarray     # uint8 per set (LB_SET_*)
     device_ms: float
+    batch_retries: int = 0     # worker.ts:80 (merged check failed -> per-request re-verification)
+    batch_sigs_success: int = 0  # worker.ts:71 (sets verified inside a passing merged check)
 
 
 class Device:
@@ -214,7 +216,8 @@ class Device:
         st = _Stats()
         rc = self.lib.lb_verify_requests(self._h, ctypes.byref(b), _ptr(valid), _ptr(err), _ptr(sst), ctypes.byref(st))
         self._check(rc, "lb_verify_requests")
-        return VerifyResult(valid[:n_req], err[:n_req], sst[:n_sets], st.device_ms)
+        return VerifyResult(valid[:n_req], err[:n_req], sst[:n_sets], st.device_ms, int(st.batch_retries),
+                            int(st.batch_sigs_success))
 
     def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
                                d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,
@@ -244,6 +247,7 @@ class Device:
     def wait(self, ticket: int) -> float:
         st = _Stats()
         self._check(self.lib.lb_wait(self._h, ticket, ctypes.byref(st)), "lb_wait")
+        self.last_stats = (int(st.batch_retries), int(st.batch_sigs_success))
         return st.device_ms
 
     def verify_same_message(self, pubkeys: Sequence[bytes], signatures: Sequence[bytes], message: bytes,

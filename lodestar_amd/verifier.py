@@ -37,6 +37,7 @@ from typing import Callable, Deque, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
+from . import metrics as M
 from .native import (LB_REQ_BAD_PUBKEY, LB_REQ_EMPTY_AGGREGATE, BadPubkeyError, Device, EmptyAggregateError,
                      pack_blobs)
 
@@ -165,6 +166,7 @@ class DeviceBackend:
             res = self.dev.verify_requests(np.array(req_off, np.uint32), pks, np.array(pk_off, np.uint32),
                                            np.frombuffer(b"".join(msgs) or b"\0", np.uint8), blob, offs,
                                            self.seed_source(), pk_indices=idx)
+        self.last_stats = (res.batch_retries, res.batch_sigs_success)
         return [bool(v) for v in res.valid], [int(e) for e in res.errors]
 
     def _key_bytes(self, keys: Sequence[PublicKey]) -> List[bytes]:
@@ -214,6 +216,8 @@ class BlsGpuVerifier:
         self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "prioritized_sig_sets": 0,
                         "jobs_started": 0, "dispatches": 0, "same_message_retry_jobs": 0,
                         "same_message_retry_sets": 0, "aggregated_pubkeys": 0}
+        # the reference's metric names (lodestar.ts:380-495), see lodestar_amd/metrics.py
+        self.pool_metrics = M.BlsPoolMetrics()
 
     def sync_pubkeys(self, pubkeys: Sequence[bytes]) -> int:
         """Append validators' pubkeys to every GPU's device table (index2pubkey
@@ -230,16 +234,25 @@ class BlsGpuVerifier:
     async def verify_signature_sets(self, sets: List[SignatureSet],
                                     opts: Optional[VerifySignatureOpts] = None) -> bool:
         opts = opts or VerifySignatureOpts()
-        self.metrics["aggregated_pubkeys"] += sum(len(s.pubkeys or []) for s in sets
-                                                  if s.type == SignatureSetType.aggregate)
+        pm = self.pool_metrics
+        n_agg = sum(len(s.pubkeys or []) for s in sets if s.type == SignatureSetType.aggregate)
+        self.metrics["aggregated_pubkeys"] += n_agg
+        pm.inc(M.AGGREGATED_PUBKEYS, n_agg)
         self.metrics["total_sig_sets"] += len(sets)
+        pm.inc(M.TOTAL_SIG_SETS, len(sets))
         if opts.priority:
             self.metrics["prioritized_sig_sets"] += len(sets)
+            pm.inc(M.PRIORITIZED_SIG_SETS, len(sets))
         if opts.batchable:
             self.metrics["batchable_sig_sets"] += len(sets)
+            pm.inc(M.BATCHABLE_SIG_SETS, len(sets))
         if opts.verify_on_main_thread and not self.verify_all_multi_thread:
             # synchronous, on the caller's thread (index.ts:174-187)
-            return self._verify_now(sets)
+            t0 = time.monotonic()
+            try:
+                return self._verify_now(sets)
+            finally:
+                pm.observe(M.MAIN_THREAD_TIME, time.monotonic() - t0)
         loop = self._get_loop()
         futs = []
         for chunk in chunkify_maximize_chunk_size(sets, MAX_SIGNATURE_SETS_PER_JOB):
@@ -334,6 +347,15 @@ class BlsGpuVerifier:
         bi = self._idle.pop()
         self.metrics["dispatches"] += 1
         self.metrics["jobs_started"] += len(jobs)
+        pm, now = self.pool_metrics, time.monotonic()
+        pm.inc(M.JOB_GROUPS_STARTED)  # index.ts:433-437
+        for t in (JobType.default, JobType.same_message):
+            pm.inc(M.JOBS_STARTED, sum(1 for j in jobs if j.type == t), type=t.value)
+            pm.inc(M.SIG_SETS_STARTED, sum(len(j.sets) for j in jobs if j.type == t), type=t.value)
+        for j in jobs:
+            pm.observe(M.JOB_WAIT_TIME, now - j.added)  # index.ts:396
+        pm.set(M.WORKERS_BUSY, len(self.backends) - len(self._idle))
+        pm.set(M.QUEUE_LENGTH, len(self._jobs))
         loop = self._get_loop()
         task = loop.run_in_executor(None, self._execute, bi, jobs)
         task.add_done_callback(lambda f, bi=bi, jobs=jobs: self._on_done(f, bi, jobs))
@@ -341,6 +363,7 @@ class BlsGpuVerifier:
     def _execute(self, bi: int, jobs: List[_Job]):
         """Runs on an executor thread (the event loop never blocks on the GPU)."""
         backend = self.backends[bi]
+        t0 = time.monotonic()
         out = [None] * len(jobs)
         default_idx = [i for i, j in enumerate(jobs) if j.type == JobType.default]
         if default_idx:
@@ -351,24 +374,38 @@ class BlsGpuVerifier:
             if j.type == JobType.same_message:
                 out[i] = ("same", backend.verify_same_message([p for p, _ in j.sets], [s for _, s in j.sets],
                                                               j.message))
-        return out
+        stats = getattr(backend, "last_stats", (0, 0)) if default_idx else (0, 0)
+        return out, time.monotonic() - t0, stats
 
     def _on_done(self, fut, bi: int, jobs: List[_Job]) -> None:
         self._idle.append(bi)
+        pm = self.pool_metrics
+        pm.set(M.WORKERS_BUSY, len(self.backends) - len(self._idle))
         try:
-            results = fut.result()
+            results, elapsed, (retries, sigs_ok) = fut.result()
         except Exception as e:  # device failure rejects every job of the package (index.ts:503-512)
             for job in jobs:
                 if not job.future.done():
                     job.future.set_exception(e)
             self._get_loop().call_soon(self._run_job)
             return
+        # index.ts:495-502 (workerId = the GPU backend)
+        started = sum(len(j.sets) for j in jobs)
+        pm.inc(M.JOBS_WORKER_TIME, elapsed, workerId=bi)
+        if started:
+            pm.observe(M.TIME_PER_SIG_SET, elapsed / started)
+        pm.inc(M.SUCCESS_JOBS_SETS, sum(j.sig_sets() for j, (k, _) in zip(jobs, results) if k != "err"))
+        pm.inc(M.ERROR_JOBS_SETS, sum(j.sig_sets() for j, (k, _) in zip(jobs, results) if k == "err"))
+        pm.inc(M.BATCH_RETRIES, retries)
+        pm.inc(M.BATCH_SIGS_SUCCESS, sigs_ok)
         for job, (kind, val) in zip(jobs, results):
             if job.future.done():
                 continue
             if kind == "ok":
                 job.future.set_result(bool(val))
             elif kind == "err":
+                if val == LB_REQ_EMPTY_AGGREGATE:  # index.ts:403-409
+                    pm.inc(M.ERROR_AGGREGATE_SETS, len(job.sets), type=job.type.value)
                 err = EmptyAggregateError("EMPTY_AGGREGATE_ARRAY") if val == LB_REQ_EMPTY_AGGREGATE else \
                     BadPubkeyError("invalid pubkey encoding") if val == LB_REQ_BAD_PUBKEY else RuntimeError(str(val))
                 job.future.set_exception(err)
@@ -377,6 +414,8 @@ class BlsGpuVerifier:
                 if not all(verdicts):
                     self.metrics["same_message_retry_jobs"] += 1
                     self.metrics["same_message_retry_sets"] += len(job.sets)
+                    pm.inc(M.SAME_MESSAGE_RETRY_JOBS)  # index.ts:566-567
+                    pm.inc(M.SAME_MESSAGE_RETRY_SETS, len(job.sets))
                 job.future.set_result(verdicts)
         self._get_loop().call_soon(self._run_job)
 

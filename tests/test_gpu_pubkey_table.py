@@ -160,6 +160,13 @@ def test_verify_by_index_merged_call_with_invalid(tdev, n_req):
     req_off, idx, pk_off, msgs, blob, offs = _pack(reqs)
     res = tdev.verify_requests(req_off, None, pk_off, msgs, blob, offs, bytes(32), pk_indices=idx)
     assert [bool(v) for v in res.valid] == [k != 37 for k in range(n_req)]
+    assert (res.batch_retries, res.batch_sigs_success) == (1, 0)  # worker.ts:80 merged batch retried
+    # all valid: the merged check passes and covers every set (worker.ts:71)
+    reqs[37][3] = (ix, m, s)
+    req_off, idx, pk_off, msgs, blob, offs = _pack(reqs)
+    res = tdev.verify_requests(req_off, None, pk_off, msgs, blob, offs, bytes(32), pk_indices=idx)
+    assert res.valid.all()
+    assert (res.batch_retries, res.batch_sigs_success) == (0, int(req_off[-1]))
 
 
 def test_bls_gpu_verifier_index_keys():

@@ -244,3 +244,34 @@ def test_device_backend_ships_indices_when_every_key_has_one():
     b.verify_requests([[s1, s3]])
     pks, idx, _ = b.dev.calls[-1]
     assert idx is None and pks.tobytes() == bytes([4]) * 96 + bytes([7]) * 96
+
+
+# ---- metrics parity (lodestar.ts:380-495 names, index.ts update sites) -------------
+def test_pool_metrics_reference_names():
+    from lodestar_amd import metrics as M
+
+    async def main():
+        b = MockBackend()
+        b.last_stats = (1, 0)
+        v = BlsGpuVerifier(backends=[b])
+        assert await v.verify_signature_sets(sets(300), VerifySignatureOpts(batchable=True, priority=True)) is True
+        with pytest.raises(EmptyAggregateError):
+            await v.verify_signature_sets([aggregate_set([], bytes(32), GOOD)])
+        out = await v.verify_signature_sets_same_message([(PK, GOOD), (PK, BAD)], bytes(32))
+        assert out == [True, False]
+        pm = v.pool_metrics
+        assert pm.get(M.TOTAL_SIG_SETS) == 301
+        assert pm.get(M.BATCHABLE_SIG_SETS) == 300 and pm.get(M.PRIORITIZED_SIG_SETS) == 300
+        assert pm.get(M.SIG_SETS_STARTED, type="default") == 301
+        assert pm.get(M.SIG_SETS_STARTED, type="same_message") == 2
+        assert pm.get(M.JOBS_STARTED, type="default") == 3
+        assert pm.get(M.ERROR_AGGREGATE_SETS, type="default") == 1
+        assert pm.get(M.ERROR_JOBS_SETS) == 1 and pm.get(M.SUCCESS_JOBS_SETS) == 301
+        assert pm.get(M.SAME_MESSAGE_RETRY_JOBS) == 1 and pm.get(M.SAME_MESSAGE_RETRY_SETS) == 2
+        assert pm.get(M.BATCH_RETRIES) >= 1
+        assert pm.histogram(M.JOB_WAIT_TIME)[0] == 4
+        names = set(pm.collect())
+        assert "lodestar_bls_thread_pool_sig_sets_total" in names
+        assert 'lodestar_bls_thread_pool_jobs_started_total{type="default"}' in names
+        await v.close()
+    run(main())
