@@ -215,6 +215,11 @@ int lb_aggregate_pubkeys_indexed(lb_ctx* ctx, uint32_t n, const uint32_t* indice
  * getAttestationDataSigningRoot (signatureSets/indexedAttestation.ts:10-19). */
 int lb_signing_roots_attestation(lb_ctx* ctx, uint32_t n, const uint8_t* data128, const uint8_t* domains,
                                  uint32_t domain_stride, uint8_t* out32);
+/* Device-resident variant: data128, domains and out32 are device pointers (e.g.
+ * out32 = the `messages` buffer of a following lb_verify_requests_device call,
+ * so signing roots never leave HBM).  Synchronises before returning. */
+int lb_signing_roots_attestation_device(lb_ctx* ctx, uint32_t n, const uint8_t* d_data128, const uint8_t* d_domains,
+                                        uint32_t domain_stride, uint8_t* d_out32);
 /* Any container given as its m (1..16) field roots per object (n x m x 32 bytes;
  * basic fields packed little-endian into a zero-padded chunk): merkleize, then SigningData. */
 int lb_signing_roots_chunks(lb_ctx* ctx, uint32_t n, uint32_t m, const uint8_t* chunks, const uint8_t* domains,

@@ -890,6 +890,18 @@ int lb_signing_roots_attestation(lb_ctx* ctx, uint32_t n, const uint8_t* data128
   return signing_roots(ctx, n, 0, data128, 128, domains, domain_stride, out32);
 }
 
+int lb_signing_roots_attestation_device(lb_ctx* ctx, uint32_t n, const uint8_t* d_data, const uint8_t* d_domains,
+                                        uint32_t dstride, uint8_t* d_out) {
+  if (!ctx || (n && (!d_data || !d_domains || !d_out)) || (dstride != 0 && dstride != 32))
+    return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  LB_LAUNCH(k_signing_root_att, blocks_for(n), TPB, n, d_data, d_domains, dstride, d_out);
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
 int lb_signing_roots_chunks(lb_ctx* ctx, uint32_t n, uint32_t m, const uint8_t* chunks, const uint8_t* domains,
                             uint32_t domain_stride, uint8_t* out32) {
   if (m < 1 || m > 16) return LB_ERR_INVALID_ARGUMENT;

@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
     "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
+    "lb_signing_roots_attestation_device",
 )
 
 
@@ -120,6 +121,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_aggregate_pubkeys_indexed.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_signing_roots_attestation.argtypes = [vp, u32, vp, vp, u32, vp]
     lib.lb_signing_roots_chunks.argtypes = [vp, u32, u32, vp, vp, u32, vp]
+    lib.lb_signing_roots_attestation_device.argtypes = [vp, u32, vp, vp, u32, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
     for name in EXPORTED_SYMBOLS:
@@ -346,6 +348,12 @@ class Device:
         self._check(self.lib.lb_signing_roots_attestation(self._h, n, _ptr(d), _ptr(dom), 0 if shared else 32,
                                                           _ptr(out)), "lb_signing_roots_attestation")
         return [out[32 * i:32 * (i + 1)].tobytes() for i in range(n)]
+
+    def signing_roots_attestation_device(self, n: int, d_data: int, d_domains: int, domain_stride: int,
+                                         d_out: int) -> None:
+        """Device pointers in and out (roots straight into a verify call's messages buffer)."""
+        self._check(self.lib.lb_signing_roots_attestation_device(self._h, n, d_data, d_domains, domain_stride, d_out),
+                    "lb_signing_roots_attestation_device")
 
     def signing_roots_chunks(self, field_roots: Sequence[Sequence[bytes]], domains) -> List[bytes]:
         """n objects given as m field roots (32 B each, same m for all)."""

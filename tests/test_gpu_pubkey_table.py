@@ -196,3 +196,29 @@ def test_bls_gpu_verifier_index_keys():
         asyncio.run(main())
     finally:
         backend.close()
+
+
+def test_infinity_key_in_table_gives_false_not_error():
+    """fromBytes accepts the infinity encoding (no validation in syncPubkeys); a set
+    over it is false (BLST_PK_IS_INFINITY caught in maybeBatch), not a rejection."""
+    dev = Device(0)
+    try:
+        inf48 = bytes([0xC0]) + bytes(47)
+        keys = [bytes.fromhex(h) for h in KATS["interop_pubkeys"][:3]] + [inf48]
+        assert dev.pubkey_table_append(keys) == 4
+        assert dev.pubkey_table_read(3, 1)[0] == bytes([0x40]) + bytes(95)
+        msgs = [hashlib.sha256(bytes([i])).digest() for i in range(4)]
+        sigs = dev.sign([sk_be(i) for i in range(3)], msgs[:3]) + [bytes([0xC0]) + bytes(95)]
+        blob, offs = pack_blobs(sigs)
+        req_off = np.array([0, 3, 4, 5], np.uint32)
+        pk_off = np.array([0, 1, 2, 3, 4], np.uint32)
+        # request 2 re-uses set 3's key with another set's data: (idx 3, msg 0, sig 0)
+        sigs2, msgs2 = sigs + [sigs[0]], msgs + [msgs[0]]
+        blob, offs = pack_blobs(sigs2)
+        res = dev.verify_requests(req_off, None, np.array([0, 1, 2, 3, 4, 5], np.uint32),
+                                  np.frombuffer(b"".join(msgs2), np.uint8), blob, offs, bytes(32),
+                                  pk_indices=np.array([0, 1, 2, 3, 3], np.uint32))
+        assert [bool(v) for v in res.valid] == [True, False, False]
+        assert list(res.errors) == [0, 0, 0]
+    finally:
+        dev.close()

@@ -51,3 +51,35 @@ def test_attestations_random_large_vs_oracle(device):
     idx = rnd.sample(range(5000), 200)
     for i in idx:
         assert got[i] == S.compute_signing_root(S.attestation_data_root(data[i]), dom)
+
+
+def test_device_signing_roots_feed_verification(device):
+    """Signing roots computed in HBM become the messages of a device-resident
+    verify call (no host round trip): attestations signed over their roots verify."""
+    import numpy as np
+    import torch
+
+    from oracle import bls12_381 as O
+    rnd = random.Random(11)
+    n = 40
+    data = [rnd.randbytes(128) for _ in range(n)]
+    dom = rnd.randbytes(32)
+    roots = [S.compute_signing_root(S.attestation_data_root(d), dom) for d in data]
+    sks = [O.interop_secret_key(i).to_bytes(32, "big") for i in range(n)]
+    sigs = device.sign(sks, roots)
+    pks = device.sk_to_pk(sks)
+    cuda = torch.device("cuda", 0)
+    t = lambda b: torch.from_numpy(np.frombuffer(b, np.uint8).copy()).to(cuda)  # noqa: E731
+    d_data, d_dom, d_msgs = t(b"".join(data)), t(dom), torch.zeros(32 * n, dtype=torch.uint8, device=cuda)
+    device.signing_roots_attestation_device(n, d_data.data_ptr(), d_dom.data_ptr(), 0, d_msgs.data_ptr())
+    assert d_msgs.cpu().numpy().tobytes() == b"".join(roots)
+    d_pks, d_sigs = t(b"".join(pks)), t(b"".join(sigs))
+    d_sigoff = torch.from_numpy(np.arange(0, 96 * (n + 1), 96, dtype=np.uint32).view(np.int32)).to(cuda)
+    d_req = torch.from_numpy(np.array([0, 20, n], np.uint32).view(np.int32)).to(cuda)
+    d_seed = torch.zeros(32, dtype=torch.uint8, device=cuda)
+    d_valid = torch.zeros(2, dtype=torch.uint8, device=cuda)
+    d_err = torch.zeros(2, dtype=torch.uint8, device=cuda)
+    device.verify_requests_device(2, n, d_req.data_ptr(), d_pks.data_ptr(), None, d_msgs.data_ptr(),
+                                  d_sigs.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(), d_valid.data_ptr(),
+                                  d_err.data_ptr())
+    assert d_valid.cpu().tolist() == [1, 1] and d_err.cpu().tolist() == [0, 0]
