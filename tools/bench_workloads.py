@@ -185,7 +185,63 @@ def main():
         ts.append(time.perf_counter() - t1)
     ssz = {"attestation_signing_roots": n, "host_call_ms_p50": round(float(np.median(ts)) * 1e3, 3),
            "roots_per_s": round(n / float(np.median(ts)), 1)}
-    out = {"workloads": "C3 + C4 shard (1/8 of 1M mixed sets)", "validators_in_table": nv, "ssz": ssz,
+    # ---- C5: block import, one 32-block epoch --------------------------------------
+    # per block: proposer + RANDAO + 128 aggregate attestations (488 keys) + sync
+    # aggregate (512 keys) + 16 exits = 147 sets, one request (verifySignatureSets
+    # per block); signing roots computed on the GPU; invalid sets injected at 1e-3
+    # (wrong message, malformed signature bytes) -> exactly those blocks are false.
+    t0 = time.time()
+    dom = rng.bytes(32)
+    blocks, all_sets = 32, []
+    att_data = [rng.bytes(128) for _ in range(blocks * 128)]
+    att_roots = dev.signing_roots_attestation(att_data, dom)
+    hdr = dev.signing_roots_chunks([[rng.bytes(32) for _ in range(5)] for _ in range(blocks)], dom)
+    rnd_roots = dev.signing_roots_chunks([[int(e).to_bytes(8, "little") + bytes(24)] for e in range(blocks)], dom)
+    exit_roots = dev.signing_roots_chunks([[int(e).to_bytes(8, "little") + bytes(24),
+                                            int(v).to_bytes(8, "little") + bytes(24)]
+                                           for e, v in zip(range(blocks * 16), rng.integers(0, nv, blocks * 16))], dom)
+    sync_roots = dev.signing_roots_chunks([[rng.bytes(32)] for _ in range(blocks)], dom)
+    for bi in range(blocks):
+        prop = int(rng.integers(0, nv))
+        bs = [([prop], hdr[bi]), ([prop], rnd_roots[bi])]
+        for k in range(128):
+            bs.append(([int(m) for m in rng.choice(nv, a.committee, replace=False)], att_roots[bi * 128 + k]))
+        bs.append(([int(m) for m in rng.choice(nv, 512, replace=False)], sync_roots[bi]))
+        for k in range(16):
+            bs.append(([int(rng.integers(0, nv))], exit_roots[bi * 16 + k]))
+        all_sets.append(bs)
+    flat = [st for bs in all_sets for st in bs]
+    c5_sigs = sign_many([sum(sks[i] for i in ix) % R_ORDER for ix, _ in flat], [m for _, m in flat])
+    c5_msgs = [m for _, m in flat]
+    bad_blocks = set()
+    for j in rng.choice(len(flat), max(2, len(flat) // 1000), replace=False):
+        j = int(j)
+        bad_blocks.add(j // 147)
+        if j % 2:
+            c5_msgs[j] = hashlib.sha256(b"wrong" + j.to_bytes(4, "little")).digest()
+        else:
+            c5_sigs[j] = bytes([10]) * 96  # Buffer.alloc(96, 10), bls.test.ts:48
+    c5_idx = np.array([i for ix, _ in flat for i in ix], np.uint32)
+    c5_pko = np.zeros(len(flat) + 1, np.uint32)
+    c5_pko[1:] = np.cumsum([len(ix) for ix, _ in flat])
+    c5_req = np.arange(0, len(flat) + 1, 147, dtype=np.uint32)
+    c5_blob, c5_offs = pack_blobs(c5_sigs)
+    c5_mg = np.frombuffer(b"".join(c5_msgs), np.uint8)
+    gen_c5_s = time.time() - t0
+    r = dev.verify_requests(c5_req, None, c5_pko, c5_mg, c5_blob, c5_offs, bytes(32), pk_indices=c5_idx)
+    expect = [bi not in bad_blocks for bi in range(blocks)]
+    assert [bool(v) for v in r.valid] == expect, "C5 block verdicts"
+    ts = []
+    for _ in range(a.reps):
+        t1 = time.perf_counter()
+        dev.verify_requests(c5_req, None, c5_pko, c5_mg, c5_blob, c5_offs, bytes(32), pk_indices=c5_idx)
+        ts.append(time.perf_counter() - t1)
+    c5 = {"blocks": blocks, "sets": len(flat), "pubkeys": int(len(c5_idx)), "invalid_blocks": sorted(bad_blocks),
+          "verdicts_match": True, "batch_retries": r.batch_retries, "epoch_ms_p50": round(float(np.median(ts)) * 1e3, 3),
+          "sets_per_s": round(len(flat) / float(np.median(ts)), 1), "datagen_s": round(gen_c5_s, 2)}
+
+    out = {"workloads": "C3 + C4 shard (1/8 of 1M mixed sets) + C5 epoch", "validators_in_table": nv, "ssz": ssz,
+           "c5_block_import": c5,
            "c3": c3,
            "c4_shard": {"sets": n, "requests": nr, "pubkeys": int(len(idx)), "singles": a.singles,
                         "aggregate_and_proofs": a.aggregates, "committee": a.committee, **res},
