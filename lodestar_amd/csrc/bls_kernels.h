@@ -7,8 +7,6 @@
 #include "../../include/lodestar_bls.h"
 #include "bls_pairing.h"
 
-#include "bls_pairing.h"
-
 
 #define LB_ST_ZERO_SIGNATURE 6
 
