@@ -21,6 +21,7 @@ STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
     "pubkeys": "k_pubkeys_single", "scalar_pk": "k_scalar_pk", "lines": "k_lines",
     "decode_sigs": "k_decode_sigs", "scalar_sig": "k_scalar_sig", "sum_tree": "k_sum_tree",
     "miller_acc": "k_miller_acc", "merge": "k_merge", "lines_S": "k_lines_S", "tail": "k_tail",
+    "miller_wave": "k_pair_wc", "pubkeys_agg": "k_pubkeys_agg",
 }
 
 
@@ -52,6 +53,9 @@ def main():
             ent["hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
         if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c and c["SQ_WAVES"]:
             ent["valu_insts_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"])
+        if c.get("SQ_LDS_IDX_ACTIVE"):
+            # extra LDS cycles from bank conflicts / all LDS-array cycles (MI355X_MICROARCH.md LDS section)
+            ent["lds_bank_conflict_frac"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"], 5)
         res[stage] = ent
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
