@@ -65,12 +65,14 @@ struct Slot {
 
 struct lb_ctx {
   int device = -1;
-  // total streams <= GPU_MAX_HW_QUEUES (4 on the box).  Default LB_SLOTS=3: slot 0
-  // runs the two-stream DAG (synchronous calls, lowest latency), slots 1-2 one
-  // stream each; the async API round-robins all slots.  LB_SLOTS=2: two DAG
-  // slots; LB_SLOTS=4: four single-stream slots.
+  // total streams <= GPU_MAX_HW_QUEUES (4 on the box; a fifth stream shares a
+  // hardware queue and measured -20 %, profiles/ab_r01i.txt).  Default LB_SLOTS=4:
+  // four single-stream slots, i.e. four calls in flight on the async API; a
+  // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
+  // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
+  // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
   static constexpr int kMaxSlots = 4;
-  int n_slots = 3;
+  int n_slots = 4;
   int streams_per_slot[kMaxSlots] = {2, 1, 1, 1};
   Slot slots[kMaxSlots];
   int next_slot = 0;
@@ -389,6 +391,27 @@ int end_call_async(lb_ctx* ctx, Slot& sl) {
   return LB_OK;
 }
 
+// Synchronous verify calls run on slot 0 as the two-stream DAG.  When slot 0
+// owns a single stream (the default four single-stream slots), the call
+// borrows slot 1's stream (after slot 1's call in flight completes) and the
+// guard hands it back when the call returns (the call is complete by then).
+struct BorrowGuard {
+  lb_ctx* ctx;
+  bool active = false;
+  ~BorrowGuard() {
+    if (active) ctx->slots[0].st[1] = ctx->slots[0].st[0];
+  }
+};
+int borrow_second_stream(lb_ctx* ctx, BorrowGuard& g) {
+  Slot& s0 = ctx->slots[0];
+  if (ctx->streams_per_slot[0] == 1 && ctx->n_slots >= 2) {
+    LB_TRY(finish_slot(ctx, ctx->slots[1]));
+    s0.st[1] = ctx->slots[1].st[0];
+    g.active = true;
+  }
+  return LB_OK;
+}
+
 // Idle slot 0 for the synchronous helper entry points.
 int helper_slot(lb_ctx* ctx) {
   for (int i = 0; i < ctx->n_slots; i++) LB_TRY(finish_slot(ctx, ctx->slots[i]));
@@ -431,6 +454,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
   }
   for (int s = 0; s < lb_ctx::kMaxSlots; s++)
     ctx->streams_per_slot[s] = ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;
+  // LB_SLOT0_STREAMS=1|2 overrides slot 0's two-stream DAG (the synchronous, lowest-latency slot)
+  if (const char* e = getenv("LB_SLOT0_STREAMS")) ctx->streams_per_slot[0] = atoi(e) == 1 ? 1 : 2;
   for (int s = 0; ok && s < ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++)
@@ -550,6 +575,8 @@ int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d
   if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   uint64_t t = 0;
+  BorrowGuard g{ctx};
+  LB_TRY(borrow_second_stream(ctx, g));
   LB_TRY(submit_device(ctx, ctx->slots[0], b, d_valid, d_req_err, d_set_status, &t));  // slot 0: DAG, lowest latency
   return lb_wait(ctx, t, stats);
 }
@@ -607,6 +634,8 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
   const size_t out_bytes = al(nr) * 2 + al(ns ? ns : 1);
   Slot& sl = ctx->slots[0];  // synchronous host API: slot 0 (two-stream DAG)
+  BorrowGuard g{ctx};
+  LB_TRY(borrow_second_stream(ctx, g));
   LB_TRY(finish_slot(ctx, sl));
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
   LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
