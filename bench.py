@@ -90,7 +90,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("LB_SLOTS", "4")),
+    ap.add_argument("--inflight", type=int,
+                    default=int(os.environ.get("LB_SLOTS",
+                                               "8" if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 8 else "4")),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
     a = ap.parse_args()
 

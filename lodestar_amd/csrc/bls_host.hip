@@ -66,14 +66,15 @@ struct Slot {
 struct lb_ctx {
   int device = -1;
   // total streams <= GPU_MAX_HW_QUEUES (4 on the box; a fifth stream shares a
-  // hardware queue and measured -20 %, profiles/ab_r01i.txt).  Default LB_SLOTS=4:
-  // four single-stream slots, i.e. four calls in flight on the async API; a
+  // hardware queue and measured -20 %, profiles/ab_r01i.txt).  Default: one
+  // single-stream slot per hardware queue (4, or 8 with GPU_MAX_HW_QUEUES>=8),
+  // i.e. that many calls in flight on the async API; a
   // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
   // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
   // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
-  static constexpr int kMaxSlots = 4;
+  static constexpr int kMaxSlots = 8;
   int n_slots = 4;
-  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1};
+  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1, 1, 1, 1, 1};
   Slot slots[kMaxSlots];
   int next_slot = 0;
   uint64_t next_ticket = 1;
@@ -439,6 +440,10 @@ int lb_create(int device, lb_ctx** out_ctx) {
   lb_ctx* ctx = new lb_ctx();
   ctx->device = device;
   bool ok = hipSetDevice(device) == hipSuccess;
+  // one single-stream slot per hardware queue HIP gives this process (4 by
+  // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8
+  // calls in flight -- within run-to-run noise of 4 on MI355X, profiles/ab_r01i.txt)
+  if (const char* e = getenv("GPU_MAX_HW_QUEUES")) ctx->n_slots = atoi(e) >= 8 ? 8 : 4;
   if (const char* e = getenv("LB_SLOTS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
