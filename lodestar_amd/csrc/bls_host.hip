@@ -271,7 +271,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
     LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
     if (d_pk_off)
-      LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, 2048u, TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
+      // one wave per set, grid-stride: enough waves that every aggregate of a
+      // C4/C5-sized call (thousands of committee sets) gets its own
+      LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, n_sets < 16384u ? n_sets : 16384u, TPB, n_sets, src, d_pk_off, d_pk,
+               d_pk_st);
     LB_STAGE("scalar_pk", 0, k_scalar_pk, blocks_for(n_sets), TPB, n_sets, d_seed, (const g1j*)d_pk,
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
