@@ -4,15 +4,27 @@ Workload (BASELINE.json configs[1], the single-GPU config the metric is quoted
 on): 65,536 distinct-message single-pubkey attestation sets per GPU, submitted
 as 512 requests x 128 sets (MAX_SIGNATURE_SETS_PER_JOB, packages/beacon-node/
 src/chain/bls/multithread/index.ts:57), each request verified with
-verifySignatureSetsMaybeBatch semantics.  A "step" = one lb_verify_requests
-call over the whole 65,536-set batch with inputs already resident in HBM.
-Synthetic data: interop secret keys (packages/state-transition/src/util/
-interop.ts:19-23), messages sha256(seed || LE64(i)), signatures from the GPU
-signer (parity-checked against the oracle by tests and smoke()).
+verifySignatureSetsMaybeBatch semantics.  A "step" = one call over the whole
+65,536-set batch with inputs already resident in HBM.  Synthetic data: interop
+secret keys (packages/state-transition/src/util/interop.ts:19-23), messages
+sha256(seed || LE64(i)), signatures from the GPU signer (parity-checked
+against the oracle by tests and smoke()).
 
-Multi-GPU: each rank verifies its own 65,536 sets (weak scaling; sets are
-independent, no data-path collective).  value = total sets over all ranks /
-max-over-ranks time.
+Multi-GPU (--gpus N): one process per GPU.  Without WORLD_SIZE in the
+environment, bench.py starts the N ranks itself (child processes, before any
+GPU call); under torchrun it is one of them.  Each rank verifies its own
+65,536 sets per step (weak scaling, no data-path collective): every step runs
+as a two-phase call up to the rank's merged Miller product, the 576-byte Fp12
+partials of all ranks are all-gathered over gloo (host memory) and the
+combined check final_exp(prod) == 1 runs once per rank on its own GPU
+(north_star: partials combined on the host).  value = total sets
+over all ranks / max-over-ranks time.
+
+Secondary legs (N = 1, after the timed region; reported, never `value`):
+host-buffer API throughput (PCIe included), same-message gossip jobs (512
+jobs x 128 sets per call), an adversarial leg (one wrong-message set per call),
+the C1 CPU p50 of one 128-set job, p50 latency of one 128-set request on the
+GPU, the CPU baseline.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -22,6 +34,8 @@ import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -77,6 +91,40 @@ def cpu_baseline_c(pks, msgs, sigs, seconds: float, threads: int, per_request: i
     return done / el, done, el, C.variant()
 
 
+def cpu_c1_p50(pks, msgs, sigs, per_request: int, reps: int):
+    """C1 (BASELINE.json configs[0]): one 128-set verifySignatureSets job as one
+    worker thread runs it (worker.ts:30-108 on one core), p50 over `reps`."""
+    from oracle import c_oracle as C
+    req_off = np.array([0, per_request], np.uint32)
+    pk = np.frombuffer(b"".join(pks[:per_request]), np.uint8)
+    mg = np.frombuffer(b"".join(msgs[:per_request]), np.uint8)
+    blob, offs = C.pack_blobs(sigs[:per_request])
+    lat = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        valid, _ = C.verify_requests(req_off, pk, None, mg, blob, offs, bytes(32), 1)
+        lat.append((time.perf_counter() - t1) * 1e3)
+        assert valid.all()
+    return float(np.median(lat))
+
+
+def launch_ranks(a) -> int:
+    """--gpus N without a launcher: one child process per GPU (started before
+    this process touches the GPU), RANK/LOCAL_RANK/WORLD_SIZE in their env;
+    rank 0 prints the JSON line.  Returns the worst exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,12 +137,18 @@ def main():
                     help="sync calls after the timed region whose stage times price the dominant kernel")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the secondary legs (host API, same-message, ...)")
     ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
+    ap.add_argument("--combine", choices=["auto", "on", "off"], default="auto",
+                    help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on for N > 1)")
     ap.add_argument("--inflight", type=int,
                     default=int(os.environ.get("LB_SLOTS",
                                                "8" if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 8 else "4")),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
     a = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
 
     import torch
     import torch.distributed as dist
@@ -103,12 +157,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")  # barrier + max-over-ranks only; no data-path collective
+        dist.init_process_group("gloo")  # barrier, max-over-ranks and the 576-byte partials; no data-path collective
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)  # one process per GPU; ranks > devices only when rehearsing
     torch.cuda.set_device(gpu)
     from lodestar_amd.native import Device
     dev = Device(gpu)
+    combine = a.combine == "on" or (a.combine == "auto" and world > 1)
 
     n = a.sets
     seed = hashlib.sha256(b"lodestar-mi355x-bench").digest()
@@ -134,10 +189,11 @@ def main():
     d_err = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
     torch.cuda.synchronize()
 
-    def submit(k, nr=n_req, ns=n):
-        return dev.verify_requests_device_async(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
-                                                d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
-                                                d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
+    def submit(k, msg_ptr=None, partial=False):
+        return dev.verify_requests_device_async(n_req, n, d_reqoff.data_ptr(), d_pk.data_ptr(), None,
+                                                msg_ptr or d_msg.data_ptr(), d_sig.data_ptr(), d_sigoff.data_ptr(),
+                                                d_seed.data_ptr(), d_valid[k % nbuf].data_ptr(),
+                                                d_err[k % nbuf].data_ptr(), partial=partial)
 
     def step(k=0, nr=n_req, ns=n):
         # synchronous call (library slot 0: two-stream DAG, lowest latency)
@@ -145,8 +201,36 @@ def main():
                                    d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
                                    d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
 
+    combined = {"checks": 0, "passed": 0, "partials_per_check": 0, "gather_ms": 0.0, "check_ms": 0.0}
+
+    def resolve(t):
+        """Two-phase step: this rank's partial, all ranks' partials gathered on the
+        host (gloo), one final exponentiation on this GPU, resume with the verdict."""
+        part = dev.partial_wait_t(t)
+        t1 = time.perf_counter()
+        if world > 1:
+            mine = torch.frombuffer(bytearray(part), dtype=torch.uint8)
+            parts = [torch.zeros(576, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            partials = [bytes(p.numpy().tobytes()) for p in parts]
+        else:
+            partials = [part]
+        t2 = time.perf_counter()
+        ok = dev.gt_check(partials)
+        t3 = time.perf_counter()
+        dev.finish_t(t, ok)
+        dev.wait(t)
+        combined["checks"] += 1
+        combined["passed"] += int(ok)
+        combined["partials_per_check"] = len(partials)
+        combined["gather_ms"] += (t2 - t1) * 1e3
+        combined["check_ms"] += (t3 - t2) * 1e3
+
     for k in range(a.warmup):
         step(k)
+    if combine:  # warm the two-phase path too (every rank takes part in each gather)
+        resolve(submit(0, partial=True))
+        combined.update(checks=0, passed=0, gather_ms=0.0, check_ms=0.0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -161,25 +245,26 @@ def main():
 
     pending = []
     for k in range(a.steps):
-        if a.sync:
+        if a.sync and not combine:
             step(k)
             accumulate()
         else:
-            pending.append(submit(k))
-            if len(pending) >= nbuf:
-                dev.wait(pending.pop(0))
+            pending.append(submit(k, partial=combine))
+            if len(pending) >= (1 if a.sync else nbuf):
+                t = pending.pop(0)
+                resolve(t) if combine else dev.wait(t)
                 accumulate()
     for t in pending:
-        dev.wait(t)
+        resolve(t) if combine else dev.wait(t)
         accumulate()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
     ok = all(bool(v.cpu().numpy().all()) for v in d_valid) and not any(bool(e.cpu().numpy().any()) for e in d_err)
 
     # the same call, one at a time: per-kernel durations without other calls'
@@ -202,6 +287,10 @@ def main():
     p50 = float(np.median(lat)) if lat else None
     lat_stages = {name: round(ms, 3) for name, ms in dev.last_stage_times()} if lat else None
 
+    legs = {}
+    if world == 1 and not a.no_legs:
+        legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off)
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -209,40 +298,9 @@ def main():
     total_sets = n * world * a.steps
     value = total_sets / elapsed
     stage_ms = {k: v / max(n_acc[0], 1) for k, v in stage_acc.items()}
-    # roofline over the dominant kernel
-    roof = None
-    counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
-    timing = iso_ms if iso_ms else stage_ms
-    dom = max((k for k in timing if k not in ("start", "h2d", "d2h")), key=lambda k: timing[k])
-    if os.path.exists(counts_path):
-        oc = json.load(open(counts_path))
-        st = oc["stages"].get(dom)
-        if st:
-            per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
-            mads = per_set * n
-            achieved = mads / (timing[dom] * 1e-3) / 1e12
-            peak = PEAK_MAD_PER_S / 1e12
-            traffic = None
-            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_path):
-                traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
-            roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
-                    "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
-                    "algorithmic_mads_per_launch": mads,
-                    "launch_ms": round(timing[dom], 3),
-                    "timing": "median of %d one-at-a-time calls after the timed region (HIP events on the "
-                              "kernel's stream)" % a.iso_reps if iso_ms else "timed region, calls overlapped"}
-            if iso_ms and dom in stage_ms:
-                # the same kernel while other calls' kernels share the CUs (timed region)
-                roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
-                roof["in_pipeline_frac"] = round(mads / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
-            if "mads_per_set_total" in oc:
-                # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
-                pipe = value * oc["mads_per_set_total"] / 1e12
-                roof["pipeline_achieved"] = round(pipe, 4)
-                roof["pipeline_frac"] = round(pipe / peak, 5)
-                roof["mads_per_set"] = round(oc["mads_per_set_total"])
+    roof = roofline(iso_ms, stage_ms, n, value, a.iso_reps)
     cpu = None
+    c1 = None
     if not a.no_cpu_baseline and world == 1:
         # the box's CPU share is 16 threads per GPU (os.cpu_count() shows the whole host)
         threads = max(1, min(16, os.cpu_count() or 1))
@@ -252,6 +310,10 @@ def main():
                          f"verified by the C restatement oracle/c/bls_oracle.c ({variant}, {threads} threads, "
                          f"{el:.1f} s); blst itself cannot run here (no node>=20 / @chainsafe/blst); the "
                          f"reference's own anchor is ~0.9 ms/set/core (metrics/metrics/lodestar.ts:470)"}
+        c1 = {"config": "C1: verifySignatureSets on one 128-set job (BASELINE.json configs[0])",
+              "cpu_p50_ms": round(cpu_c1_p50(pks, msgs, sigs, a.per_request, 7), 3), "cpu_threads": 1,
+              "cpu_kind": "port (oracle/c/bls_oracle.c, one worker thread)",
+              "gpu_p50_ms": round(p50, 3) if p50 is not None else None}
     out = {
         "metric": "verified signature sets/sec",
         "value": round(value, 2),
@@ -268,19 +330,142 @@ def main():
         "config": {"workload": f"C2: {n} distinct-message single-pubkey sets per GPU, {n_req} requests x "
                                f"{a.per_request} sets, verifySignatureSetsMaybeBatch semantics",
                    "sets_per_gpu": n, "sets_per_request": a.per_request, "parallelism": f"shard{world}"},
+        "requested_gpus": a.gpus,
+        "ranks_joined": world,
         "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
         "p50_stage_ms": lat_stages,
         "all_valid": ok,
-        "overlap": "sync" if a.sync else f"{nbuf} calls in flight (lb_verify_requests_device_async)",
+        "overlap": "sync" if a.sync else f"{nbuf} calls in flight",
+        "combine": ({"mode": "two-phase calls; per-step all-gather of the ranks' 576-byte Fp12 partials (gloo) and "
+                             "one final exponentiation per rank on its GPU (lb_gt_check)",
+                     "checks": combined["checks"], "passed": combined["passed"],
+                     "partials_per_check": combined["partials_per_check"],
+                     "gather_ms_avg": round(combined["gather_ms"] / max(combined["checks"], 1), 3),
+                     "check_ms_avg": round(combined["check_ms"] / max(combined["checks"], 1), 3)}
+                    if combine else None),
         "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
         "iso_stage_ms": {k: round(v, 3) for k, v in iso_ms.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "c1": c1,
+        **legs,
         "datagen_s": round(t_gen, 2),
     }
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+
+
+def roofline(iso_ms, stage_ms, n, value, iso_reps):
+    """Dominant kernel's integer-MAD roofline (achieved = algorithmic mads of one
+    launch / its HIP-event duration, one call at a time) + the pipeline's."""
+    counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
+    timing = iso_ms if iso_ms else stage_ms
+    cands = [k for k in timing if k not in ("start", "h2d", "d2h")]
+    if not cands or not os.path.exists(counts_path):
+        return None
+    dom = max(cands, key=lambda k: timing[k])
+    oc = json.load(open(counts_path))
+    st = oc["stages"].get(dom)
+    if not st:
+        return None
+    per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
+    mads = per_set * n
+    achieved = mads / (timing[dom] * 1e-3) / 1e12
+    peak = PEAK_MAD_PER_S / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+    roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
+            "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
+            "algorithmic_mads_per_launch": mads,
+            "launch_ms": round(timing[dom], 3),
+            "timing": "median of %d one-at-a-time calls after the timed region (HIP events on the "
+                      "kernel's stream)" % iso_reps if iso_ms else "timed region, calls overlapped"}
+    if iso_ms and dom in stage_ms:
+        # the same kernel while other calls' kernels share the CUs (timed region)
+        roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
+        roof["in_pipeline_frac"] = round(mads / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
+    if "mads_per_set_total" in oc:
+        # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
+        pipe = value * oc["mads_per_set_total"] / 1e12
+        roof["pipeline_achieved"] = round(pipe, 4)
+        roof["pipeline_frac"] = round(pipe / peak, 5)
+        roof["mads_per_set"] = round(oc["mads_per_set_total"])
+    return roof
+
+
+def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off):
+    legs = {}
+    reps = max(4, a.steps // 2)
+    # (1) host-buffer API (what BlsGpuVerifier calls): numpy inputs, pinned staging, PCIe both ways
+    pk_h = np.frombuffer(b"".join(pks), np.uint8)
+    mg_h = np.frombuffer(b"".join(msgs), np.uint8)
+    blob_h = np.frombuffer(b"".join(sigs), np.uint8)
+    seed = hashlib.sha256(b"batch-rand").digest()
+    pcs = [dev.verify_requests_async(req_off, pk_h, None, mg_h, blob_h, sig_off, seed) for _ in range(nbuf)]
+    for pc in pcs:
+        assert dev.wait_call(pc).valid.all()
+    t1 = time.perf_counter()
+    pend = []
+    for _ in range(reps):
+        pend.append(dev.verify_requests_async(req_off, pk_h, None, mg_h, blob_h, sig_off, seed))
+        if len(pend) >= nbuf:
+            dev.wait_call(pend.pop(0))
+    allv = True
+    for pc in pend:
+        allv &= bool(dev.wait_call(pc).valid.all())
+    el = time.perf_counter() - t1
+    legs["host_api"] = {"sets_per_s": round(n * reps / el, 1), "calls": reps, "all_valid": allv,
+                        "api": f"lb_verify_requests_async, host buffers, {nbuf} calls in flight (PCIe included)"}
+    # (2) adversarial: one wrong-message set per call -> merged check fails, every request's tail runs
+    bad = bytearray(b"".join(msgs))
+    bad[32 * (n // 2):32 * (n // 2) + 32] = hashlib.sha256(b"wrong").digest()
+    d_bad = torch.from_numpy(np.frombuffer(bytes(bad), np.uint8).copy()).to(cuda)
+    torch.cuda.synchronize()
+    dev.wait(submit(0, d_bad.data_ptr()))
+    t1 = time.perf_counter()
+    pend = []
+    for k in range(reps):
+        pend.append(submit(k, d_bad.data_ptr()))
+        if len(pend) >= nbuf:
+            dev.wait(pend.pop(0))
+    for t in pend:
+        dev.wait(t)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    legs["adversarial"] = {"sets_per_s": round(n * reps / el, 1), "calls": reps,
+                           "case": "one wrong-message set per 65,536-set call: merged check fails, 512 per-request "
+                                   "tails (worker.ts:74-85 retry)"}
+    # (3) same-message gossip jobs: 512 attestation-data groups x 128 validators per call, pubkeys by index
+    from lodestar_amd.native import Device  # noqa: F401
+    n_jobs, per_job = 512, 128
+    roots = [hashlib.sha256(b"attdata" + j.to_bytes(4, "little")).digest() for j in range(n_jobs)]
+    if dev.pubkey_table_size() < len(pks):
+        dev.pubkey_table_append(pks)
+    rng = np.random.default_rng(3)
+    members = [rng.choice(len(pks), per_job, replace=False) for _ in range(n_jobs)]
+    flat_sk = [sks[int(v)] for m in members for v in m]
+    flat_msg = [roots[j] for j in range(n_jobs) for _ in range(per_job)]
+    sm_sigs = []
+    for s in range(0, len(flat_sk), 16384):
+        sm_sigs += dev.sign(flat_sk[s:s + 16384], flat_msg[s:s + 16384])
+    jobs = [([int(v) for v in members[j]], sm_sigs[j * per_job:(j + 1) * per_job], roots[j]) for j in range(n_jobs)]
+    res, fast, _ = dev.verify_same_message_batch(jobs, seed, by_index=True)
+    assert all(fast) and all(all(r) for r in res)
+    lat = []
+    for _ in range(max(3, reps // 2)):
+        t1 = time.perf_counter()
+        dev.verify_same_message_batch(jobs, seed, by_index=True)
+        lat.append(time.perf_counter() - t1)
+    sm_stage = {k: round(v, 3) for k, v in dev.last_stage_times()}
+    legs["same_message"] = {"sets_per_s": round(n_jobs * per_job / float(np.median(lat)), 1),
+                            "ms_per_call": round(float(np.median(lat)) * 1e3, 3), "jobs": n_jobs,
+                            "sets_per_job": per_job,
+                            "api": "lb_verify_same_message_batch (host buffers, validator indices, one call)",
+                            "stage_ms": sm_stage}
+    return legs
 
 
 if __name__ == "__main__":

@@ -65,7 +65,7 @@ extern "C" {
 #define LB_SIG_UNCOMPRESSED 192
 #define LB_MESSAGE_BYTES 32
 #define LB_SEED_BYTES 32
-#define LB_GT_BYTES 576
+#define LB_GT_BYTES 576 /* an Fp12 value: 12 x 48-byte big-endian Fp */
 
 typedef struct lb_ctx lb_ctx;
 
@@ -144,16 +144,57 @@ int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* batch, uint8_
                               uint8_t* d_out_request_error, uint8_t* d_out_set_status, lb_verify_stats* stats);
 
 /*
- * Asynchronous device-resident variant: enqueue the call and return a ticket;
- * lb_wait(ticket) blocks until it is complete.  Up to two calls are in flight
- * per context (each on its own pair of HIP streams and workspace), so the
- * tail of one call overlaps the per-set stages of the next -- the way the
- * reference pool keeps several worker packages in flight (index.ts:362-519).
- * Input and output buffers must stay valid until lb_wait returns.
+ * Asynchronous variants: enqueue the call and return a ticket; lb_wait(ticket)
+ * blocks until it is complete and reports THAT call's stats.  One call is in
+ * flight per slot (LB_SLOTS, default 4 = one per HIP hardware queue, each with
+ * its own stream, workspace and pinned staging), so the tail of one call
+ * overlaps the per-set stages of the next -- the way the reference pool keeps
+ * several worker packages in flight (index.ts:362-519).  Submitting more calls
+ * than slots first waits for the oldest call of the reused slot.
+ *   lb_verify_requests_device_async: every pointer is device memory (bench.py).
+ *   lb_verify_requests_async: host buffers, staged through the slot's pinned
+ *     buffer; the outputs are written when the call retires (lb_wait, or a
+ *     later call reusing the slot).  The caller keeps every buffer valid until
+ *     lb_wait returns.
  */
 int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* d_out_request_valid,
                                     uint8_t* d_out_request_error, uint8_t* d_out_set_status, uint64_t* out_ticket);
+int lb_verify_requests_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* out_request_valid,
+                             uint8_t* out_request_error, uint8_t* out_set_status, uint64_t* out_ticket);
 int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats);
+
+/*
+ * Multi-GPU combine (BASELINE north_star: "the per-GPU
+ * partial Fp12 Miller-loop products (576 B each) are combined on the host").
+ * The batch equation is multiplicative across shards, so each GPU verifies its
+ * shard of requests up to its merged Miller product
+ *     P_g = prod_{k in shard, not already false} F_k * Miller(-g1, sum_k S_k)
+ * and stops there (two-phase call).  The host gathers the partials, checks
+ * final_exp(prod_g P_g) == 1 ONCE (lb_gt_check, on any one GPU), and resumes
+ * every shard with the verdict: merged_ok = 1 -> every request that is not
+ * already false is valid, no further work; merged_ok = 0 -> each shard runs its
+ * per-request tails (each request verified alone, as worker.ts:74-85 does after
+ * a failed merged batch).  Either way the per-request verdicts are those of
+ * lb_verify_requests.  Reference analogue of the fan-out: the pool's chunking
+ * across workers, chain/bls/multithread/index.ts:191-205.
+ *
+ *   lb_verify_requests_partial_async(flags)  enqueue (LB_BATCH_DEVICE: every
+ *                                           pointer, outputs included, is device memory)
+ *   lb_partial_wait(ticket, out576)          block until the shard's partial is ready
+ *   lb_gt_check(n, partials, out_is_one)     final_exp(prod of n partials) == 1
+ *   lb_verify_requests_finish(ticket, ok)    resume the shard with the verdict
+ *   lb_wait(ticket)                          verdicts (and stats) of the shard
+ * A partial is 12 big-endian canonical Fp coefficients (c0.c0.c0 ... c1.c2.c1,
+ * the lb_pairing order); an empty shard's partial is 1.  A two-phase call that
+ * is waited for without lb_verify_requests_finish resumes with merged_ok = 0.
+ */
+#define LB_BATCH_DEVICE 1u
+int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* batch, uint32_t flags,
+                                     uint8_t* out_request_valid, uint8_t* out_request_error, uint8_t* out_set_status,
+                                     uint64_t* out_ticket);
+int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576);
+int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* out_is_one);
+int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok);
 
 /*
  * verifySignatureSetsSameMessage for one job (<= 128 sets in the reference,
@@ -166,6 +207,35 @@ int lb_verify_same_message(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys /* n 
                            const uint8_t* signatures, const uint32_t* sig_offsets /* n + 1 */,
                            const uint8_t* message /* 32 */, const uint8_t* seed /* 32 */, uint8_t* out_valid,
                            uint32_t* out_used_fast_path);
+
+/*
+ * Many same-message jobs in one call (the dominant gossip load: one job per
+ * attestation-data group, chunked to <= 128 sets by verifySignatureSetsSameMessage,
+ * index.ts:218-242).  Job j = sets [job_offsets[j], job_offsets[j+1]) over
+ * messages[32 j .. 32 j + 32).  Every signature is decoded and validated once
+ * on the GPU, each job's pubkeys and signatures are summed (plain sums, as
+ * jobItemWorkReq does, jobItem.ts:64-86) and all jobs' aggregated sets are
+ * verified together as 1-set requests of one merged call; the sets of a job
+ * whose aggregate fails (or that holds a signature failing
+ * Signature.fromBytes(validate=true)) are re-verified each alone
+ * (jobItemSameMessageToMultiSet, jobItem.ts:93-125).  out_valid: n_sets
+ * verdicts; out_job_fast (optional): 1 where the job's aggregate passed.
+ * stats (optional): batch_retries = jobs retried set by set,
+ * batch_sigs_success = sets verified by a passing aggregate.
+ */
+typedef struct {
+  uint32_t n_jobs;
+  uint32_t n_sets;
+  const uint32_t* job_offsets;     /* n_jobs + 1                                    */
+  const uint8_t* pubkeys;          /* n_sets x 96 (uncompressed), or NULL with ...  */
+  const uint32_t* pubkey_indices;  /* n_sets validator indices (device pubkey table) */
+  const uint8_t* signatures;       /* concatenated signature bytes                  */
+  const uint32_t* sig_offsets;     /* n_sets + 1                                    */
+  const uint8_t* messages;         /* n_jobs x 32                                   */
+  const uint8_t* seed;             /* 32                                            */
+} lb_same_message_batch;
+int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* batch, uint8_t* out_valid,
+                                 uint8_t* out_job_fast, lb_verify_stats* stats);
 
 /* Sum of n uncompressed pubkeys -> 96-byte uncompressed encoding.  n == 0 ->
  * LB_ERR_INVALID_ARGUMENT (EMPTY_AGGREGATE_ARRAY). *out_status = LB_SET_*. */

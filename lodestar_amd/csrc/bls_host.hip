@@ -43,6 +43,23 @@ static unsigned long long opcount_read_reset() {
 // ============================================================================
 // Host side: context, workspace, C ABI
 // ============================================================================
+// What a call keeps between its front half (everything up to the merged
+// product) and its tails (per-request final exponentiations), so a two-phase
+// call (lb_verify_requests_partial_async) can stop after the front half, hand
+// its Fp12 partial to the host and resume with the host's combined verdict.
+struct PipeState {
+  uint32_t n_req = 0, n_sets = 0, n_pairs = 0;
+  bool merged = false, tail_wave = true;
+  const uint32_t* d_req_off = nullptr;
+  uint32_t* d_lines = nullptr;
+  g2a* d_S = nullptr;
+  fp12* d_F = nullptr;
+  uint8_t* d_bad = nullptr;
+  uint8_t* d_valid = nullptr;
+  uint8_t* d_mflag = nullptr;
+  uint32_t* d_mstats = nullptr;
+};
+
 // One in-flight call: two streams (DAG), own workspace, staging and events.
 struct Slot {
   hipStream_t st[2] = {};
@@ -52,7 +69,7 @@ struct Slot {
   size_t ws_cap = 0;
   char* h_pin = nullptr;
   size_t pin_cap = 0;
-  static constexpr int kMaxStages = 20;
+  static constexpr int kMaxStages = 24;
   hipEvent_t ev0[kMaxStages] = {}, ev1[kMaxStages] = {};
   const char* stage_name[kMaxStages] = {};
   int n_stages = 0;
@@ -61,6 +78,25 @@ struct Slot {
   bool busy = false;
   uint64_t ticket = 0;
   uint32_t* h_stats = nullptr;  // pinned: [batch_retries, batch_sigs_success] of the call in flight
+  PipeState ps;
+  // two-phase calls: front half enqueued, tails wait for lb_verify_requests_finish
+  bool partial_pending = false;
+  hipEvent_t partial_ev = nullptr;
+  uint8_t* h_partial = nullptr;  // pinned, 576 B
+  // host-buffer calls: device outputs, their pinned copies and the caller's
+  // buffers they are copied into when the call retires (finish_slot)
+  uint8_t *dv_valid = nullptr, *dv_err = nullptr, *dv_sst = nullptr;
+  char* h_out = nullptr;
+  uint8_t *out_valid = nullptr, *out_err = nullptr, *out_sst = nullptr;
+  uint32_t out_nr = 0, out_ns = 0;
+};
+
+// Stats of a retired call, kept per ticket (lb_wait reports the stats of ITS
+// ticket even when another call retired the slot first).
+struct TicketStats {
+  uint64_t ticket = 0;
+  uint32_t batch_retries = 0, batch_sigs_success = 0;
+  float wall_ms = 0.f;
 };
 
 struct lb_ctx {
@@ -105,6 +141,14 @@ struct lb_ctx {
   unsigned long long stage_ops[Slot::kMaxStages] = {};
   float wall_ms = 0.f;
   uint32_t batch_retries = 0, batch_sigs_success = 0;
+  static constexpr int kTicketRing = 64;
+  TicketStats tstats[kTicketRing];
+  // lb_gt_check runs on its own stream and buffers, so the host combine of the
+  // shards' partials never drains the slots' calls in flight
+  hipStream_t aux_stream = nullptr;
+  uint8_t* d_aux = nullptr;
+  uint8_t* h_aux = nullptr;
+  size_t aux_cap = 0;
 };
 
 namespace {
@@ -224,10 +268,35 @@ int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
 // (k_miller_acc, several pairs per lane sharing the Fp12 squarings); the
 // original one-pair-per-lane Miller (k_miller_sets + k_prod_tree) remains
 // selectable with LB_MILLER=lane for comparison.
+// Tails of a call (after the per-request products F_k): with a merged check,
+// the per-request tails run only when d_mflag[0] == 0 (k_lines_S / k_tail skip
+// themselves otherwise); without one, every request runs its tail.
+int run_tails(lb_ctx* ctx, Slot& sl) {
+  const PipeState& p = sl.ps;
+  if (p.merged) {
+    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
+             p.d_lines, (const uint8_t*)p.d_mflag);
+    LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
+             (const fp12*)p.d_F, (const uint8_t*)p.d_bad, p.d_valid, (const uint8_t*)p.d_mflag);
+    hipLaunchKernelGGL(k_merge_stats, dim3(1), dim3(TPB), 0, sl.st[0], p.n_req, p.d_req_off, (const uint8_t*)p.d_bad,
+                       (const uint8_t*)p.d_mflag, p.d_mstats);
+    LB_HIP(hipGetLastError());
+    LB_HIP(hipMemcpyAsync(sl.h_stats, p.d_mstats, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st[0]));
+  } else if (p.tail_wave) {
+    LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
+             (const fp12*)p.d_F, (const uint8_t*)p.d_bad, p.d_valid, (const uint8_t*)nullptr);
+  } else {
+    LB_STAGE("final_exp", 0, k_final, blocks_for(p.n_req), TPB, p.n_req, (const fp12*)p.d_F, (const uint8_t*)p.d_bad,
+             p.d_valid);
+  }
+  return LB_OK;
+}
+
 int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
                  const uint8_t* d_pks, const uint32_t* d_pk_off, const uint32_t* d_pk_idx, const uint8_t* d_msgs, const uint8_t* d_sigs,
                  const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
-                 uint8_t* d_set_status, Bump& ws) {
+                 uint8_t* d_set_status, Bump& ws, uint8_t* d_partial = nullptr) {
+  const bool partial = d_partial != nullptr;
   const uint32_t ns = n_sets ? n_sets : 1;
   g2j* d_sig = ws.take<g2j>(ns);
   g2j* d_rsig = ws.take<g2j>(ns);
@@ -239,9 +308,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   const bool by_wave =
       !by_lines && (ctx->miller_mode == 3 || (ctx->miller_mode == 0 && n_sets <= ctx->wave_max_sets));
   fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);  // per-set Miller values (lane / wave modes)
-  const bool tail_wave = ctx->tail_wave;
+  // a two-phase call always merges (its partial is the merged product) and uses the wave tails
+  const bool tail_wave = ctx->tail_wave || partial;
   // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
-  const bool merged = tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req;
+  const bool merged = partial || (tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req);
   const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
   uint32_t* d_lines =
       (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
@@ -321,6 +391,20 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   } else
     LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, fS_in,
              (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
+  PipeState& ps = sl.ps;
+  ps.n_req = n_req;
+  ps.n_sets = n_sets;
+  ps.n_pairs = n_pairs;
+  ps.merged = merged;
+  ps.tail_wave = tail_wave;
+  ps.d_req_off = d_req_off;
+  ps.d_lines = d_lines;
+  ps.d_S = d_S;
+  ps.d_F = d_F;
+  ps.d_bad = d_bad;
+  ps.d_valid = d_valid;
+  ps.d_mflag = d_mflag;
+  ps.d_mstats = d_mstats;
   if (merged) {
     // merged check: one tail for the whole call; per-request tails only if it fails
     LB_HIP(hipMemsetAsync(d_mflag, 0, 2, sl.st[0]));
@@ -328,22 +412,20 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              d_Fall);
     LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
              (const uint8_t*)nullptr);
+    if (partial) {
+      // two-phase call: the merged Miller product goes to the host, which
+      // combines it with the other GPUs' partials; the tails wait for its verdict
+      LB_STAGE("partial", 0, k_partial, 1u, TPB, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+               (const fp12*)d_Fall, d_partial);
+      LB_HIP(hipMemcpyAsync(sl.h_partial, d_partial, LB_GT_BYTES, hipMemcpyDeviceToHost, sl.st[0]));
+      LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
+      sl.partial_pending = true;
+      return LB_OK;
+    }
     LB_STAGE("tail_all", 0, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
              (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
-    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines,
-             (const uint8_t*)d_mflag);
-    LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
-             (const uint8_t*)d_bad, d_valid, (const uint8_t*)d_mflag);
-    hipLaunchKernelGGL(k_merge_stats, dim3(1), dim3(TPB), 0, sl.st[0], n_req, d_req_off, (const uint8_t*)d_bad,
-                       (const uint8_t*)d_mflag, d_mstats);
-    LB_HIP(hipGetLastError());
-    LB_HIP(hipMemcpyAsync(sl.h_stats, d_mstats, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st[0]));
-  } else if (tail_wave)
-    LB_STAGE("tail", 0, k_tail, n_req, TPB, n_req, n_pairs, n_sets, (const uint32_t*)d_lines, (const fp12*)d_F,
-             (const uint8_t*)d_bad, d_valid, (const uint8_t*)nullptr);
-  else
-    LB_STAGE("final_exp", 0, k_final, blocks_for(n_req), TPB, n_req, (const fp12*)d_F, (const uint8_t*)d_bad, d_valid);
-  return LB_OK;
+  }
+  return run_tails(ctx, sl);
 }
 
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
@@ -351,7 +433,7 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
                    (size_t)LB_MILLER_LINES * 72 * 4;
   size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
-  return ns * per_set + (size_t)(n_req + 1) * per_req + 64 * 256;
+  return ns * per_set + (size_t)(n_req + 1) * per_req + 64 * 256 + 4096;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -363,9 +445,43 @@ int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
   return LB_OK;
 }
 
-// Wait for a slot's outstanding call and publish its stage times.
+// Copy a host-buffer call's verdicts from the device into its pinned staging
+// (enqueued after the tails; the caller's buffers are filled in finish_slot).
+int enqueue_host_out(lb_ctx* ctx, Slot& sl) {
+  if (!sl.out_valid) return LB_OK;
+  const size_t a = (sl.out_nr + 255) & ~(size_t)255;
+  LB_HIP(hipMemcpyAsync(sl.h_out, sl.dv_valid, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_HIP(hipMemcpyAsync(sl.h_out + a, sl.dv_err, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
+  if (sl.out_ns) LB_HIP(hipMemcpyAsync(sl.h_out + 2 * a, sl.dv_sst, sl.out_ns, hipMemcpyDeviceToHost, sl.st[0]));
+  return LB_OK;
+}
+
+int end_call(lb_ctx* ctx, Slot& sl) {
+  LB_TRY(enqueue_host_out(ctx, sl));
+  LB_HIP(hipEventRecord(sl.wall1, sl.st[0]));
+  LB_HIP(hipEventRecord(sl.done, sl.st[0]));
+  return LB_OK;
+}
+
+// Second phase of a two-phase call: the host's combined verdict (merged_ok)
+// decides whether the per-request tails run (k_lines_S / k_tail skip
+// themselves when d_mflag[0] != 0).
+int finish_partial(lb_ctx* ctx, Slot& sl, bool merged_ok) {
+  if (!sl.partial_pending) return LB_OK;
+  sl.partial_pending = false;
+  if (sl.ps.n_req) {  // (an empty call has no tails)
+    LB_HIP(hipMemsetAsync(sl.ps.d_mflag, merged_ok ? 1 : 0, 1, sl.st[0]));
+    LB_TRY(run_tails(ctx, sl));
+  }
+  return end_call(ctx, sl);
+}
+
+// Wait for a slot's outstanding call and publish its stage times, stats and
+// (host-buffer calls) verdicts.  A two-phase call whose host verdict never came
+// runs its per-request tails (merged_ok = 0: every verdict computed alone).
 int finish_slot(lb_ctx* ctx, Slot& sl) {
   if (!sl.busy) return LB_OK;
+  LB_TRY(finish_partial(ctx, sl, false));
   LB_HIP(hipEventSynchronize(sl.done));
   ctx->n_stages = sl.n_stages;
   for (int i = 0; i < sl.n_stages; i++) {
@@ -378,21 +494,42 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
   LB_HIP(hipEventElapsedTime(&ctx->wall_ms, sl.wall0, sl.wall1));
   ctx->batch_retries = sl.h_stats[0];
   ctx->batch_sigs_success = sl.h_stats[1];
+  TicketStats& ts = ctx->tstats[sl.ticket % lb_ctx::kTicketRing];
+  ts.ticket = sl.ticket;
+  ts.batch_retries = sl.h_stats[0];
+  ts.batch_sigs_success = sl.h_stats[1];
+  ts.wall_ms = ctx->wall_ms;
+  if (sl.out_valid) {
+    const size_t a = (sl.out_nr + 255) & ~(size_t)255;
+    memcpy(sl.out_valid, sl.h_out, sl.out_nr);
+    memcpy(sl.out_err, sl.h_out + a, sl.out_nr);
+    if (sl.out_sst && sl.out_ns) memcpy(sl.out_sst, sl.h_out + 2 * a, sl.out_ns);
+    sl.out_valid = sl.out_err = sl.out_sst = nullptr;
+  }
   sl.busy = false;
   return LB_OK;
 }
 
 int begin_call(lb_ctx* ctx, Slot& sl) {
   sl.n_stages = 0;
+  sl.partial_pending = false;
+  sl.out_valid = sl.out_err = sl.out_sst = nullptr;
   LB_HIP(hipEventRecord(sl.wall0, sl.st[0]));
   return LB_OK;
 }
+// Mark the slot busy under a new ticket; a complete call also records its end
+// (a two-phase call records it in finish_partial).
 int end_call_async(lb_ctx* ctx, Slot& sl) {
-  LB_HIP(hipEventRecord(sl.wall1, sl.st[0]));
-  LB_HIP(hipEventRecord(sl.done, sl.st[0]));
+  if (!sl.partial_pending) LB_TRY(end_call(ctx, sl));
   sl.busy = true;
   sl.ticket = ctx->next_ticket++;
   return LB_OK;
+}
+
+Slot* slot_of_ticket(lb_ctx* ctx, uint64_t ticket) {
+  for (int s = 0; s < ctx->n_slots; s++)
+    if (ctx->slots[s].busy && ctx->slots[s].ticket == ticket) return &ctx->slots[s];
+  return nullptr;
 }
 
 // Synchronous verify calls run on slot 0 as the two-stream DAG.  When slot 0
@@ -474,10 +611,13 @@ int lb_create(int device, lb_ctx** out_ctx) {
       ok = hipEventCreate(&sl.ev0[i]) == hipSuccess && hipEventCreate(&sl.ev1[i]) == hipSuccess;
     ok = ok && hipEventCreate(&sl.wall0) == hipSuccess && hipEventCreate(&sl.wall1) == hipSuccess &&
          hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess &&
-         hipHostMalloc(&sl.h_stats, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+         hipEventCreateWithFlags(&sl.partial_ev, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc(&sl.h_stats, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc(&sl.h_partial, LB_GT_BYTES, hipHostMallocDefault) == hipSuccess;
     if (ok) sl.h_stats[0] = sl.h_stats[1] = 0;
   }
   ctx->stream = ctx->slots[0].st[0];
+  ok = ok && hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) == hipSuccess;
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;
@@ -504,11 +644,19 @@ int lb_destroy(lb_ctx* ctx) {
     if (sl.wall0) (void)hipEventDestroy(sl.wall0);
     if (sl.wall1) (void)hipEventDestroy(sl.wall1);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.partial_ev) (void)hipEventDestroy(sl.partial_ev);
     if (sl.h_stats) (void)hipHostFree(sl.h_stats);
+    if (sl.h_partial) (void)hipHostFree(sl.h_partial);
     for (int i = 0; i < ctx->streams_per_slot[s]; i++)
       if (sl.st[i]) (void)hipStreamDestroy(sl.st[i]);
   }
   if (ctx->d_table) (void)hipFree(ctx->d_table);
+  if (ctx->aux_stream) {
+    (void)hipStreamSynchronize(ctx->aux_stream);
+    (void)hipStreamDestroy(ctx->aux_stream);
+  }
+  if (ctx->d_aux) (void)hipFree(ctx->d_aux);
+  if (ctx->h_aux) (void)hipHostFree(ctx->h_aux);
   delete ctx;
   return LB_OK;
 }
@@ -536,71 +684,32 @@ int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names
 }
 
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
-                         uint8_t* d_set_status, uint64_t* out_ticket) {
+                         uint8_t* d_set_status, bool partial, uint64_t* out_ticket) {
   LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
   LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(b->n_requests, b->n_sets)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
+  uint8_t* d_partial = partial ? ws.take<uint8_t>(LB_GT_BYTES) : nullptr;
   LB_TRY(begin_call(ctx, sl));
   if (b->n_requests)
     LB_TRY(run_pipeline(ctx, sl, b->n_requests, b->n_sets, b->request_offsets, b->pubkeys, b->pk_offsets,
-                        b->pubkey_indices, b->messages,
-                        b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err, d_set_status, ws));
+                        b->pubkey_indices, b->messages, b->signatures, b->sig_offsets, b->seed, d_valid, d_req_err,
+                        d_set_status, ws, d_partial));
+  else if (partial) {  // nothing to verify: the partial is the identity (1 in Fp12)
+    memset(sl.h_partial, 0, LB_GT_BYTES);
+    sl.h_partial[47] = 1;
+    LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
+    sl.ps = PipeState{};
+    sl.partial_pending = true;
+  }
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
   return LB_OK;
 }
 
-int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
-                                    uint8_t* d_set_status, uint64_t* out_ticket) {
-  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
-  LB_TRY(validate_batch(ctx, b));
-  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
-  LB_HIP(hipSetDevice(ctx->device));
-  Slot& sl = ctx->slots[ctx->next_slot];
-  ctx->next_slot = (ctx->next_slot + 1) % ctx->n_slots;
-  return submit_device(ctx, sl, b, d_valid, d_req_err, d_set_status, out_ticket);
-}
-
-int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
-  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
-  LB_HIP(hipSetDevice(ctx->device));
-  for (int s = 0; s < ctx->n_slots; s++) {
-    Slot& sl = ctx->slots[s];
-    if (sl.busy && sl.ticket == ticket) LB_TRY(finish_slot(ctx, sl));
-  }
-  if (stats) {
-    stats->batch_retries = ctx->batch_retries;
-    stats->batch_sigs_success = ctx->batch_sigs_success;
-    stats->device_ms = ctx->wall_ms;
-  }
-  return LB_OK;
-}
-
-int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
-                              uint8_t* d_set_status, lb_verify_stats* stats) {
-  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
-  LB_TRY(validate_batch(ctx, b));
-  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
-  LB_HIP(hipSetDevice(ctx->device));
-  uint64_t t = 0;
-  BorrowGuard g{ctx};
-  LB_TRY(borrow_second_stream(ctx, g));
-  LB_TRY(submit_device(ctx, ctx->slots[0], b, d_valid, d_req_err, d_set_status, &t));  // slot 0: DAG, lowest latency
-  return lb_wait(ctx, t, stats);
-}
-
-int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
-                       uint8_t* out_set_status, lb_verify_stats* stats) {
-  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
-  LB_TRY(validate_batch(ctx, b));
-  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
-  LB_HIP(hipSetDevice(ctx->device));
+// Host-side checks of a host-buffer batch: offsets must be monotone and start
+// at 0 (a kernel must never index out of bounds).
+static int check_host_batch(lb_ctx* ctx, const lb_request_batch* b) {
   const uint32_t nr = b->n_requests, ns = b->n_sets;
-  if (nr == 0) {
-    if (stats) *stats = lb_verify_stats{0, 0, 0.0};
-    return LB_OK;
-  }
-  // validate offsets on the host (a kernel must never index out of bounds)
   if (b->request_offsets[0] != 0 || b->request_offsets[nr] != ns) {
     ctx->err = "request_offsets must start at 0 and end at n_sets";
     return LB_ERR_INVALID_ARGUMENT;
@@ -619,9 +728,7 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
       ctx->err = "sig_offsets not monotone";
       return LB_ERR_INVALID_ARGUMENT;
     }
-  std::vector<uint32_t> pk_off_local;
-  const uint32_t* pk_off = b->pk_offsets;
-  if (pk_off) {
+  if (const uint32_t* pk_off = b->pk_offsets) {
     if (pk_off[0] != 0) {
       ctx->err = "pk_offsets must start at 0";
       return LB_ERR_INVALID_ARGUMENT;
@@ -632,18 +739,26 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
         return LB_ERR_INVALID_ARGUMENT;
       }
   }
+  return LB_OK;
+}
+
+// Host-buffer call on slot `sl`: inputs staged through the slot's pinned
+// buffer (one H2D copy), the pipeline, verdicts copied back into pinned memory
+// on the slot's stream and into the caller's buffers when the call retires.
+static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
+                       uint8_t* out_set_status, bool partial, uint64_t* out_ticket) {
+  const uint32_t nr = b->n_requests, ns = b->n_sets;
+  LB_TRY(check_host_batch(ctx, b));
+  const uint32_t* pk_off = b->pk_offsets;
   const size_t n_pk = pk_off ? pk_off[ns] : ns;
   const bool by_index = b->pubkey_indices != nullptr;
   const size_t sig_bytes = b->sig_offsets[ns];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = pk_off ? sizeof(uint32_t) * (ns + 1) : 0,
-               sz_pk = n_pk * (by_index ? sizeof(uint32_t) : 96), sz_msg = (size_t)ns * 32, sz_sigo = sizeof(uint32_t) * (ns + 1),
-               sz_sig = sig_bytes, sz_seed = 32;
+               sz_pk = n_pk * (by_index ? sizeof(uint32_t) : 96), sz_msg = (size_t)ns * 32,
+               sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = sig_bytes, sz_seed = 32;
   const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
-  const size_t out_bytes = al(nr) * 2 + al(ns ? ns : 1);
-  Slot& sl = ctx->slots[0];  // synchronous host API: slot 0 (two-stream DAG)
-  BorrowGuard g{ctx};
-  LB_TRY(borrow_second_stream(ctx, g));
+  const size_t out_bytes = al(nr ? nr : 1) * 2 + al(ns ? ns : 1);
   LB_TRY(finish_slot(ctx, sl));
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
   LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
@@ -662,10 +777,20 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   stage(b->signatures, sz_sig);
   stage(b->seed, sz_seed);
   char* d_in = ws.take<char>(in_bytes);
-  uint8_t* d_valid = ws.take<uint8_t>(nr);
-  uint8_t* d_err = ws.take<uint8_t>(nr);
+  uint8_t* d_valid = ws.take<uint8_t>(nr ? nr : 1);
+  uint8_t* d_err = ws.take<uint8_t>(nr ? nr : 1);
   uint8_t* d_sst = ws.take<uint8_t>(ns ? ns : 1);
+  uint8_t* d_partial = partial ? ws.take<uint8_t>(LB_GT_BYTES) : nullptr;
   LB_TRY(begin_call(ctx, sl));
+  sl.dv_valid = d_valid;
+  sl.dv_err = d_err;
+  sl.dv_sst = d_sst;
+  sl.h_out = h + in_bytes;
+  sl.out_valid = out_valid;
+  sl.out_err = out_req_err;
+  sl.out_sst = out_set_status;
+  sl.out_nr = nr;
+  sl.out_ns = out_set_status ? ns : 0;
   LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
   size_t o = 0;
   auto dptr = [&](size_t n) {
@@ -680,25 +805,167 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
   const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
   const uint8_t* d_sig = (const uint8_t*)dptr(sz_sig);
   const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
-  LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? nullptr : d_pks, d_pko,
-                      by_index ? (const uint32_t*)d_pks : nullptr, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst, ws));
-  char* h_out = h + in_bytes;
-  LB_HIP(hipMemcpyAsync(h_out, d_valid, nr, hipMemcpyDeviceToHost, sl.st[0]));
-  LB_HIP(hipMemcpyAsync(h_out + al(nr), d_err, nr, hipMemcpyDeviceToHost, sl.st[0]));
-  if (ns) LB_HIP(hipMemcpyAsync(h_out + 2 * al(nr), d_sst, ns, hipMemcpyDeviceToHost, sl.st[0]));
-  LB_TRY(end_call_async(ctx, sl));
-  LB_TRY(finish_slot(ctx, sl));
-  memcpy(out_valid, h_out, nr);
-  memcpy(out_req_err, h_out + al(nr), nr);
-  if (out_set_status && ns) memcpy(out_set_status, h_out + 2 * al(nr), ns);
-  if (stats) {
-    stats->batch_retries = ctx->batch_retries;
-    stats->batch_sigs_success = ctx->batch_sigs_success;
-    stats->device_ms = ctx->wall_ms;
+  if (nr) {
+    LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? nullptr : d_pks, d_pko,
+                        by_index ? (const uint32_t*)d_pks : nullptr, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst,
+                        ws, d_partial));
+  } else if (partial) {
+    memset(sl.h_partial, 0, LB_GT_BYTES);
+    sl.h_partial[47] = 1;
+    LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
+    sl.ps = PipeState{};
+    sl.partial_pending = true;
   }
+  LB_TRY(end_call_async(ctx, sl));
+  *out_ticket = sl.ticket;
   return LB_OK;
 }
 
+static void fill_stats(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
+  if (!stats) return;
+  const TicketStats& ts = ctx->tstats[ticket % lb_ctx::kTicketRing];
+  if (ts.ticket == ticket) {
+    stats->batch_retries = ts.batch_retries;
+    stats->batch_sigs_success = ts.batch_sigs_success;
+    stats->device_ms = ts.wall_ms;
+  } else {  // more than kTicketRing calls retired since: the stats are gone
+    *stats = lb_verify_stats{0, 0, 0.0};
+  }
+}
+
+Slot& next_async_slot(lb_ctx* ctx) {
+  Slot& sl = ctx->slots[ctx->next_slot];
+  ctx->next_slot = (ctx->next_slot + 1) % ctx->n_slots;
+  return sl;
+}
+
+int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
+                                    uint8_t* d_set_status, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  return submit_device(ctx, next_async_slot(ctx), b, d_valid, d_req_err, d_set_status, false, out_ticket);
+}
+
+int lb_verify_requests_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
+                             uint8_t* out_set_status, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  return submit_host(ctx, next_async_slot(ctx), b, out_valid, out_req_err, out_set_status, false, out_ticket);
+}
+
+int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* b, uint32_t flags, uint8_t* out_valid,
+                                     uint8_t* out_req_err, uint8_t* out_set_status, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot& sl = next_async_slot(ctx);
+  if (flags & LB_BATCH_DEVICE)
+    return submit_device(ctx, sl, b, out_valid, out_req_err, out_set_status, true, out_ticket);
+  return submit_host(ctx, sl, b, out_valid, out_req_err, out_set_status, true, out_ticket);
+}
+
+int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576) {
+  if (!ctx || !out576) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot* sl = slot_of_ticket(ctx, ticket);
+  if (!sl || !sl->partial_pending) {
+    ctx->err = "ticket is not a pending two-phase call";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  LB_HIP(hipEventSynchronize(sl->partial_ev));
+  memcpy(out576, sl->h_partial, LB_GT_BYTES);
+  return LB_OK;
+}
+
+int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot* sl = slot_of_ticket(ctx, ticket);
+  if (!sl || !sl->partial_pending) {
+    ctx->err = "ticket is not a pending two-phase call";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  return finish_partial(ctx, *sl, merged_ok != 0);
+}
+
+int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* out_is_one) {
+  if (!ctx || !out_is_one || (n && !partials576)) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  const size_t need = (size_t)n * LB_GT_BYTES + 256;
+  if (need > ctx->aux_cap) {
+    LB_HIP(hipStreamSynchronize(ctx->aux_stream));
+    if (ctx->d_aux) LB_HIP(hipFree(ctx->d_aux));
+    if (ctx->h_aux) LB_HIP(hipHostFree(ctx->h_aux));
+    ctx->d_aux = nullptr;
+    ctx->h_aux = nullptr;
+    ctx->aux_cap = 0;
+    const size_t cap = need < 16 * LB_GT_BYTES + 256 ? 16 * LB_GT_BYTES + 256 : need;
+    if (hipMalloc(&ctx->d_aux, cap) != hipSuccess || hipHostMalloc(&ctx->h_aux, cap, hipHostMallocDefault) != hipSuccess) {
+      ctx->err = "gt_check buffers";
+      return LB_ERR_OUT_OF_MEMORY;
+    }
+    ctx->aux_cap = cap;
+  }
+  uint8_t* d_out = ctx->d_aux;
+  uint8_t* d_in = ctx->d_aux + 256;
+  if (n) {
+    memcpy(ctx->h_aux + 256, partials576, (size_t)n * LB_GT_BYTES);
+    LB_HIP(hipMemcpyAsync(d_in, ctx->h_aux + 256, (size_t)n * LB_GT_BYTES, hipMemcpyHostToDevice, ctx->aux_stream));
+  }
+  hipLaunchKernelGGL(k_gt_check, dim3(1), dim3(TPB), 0, ctx->aux_stream, n, (const uint8_t*)d_in, d_out);
+  LB_HIP(hipGetLastError());
+  LB_HIP(hipMemcpyAsync(ctx->h_aux, d_out, 2, hipMemcpyDeviceToHost, ctx->aux_stream));
+  LB_HIP(hipStreamSynchronize(ctx->aux_stream));
+  if (ctx->h_aux[1]) {
+    ctx->err = "partial with a coefficient >= p";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  *out_is_one = ctx->h_aux[0] ? 1 : 0;
+  return LB_OK;
+}
+
+int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
+  fill_stats(ctx, ticket, stats);
+  return LB_OK;
+}
+
+int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
+                              uint8_t* d_set_status, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  uint64_t t = 0;
+  BorrowGuard g{ctx};
+  LB_TRY(borrow_second_stream(ctx, g));
+  LB_TRY(submit_device(ctx, ctx->slots[0], b, d_valid, d_req_err, d_set_status, false, &t));  // slot 0: DAG
+  return lb_wait(ctx, t, stats);
+}
+
+int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
+                       uint8_t* out_set_status, lb_verify_stats* stats) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  if (b->n_requests == 0) {
+    if (stats) *stats = lb_verify_stats{0, 0, 0.0};
+    return LB_OK;
+  }
+  uint64_t t = 0;
+  BorrowGuard g{ctx};  // synchronous host API: slot 0 (two-stream DAG, lowest latency)
+  LB_TRY(borrow_second_stream(ctx, g));
+  LB_TRY(submit_host(ctx, ctx->slots[0], b, out_valid, out_req_err, out_set_status, false, &t));
+  return lb_wait(ctx, t, stats);
+}
 // ---- helpers for small host-buffer calls ----------------------------------
 static int upload(lb_ctx* ctx, Bump& ws, const void* src, size_t n, void** out) {
   char* d = ws.take<char>(n ? n : 1);
@@ -983,61 +1250,202 @@ int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const 
   return LB_OK;
 }
 
+// Same-message jobs, batched (BlsMultiThreadWorkerPool.verifySignatureSetsSameMessage
+// jobs: jobItemWorkReq sameMessage, jobItem.ts:64-86, the worker's verify of
+// the aggregated set, index.ts:455-489, and the per-set retry of failed jobs,
+// index.ts:473-484,557-568 / jobItemSameMessageToMultiSet, jobItem.ts:93-125).
+// One device pass for all jobs: every signature decoded + validated ONCE,
+// pubkeys and signatures summed per job, and every job's aggregated set verified
+// as a 1-set request of ONE merged call; only the sets of failed jobs are then
+// re-verified, each alone, in one more call.
+int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* b, uint8_t* out_valid,
+                                 uint8_t* out_job_fast, lb_verify_stats* stats) {
+  if (!ctx || !b || (b->n_sets && !out_valid)) return LB_ERR_INVALID_ARGUMENT;
+  const uint32_t nj = b->n_jobs, ns = b->n_sets;
+  if (stats) *stats = lb_verify_stats{0, 0, 0.0};
+  if (nj == 0) return LB_OK;
+  if (!b->job_offsets || !b->sig_offsets || !b->messages || !b->seed || (ns && !b->signatures) ||
+      (ns && !b->pubkeys && !b->pubkey_indices)) {
+    ctx->err = "null pointer in lb_same_message_batch";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  if (b->job_offsets[0] != 0 || b->job_offsets[nj] != ns || b->sig_offsets[0] != 0) {
+    ctx->err = "job_offsets / sig_offsets must start at 0 (job_offsets end at n_sets)";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  for (uint32_t j = 0; j < nj; j++)
+    if (b->job_offsets[j + 1] < b->job_offsets[j]) {
+      ctx->err = "job_offsets not monotone";
+      return LB_ERR_INVALID_ARGUMENT;
+    }
+  for (uint32_t i = 0; i < ns; i++)
+    if (b->sig_offsets[i + 1] < b->sig_offsets[i]) {
+      ctx->err = "sig_offsets not monotone";
+      return LB_ERR_INVALID_ARGUMENT;
+    }
+  LB_HIP(hipSetDevice(ctx->device));
+  const bool by_index = b->pubkey_indices != nullptr;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t sz_joff = sizeof(uint32_t) * (nj + 1), sz_pk = (size_t)ns * (by_index ? 4 : 96),
+               sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = b->sig_offsets[ns], sz_msg = (size_t)nj * 32,
+               sz_seed = 32, sz_areq = sizeof(uint32_t) * (nj + 1), sz_asig = sizeof(uint32_t) * (nj + 1);
+  const size_t in_bytes =
+      al(sz_joff) + al(sz_pk) + al(sz_sigo) + al(sz_sig) + al(sz_msg) + al(sz_seed) + al(sz_areq) + al(sz_asig);
+  const size_t out_bytes = 4 * al(nj);
+  const size_t ns1 = ns ? ns : 1;
+  const size_t extra = ns1 * (sizeof(g2j) + 1) + (size_t)nj * (sizeof(g1j) + 1 + 96 + 192 + 1 + 2) + 16 * 256;
+  std::vector<uint8_t> fast(nj);
+  {
+    BorrowGuard g{ctx};  // slot 0, two-stream DAG
+    LB_TRY(borrow_second_stream(ctx, g));
+    Slot& sl = ctx->slots[0];
+    LB_TRY(finish_slot(ctx, sl));
+    LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
+    LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj)));
+    Bump ws{sl.d_ws, 0, sl.ws_cap};
+    char* h = sl.h_pin;
+    size_t ho = 0;
+    auto stage = [&](const void* src, size_t n) {
+      char* p = h + ho;
+      if (n && src) memcpy(p, src, n);
+      ho += al(n);
+      return p;
+    };
+    stage(b->job_offsets, sz_joff);
+    stage(by_index ? (const void*)b->pubkey_indices : (const void*)b->pubkeys, sz_pk);
+    stage(b->sig_offsets, sz_sigo);
+    stage(b->signatures, sz_sig);
+    stage(b->messages, sz_msg);
+    stage(b->seed, sz_seed);
+    uint32_t* areq = (uint32_t*)stage(nullptr, sz_areq);
+    uint32_t* asig = (uint32_t*)stage(nullptr, sz_asig);
+    for (uint32_t j = 0; j <= nj; j++) {
+      areq[j] = j;        // every job one request of one (aggregated) set
+      asig[j] = 192 * j;  // Signature.aggregate(...).toBytes(uncompressed)
+    }
+    char* d_in = ws.take<char>(in_bytes);
+    size_t o = 0;
+    auto dptr = [&](size_t n) {
+      char* p = d_in + o;
+      o += al(n);
+      return p;
+    };
+    const uint32_t* d_joff = (const uint32_t*)dptr(sz_joff);
+    const uint8_t* d_pks = (const uint8_t*)dptr(sz_pk);
+    const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
+    const uint8_t* d_sigs = (const uint8_t*)dptr(sz_sig);
+    const uint8_t* d_msgs = (const uint8_t*)dptr(sz_msg);
+    const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
+    const uint32_t* d_areq = (const uint32_t*)dptr(sz_areq);
+    const uint32_t* d_asig = (const uint32_t*)dptr(sz_asig);
+    g2j* d_sig = ws.take<g2j>(ns1);
+    uint8_t* d_sst = ws.take<uint8_t>(ns1);
+    g1j* d_jpk = ws.take<g1j>(nj);
+    uint8_t* d_jpkst = ws.take<uint8_t>(nj);
+    uint8_t* d_pk96 = ws.take<uint8_t>((size_t)nj * 96);
+    uint8_t* d_sig192 = ws.take<uint8_t>((size_t)nj * 192);
+    uint8_t* d_jbad = ws.take<uint8_t>(nj);
+    uint8_t* d_valid = ws.take<uint8_t>(nj);
+    uint8_t* d_err = ws.take<uint8_t>(nj);
+    LB_TRY(begin_call(ctx, sl));
+    LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
+    if (ns)
+      LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
+               d_sst);
+    const PkSource src{by_index ? nullptr : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
+                       ctx->table_n};
+    const uint32_t agg_grid = nj < 16384u ? nj : 16384u;
+    LB_STAGE("sm_pubkeys", 0, k_pubkeys_single, blocks_for(nj), TPB, nj, src, d_joff, d_jpk, d_jpkst);
+    LB_STAGE("sm_pubkeys_agg", 0, k_pubkeys_agg, agg_grid, TPB, nj, src, d_joff, d_jpk, d_jpkst);
+    LB_STAGE("sm_aggregate", 0, k_same_message_agg, agg_grid, TPB, nj, d_joff, (const g2j*)d_sig,
+             (const uint8_t*)d_sst, (const g1j*)d_jpk, d_pk96, d_sig192, d_jbad);
+    LB_TRY(run_pipeline(ctx, sl, nj, nj, d_areq, d_pk96, nullptr, nullptr, d_msgs, d_sig192, d_asig, d_seed, d_valid,
+                        d_err, nullptr, ws));
+    char* h_out = h + in_bytes;
+    LB_HIP(hipMemcpyAsync(h_out, d_valid, nj, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_HIP(hipMemcpyAsync(h_out + al(nj), d_err, nj, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_HIP(hipMemcpyAsync(h_out + 2 * al(nj), d_jbad, nj, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_HIP(hipMemcpyAsync(h_out + 3 * al(nj), d_jpkst, nj, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_TRY(end_call_async(ctx, sl));
+    LB_TRY(finish_slot(ctx, sl));
+    if (stats) stats->device_ms = ctx->wall_ms;
+    // fast path per job: aggregated set valid, every signature validated, pubkeys aggregated
+    const uint8_t *v = (const uint8_t*)h_out, *e = v + al(nj), *jb = v + 2 * al(nj), *pst = v + 3 * al(nj);
+    for (uint32_t j = 0; j < nj; j++) fast[j] = v[j] && e[j] == LB_REQ_OK && !jb[j] && pst[j] == LB_ST_OK;
+    for (uint32_t j = 0; j < nj; j++) {
+      if (out_job_fast) out_job_fast[j] = fast[j];
+      if (fast[j])
+        for (uint32_t i = b->job_offsets[j]; i < b->job_offsets[j + 1]; i++) out_valid[i] = 1;
+    }
+    uint32_t fast_sets = 0, retried_jobs = 0;
+    for (uint32_t j = 0; j < nj; j++) {
+      const uint32_t n_j = b->job_offsets[j + 1] - b->job_offsets[j];
+      if (fast[j])
+        fast_sets += n_j;
+      else if (n_j)
+        retried_jobs++;
+    }
+    if (stats) {
+      stats->batch_retries = retried_jobs;
+      stats->batch_sigs_success = fast_sets;
+    }
+    if (retried_jobs == 0) return LB_OK;
+  }
+  // per-set retry of the failed jobs: every set its own (non-batchable) 1-set request
+  std::vector<uint32_t> fs;
+  std::vector<uint32_t> req_off{0}, sig_off{0}, idx;
+  std::vector<uint8_t> pks, sigs, msgs;
+  for (uint32_t j = 0; j < nj; j++) {
+    if (fast[j]) continue;
+    for (uint32_t i = b->job_offsets[j]; i < b->job_offsets[j + 1]; i++) {
+      fs.push_back(i);
+      req_off.push_back((uint32_t)fs.size());
+      if (by_index)
+        idx.push_back(b->pubkey_indices[i]);
+      else
+        pks.insert(pks.end(), b->pubkeys + (size_t)i * 96, b->pubkeys + (size_t)i * 96 + 96);
+      sigs.insert(sigs.end(), b->signatures + b->sig_offsets[i], b->signatures + b->sig_offsets[i + 1]);
+      sig_off.push_back((uint32_t)sigs.size());
+      msgs.insert(msgs.end(), b->messages + (size_t)j * 32, b->messages + (size_t)j * 32 + 32);
+    }
+  }
+  if (fs.empty()) return LB_OK;
+  if (sigs.empty()) sigs.push_back(0);
+  lb_request_batch rb{};
+  rb.n_requests = (uint32_t)fs.size();
+  rb.n_sets = (uint32_t)fs.size();
+  rb.request_offsets = req_off.data();
+  rb.pubkeys = by_index ? nullptr : pks.data();
+  rb.pubkey_indices = by_index ? idx.data() : nullptr;
+  rb.messages = msgs.data();
+  rb.signatures = sigs.data();
+  rb.sig_offsets = sig_off.data();
+  rb.seed = b->seed;
+  std::vector<uint8_t> rv(fs.size()), re(fs.size());
+  LB_TRY(lb_verify_requests(ctx, &rb, rv.data(), re.data(), nullptr, nullptr));
+  for (size_t k = 0; k < fs.size(); k++) out_valid[fs[k]] = (rv[k] && re[k] == LB_REQ_OK) ? 1 : 0;
+  return LB_OK;
+}
+
 int lb_verify_same_message(lb_ctx* ctx, uint32_t n, const uint8_t* pks, const uint8_t* sigs, const uint32_t* sig_off,
                            const uint8_t* message, const uint8_t* seed, uint8_t* out_valid,
                            uint32_t* out_used_fast_path) {
   if (!ctx || (n && (!pks || !sigs || !sig_off || !message || !seed || !out_valid))) return LB_ERR_INVALID_ARGUMENT;
   if (out_used_fast_path) *out_used_fast_path = 0;
   if (n == 0) return LB_OK;
-  // 1. validate-deserialize every signature (jobItemWorkReq sameMessage, jobItem.ts:72-74)
-  std::vector<uint8_t> st(n);
-  LB_TRY(lb_decode_signatures(ctx, n, sigs, sig_off, st.data(), nullptr));
-  bool all_ok = true;
-  for (uint32_t i = 0; i < n; i++) all_ok &= (st[i] == LB_ST_OK);
-  if (all_ok) {
-    // 2. aggregate pubkeys and signatures (plain sums, no randomness) and
-    //    verify once: worker maybeBatch with one set (index.ts:455-489)
-    uint8_t agg_pk[96], agg_sig[192];
-    uint8_t pst = 0;
-    int32_t bad = -1;
-    LB_TRY(lb_aggregate_pubkeys(ctx, n, pks, agg_pk, &pst));
-    LB_TRY(lb_aggregate_signatures(ctx, n, sigs, sig_off, agg_sig, &bad));
-    uint32_t req_off[2] = {0, 1}, so[2] = {0, 192};
-    lb_request_batch b{};
-    b.n_requests = 1;
-    b.n_sets = 1;
-    b.request_offsets = req_off;
-    b.pubkeys = agg_pk;
-    b.messages = message;
-    b.signatures = agg_sig;
-    b.sig_offsets = so;
-    b.seed = seed;
-    uint8_t valid = 0, err = 0;
-    LB_TRY(lb_verify_requests(ctx, &b, &valid, &err, nullptr, nullptr));
-    if (valid && err == LB_REQ_OK && pst == LB_ST_OK) {
-      for (uint32_t i = 0; i < n; i++) out_valid[i] = 1;
-      if (out_used_fast_path) *out_used_fast_path = 1;
-      return LB_OK;
-    }
-  }
-  // 3. retry every set alone (jobItemSameMessageToMultiSet, jobItem.ts:93-125)
-  std::vector<uint32_t> req_off(n + 1);
-  for (uint32_t i = 0; i <= n; i++) req_off[i] = i;
-  std::vector<uint8_t> msgs((size_t)n * 32);
-  for (uint32_t i = 0; i < n; i++) memcpy(&msgs[(size_t)i * 32], message, 32);
-  lb_request_batch b{};
-  b.n_requests = n;
+  const uint32_t job_off[2] = {0, n};
+  lb_same_message_batch b{};
+  b.n_jobs = 1;
   b.n_sets = n;
-  b.request_offsets = req_off.data();
+  b.job_offsets = job_off;
   b.pubkeys = pks;
-  b.messages = msgs.data();
   b.signatures = sigs;
   b.sig_offsets = sig_off;
+  b.messages = message;
   b.seed = seed;
-  std::vector<uint8_t> err(n);
-  LB_TRY(lb_verify_requests(ctx, &b, out_valid, err.data(), nullptr, nullptr));
-  for (uint32_t i = 0; i < n; i++)
-    if (err[i] != LB_REQ_OK) out_valid[i] = 0;
+  uint8_t fast = 0;
+  LB_TRY(lb_verify_same_message_batch(ctx, &b, out_valid, &fast, nullptr));
+  if (out_used_fast_path) *out_used_fast_path = fast;
   return LB_OK;
 }
 

@@ -154,6 +154,17 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
 __global__ void __launch_bounds__(TPB) k_merge_stats(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                      const uint8_t* __restrict__ req_bad,
                                                      const uint8_t* __restrict__ mflag, uint32_t* __restrict__ out);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_partial(uint32_t n_pairs, uint32_t base,
+                                                          const uint32_t* __restrict__ lines,
+                                                          const fp12* __restrict__ F_all, uint8_t* __restrict__ out576);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_check(uint32_t n, const uint8_t* __restrict__ in576,
+                                                           uint8_t* __restrict__ out);
+__global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
+                                                          const g2j* __restrict__ sig,
+                                                          const uint8_t* __restrict__ sig_status,
+                                                          const g1j* __restrict__ job_pk, uint8_t* __restrict__ out_pk96,
+                                                          uint8_t* __restrict__ out_sig192,
+                                                          uint8_t* __restrict__ job_bad);
 __global__ void __launch_bounds__(TPB) k_signing_root_att(uint32_t n, const uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ domains, uint32_t dstride,
                                                           uint8_t* __restrict__ out);

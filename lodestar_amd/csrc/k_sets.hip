@@ -102,4 +102,66 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource p
   }
 }
 
+// Same-message jobs (jobItemWorkReq sameMessage, chain/bls/multithread/jobItem.ts:64-86):
+// one wave per job j sums the job's validated signatures (decoded ONCE by
+// k_decode_sigs) and writes the aggregate's 192-byte uncompressed encoding
+// (Signature.aggregate(sigs).toBytes(uncompressed)) and the aggregated pubkey's
+// 96-byte encoding as the inputs of a 1-set request.  A job with any signature
+// that failed Signature.fromBytes(validate=true) would have thrown on the main
+// thread (-> per-set retry, index.ts:411-414): its aggregate is written as an
+// invalid encoding (all zero bytes: compression flag clear, infinity flag clear
+// -> BAD_ENCODING), so its request is false, and job_bad[j] = 1.
+__global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
+                                                          const g2j* __restrict__ sig,
+                                                          const uint8_t* __restrict__ sig_status,
+                                                          const g1j* __restrict__ job_pk, uint8_t* __restrict__ out_pk96,
+                                                          uint8_t* __restrict__ out_sig192,
+                                                          uint8_t* __restrict__ job_bad) {
+  __shared__ g2j sh[TPB];
+  __shared__ uint32_t bad;
+  for (uint32_t j = blockIdx.x; j < n_jobs; j += gridDim.x) {
+    const uint32_t a = job_off[j], b = job_off[j + 1];
+    if (threadIdx.x == 0) bad = (a == b) ? 1u : 0u;
+    __syncthreads();
+    g2j acc;
+    jac_set_inf(acc);
+    for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
+      if (sig_status[i] != LB_ST_OK) {
+        atomicOr(&bad, 1u);
+      } else {
+        g2j t = sig[i];
+        jac_add(acc, acc, t);
+      }
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = TPB / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
+        g2j o = sh[threadIdx.x + s];
+        g2j m = sh[threadIdx.x];
+        jac_add(m, m, o);
+        sh[threadIdx.x] = m;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      uint8_t* os = out_sig192 + (size_t)j * 192;
+      if (bad) {
+        for (int k = 0; k < 192; k++) os[k] = 0;
+      } else {
+        g2j tot = sh[0];
+        g2a s;
+        jac_to_aff(s, tot);
+        g2_serialize(os, s);
+      }
+      g1j p = job_pk[j];
+      g1a pa;
+      jac_to_aff(pa, p);
+      g1_serialize(out_pk96 + (size_t)j * 96, pa);
+      job_bad[j] = bad ? 1 : 0;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace lb

@@ -86,6 +86,53 @@ __global__ void __launch_bounds__(TPB) k_merge_stats(uint32_t n_req, const uint3
   }
 }
 
+// Partial of a call for the multi-GPU combine (north_star): the
+// call's merged Miller product P = F_all * Miller(-g1, S_all) BEFORE the final
+// exponentiation, as 576 bytes (12 big-endian canonical Fp coefficients,
+// c0.c0.c0 ... c1.c2.c1, the lb_pairing order).  The host multiplies the
+// partials of all GPUs and checks final_exp(prod) == 1 once (k_gt_check).
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_partial(uint32_t n_pairs, uint32_t base,
+                                                          const uint32_t* __restrict__ lines,
+                                                          const fp12* __restrict__ F_all, uint8_t* __restrict__ out576) {
+  __shared__ wc_smem S;
+  wc_init_tables(S);
+  wc_miller_from_lines(S, WC_FS, lines, n_pairs, base);
+  wc_load12(S, WC_F, F_all[0]);
+  wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
+  if (threadIdx.x < 12) fp_write_be(out576 + 48 * threadIdx.x, S.slot[WC_F][threadIdx.x]);
+}
+
+// out[0] = 1 iff final_exp(prod_i partial_i) == 1 for n partials of 576 bytes
+// (the host-side combine of the per-GPU partials; one wave).  A coefficient
+// that is not < p makes the product invalid (out[0] = 0, out[1] = 1).
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_check(uint32_t n, const uint8_t* __restrict__ in576,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ wc_smem S;
+  __shared__ uint32_t bad;
+  if (threadIdx.x == 0) bad = 0;
+  wc_init_tables(S);
+  wc_init_gammas(S);
+  wc_set_one(S, WC_ACC);
+  for (uint32_t i = 0; i < n; i++) {
+    if (threadIdx.x < 12) {
+      fp v;
+      if (!fp_read_masked(v, in576 + (size_t)i * 576 + 48 * threadIdx.x, false)) {
+        atomicOr(&bad, 1u);
+        fp_zero(v);
+      }
+      S.slot[WC_B][threadIdx.x] = v;
+    }
+    __syncthreads();
+    wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_B);
+  }
+  wc_copy(S, WC_C, WC_ACC);
+  wc_final_exp(S, WC_F, WC_C);
+  if (threadIdx.x == 0) {
+    out[0] = (!bad && wc_is_one(S, WC_F)) ? 1 : 0;
+    out[1] = bad ? 1 : 0;
+  }
+}
+
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,

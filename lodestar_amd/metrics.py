@@ -35,6 +35,12 @@ TIME_PER_SIG_SET = "lodestar_bls_worker_thread_time_per_sigset_seconds"  # histo
 TOTAL_SIG_SETS = P + "sig_sets_total"
 PRIORITIZED_SIG_SETS = P + "prioritized_sig_sets_total"
 BATCHABLE_SIG_SETS = P + "batchable_sig_sets_total"
+LATENCY_TO_WORKER = P + "latency_to_worker"                    # histogram (dispatch -> GPU submission thread)
+LATENCY_FROM_WORKER = P + "latency_from_worker"                # histogram (verdicts ready -> event loop)
+SIG_DESERIALIZATION_MAIN_THREAD = P + "signature_deserialization_main_thread_time_seconds"  # GPU decode stage
+PUBKEYS_AGGREGATION_MAIN_THREAD = P + "pubkeys_aggregation_main_thread_time_seconds"      # GPU aggregation stage
+SINGLE_THREAD_TIME = "lodestar_bls_single_thread_time_seconds"                  # histogram
+SINGLE_THREAD_TIME_PER_SIGSET = "lodestar_bls_single_thread_time_per_sigset_seconds"  # histogram
 
 
 class BlsPoolMetrics:

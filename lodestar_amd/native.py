@@ -37,8 +37,12 @@ EXPORTED_SYMBOLS = (
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
     "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
-    "lb_signing_roots_attestation_device",
+    "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
+    "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
 )
+
+LB_BATCH_DEVICE = 1
+LB_GT_BYTES = 576
 
 
 class LodestarBlsError(RuntimeError):
@@ -75,6 +79,20 @@ class _RequestBatch(ctypes.Structure):
     ]
 
 
+class _SameMessageBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_jobs", ctypes.c_uint32),
+        ("n_sets", ctypes.c_uint32),
+        ("job_offsets", ctypes.c_void_p),
+        ("pubkeys", ctypes.c_void_p),
+        ("pubkey_indices", ctypes.c_void_p),
+        ("signatures", ctypes.c_void_p),
+        ("sig_offsets", ctypes.c_void_p),
+        ("messages", ctypes.c_void_p),
+        ("seed", ctypes.c_void_p),
+    ]
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("batch_retries", ctypes.c_uint32), ("batch_sigs_success", ctypes.c_uint32),
                 ("device_ms", ctypes.c_double)]
@@ -89,6 +107,16 @@ def load_library() -> ctypes.CDLL:
     if _lib is not None:
         return _lib
     path = library_path()
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, and
+    # when /opt/rocm's is loaded first (by this library) torch's HIP
+    # initialisation fails later in the same process ("No HIP GPUs are
+    # available").  Loading torch first makes both share torch's runtime, the
+    # order bench.py and the tests use.
+    if os.environ.get("LB_NO_TORCH_PRELOAD") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(path):
         raise LodestarBlsError(
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
@@ -113,6 +141,15 @@ def load_library() -> ctypes.CDLL:
     lib.lb_verify_requests_device_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_Stats)]
+    lib.lb_verify_requests_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
+                                             ctypes.POINTER(ctypes.c_uint64)]
+    lib.lb_verify_requests_partial_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), u32, vp, vp, vp,
+                                                     ctypes.POINTER(ctypes.c_uint64)]
+    lib.lb_partial_wait.argtypes = [vp, ctypes.c_uint64, vp]
+    lib.lb_gt_check.argtypes = [vp, u32, vp, ctypes.POINTER(ctypes.c_int32)]
+    lib.lb_verify_requests_finish.argtypes = [vp, ctypes.c_uint64, i32]
+    lib.lb_verify_same_message_batch.argtypes = [vp, ctypes.POINTER(_SameMessageBatch), vp, vp,
+                                                 ctypes.POINTER(_Stats)]
     lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
     lib.lb_pubkey_table_append.argtypes = [vp, u32, vp, u32, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_pubkey_table_size.argtypes = [vp, ctypes.POINTER(u32)]
@@ -161,6 +198,20 @@ class VerifyResult:
     batch_sigs_success: int = 0  # worker.ts:71 (sets verified inside a passing merged check)
 
 
+@dataclass
+class PendingCall:
+    """An enqueued host-buffer call: its ticket, the output arrays the library
+    fills when the call retires and the input arrays it reads until then."""
+    ticket: int
+    n_req: int
+    n_sets: int
+    valid: np.ndarray
+    err: np.ndarray
+    sst: np.ndarray
+    keep: object
+    partial: bool = False
+
+
 class Device:
     """One lb_ctx bound to one GPU (one per process per GPU)."""
 
@@ -191,35 +242,133 @@ class Device:
             raise LodestarBlsError(f"{what} failed ({rc}): {msg}")
 
     # -- hot path ------------------------------------------------------------
-    def verify_requests(self, request_offsets: np.ndarray, pubkeys: np.ndarray, pk_offsets: Optional[np.ndarray],
-                        messages: np.ndarray, sig_blob: np.ndarray, sig_offsets: np.ndarray, seed: bytes,
-                        batchable: Optional[np.ndarray] = None,
-                        pk_indices: Optional[np.ndarray] = None) -> VerifyResult:
-        """pk_indices (u32 validator indices into the device pubkey table) replaces pubkeys when given."""
+    @staticmethod
+    def _host_batch(request_offsets, pubkeys, pk_offsets, messages, sig_blob, sig_offsets, seed, batchable=None,
+                    pk_indices=None):
+        """(batch struct, arrays it points into, n_req, n_sets) for a host-buffer call."""
         request_offsets = np.ascontiguousarray(request_offsets, dtype=np.uint32)
         n_req = len(request_offsets) - 1
         n_sets = int(request_offsets[-1]) if n_req >= 0 else 0
         pubkeys = _u8(pubkeys) if pubkeys is not None and len(pubkeys) else np.zeros(1, np.uint8)
         messages = _u8(messages) if len(messages) else np.zeros(1, np.uint8)
+        if len(messages) < 32 * n_sets:
+            raise ValueError(f"messages: {len(messages)} bytes for {n_sets} sets (32 bytes each)")
         sig_blob = _u8(sig_blob) if len(sig_blob) else np.zeros(1, np.uint8)
         sig_offsets = np.ascontiguousarray(sig_offsets, dtype=np.uint32)
+        if len(sig_offsets) != n_sets + 1:
+            raise ValueError("sig_offsets must have n_sets + 1 entries")
         pk_offsets = None if pk_offsets is None else np.ascontiguousarray(pk_offsets, dtype=np.uint32)
+        if batchable is not None:
+            batchable = np.ascontiguousarray(batchable, dtype=np.uint8)
         seed_a = _u8(seed)
-        assert len(seed_a) == 32
+        if len(seed_a) != 32:
+            raise ValueError("seed must be 32 bytes")
         if pk_indices is not None:
             pk_indices = np.ascontiguousarray(pk_indices, dtype=np.uint32)
             if len(pk_indices) == 0:
                 pk_indices = np.zeros(1, np.uint32)
         b = _RequestBatch(n_req, n_sets, _ptr(request_offsets), _ptr(batchable), _ptr(pubkeys), _ptr(pk_offsets),
                           _ptr(messages), _ptr(sig_blob), _ptr(sig_offsets), _ptr(seed_a), _ptr(pk_indices))
+        keep = (request_offsets, pubkeys, messages, sig_blob, sig_offsets, pk_offsets, batchable, seed_a, pk_indices)
+        return b, keep, n_req, n_sets
+
+    def verify_requests(self, request_offsets: np.ndarray, pubkeys: np.ndarray, pk_offsets: Optional[np.ndarray],
+                        messages: np.ndarray, sig_blob: np.ndarray, sig_offsets: np.ndarray, seed: bytes,
+                        batchable: Optional[np.ndarray] = None,
+                        pk_indices: Optional[np.ndarray] = None) -> VerifyResult:
+        """pk_indices (u32 validator indices into the device pubkey table) replaces pubkeys when given."""
+        b, keep, n_req, n_sets = self._host_batch(request_offsets, pubkeys, pk_offsets, messages, sig_blob,
+                                                  sig_offsets, seed, batchable, pk_indices)
         valid = np.zeros(max(n_req, 1), np.uint8)
         err = np.zeros(max(n_req, 1), np.uint8)
         sst = np.zeros(max(n_sets, 1), np.uint8)
         st = _Stats()
         rc = self.lib.lb_verify_requests(self._h, ctypes.byref(b), _ptr(valid), _ptr(err), _ptr(sst), ctypes.byref(st))
         self._check(rc, "lb_verify_requests")
+        del keep
         return VerifyResult(valid[:n_req], err[:n_req], sst[:n_sets], st.device_ms, int(st.batch_retries),
                             int(st.batch_sigs_success))
+
+    def verify_requests_async(self, request_offsets, pubkeys, pk_offsets, messages, sig_blob, sig_offsets, seed,
+                              batchable=None, pk_indices=None, partial: bool = False) -> "PendingCall":
+        """lb_verify_requests_async (or the two-phase lb_verify_requests_partial_async):
+        enqueue on the next slot and return at once; wait_call() gives the verdicts."""
+        b, keep, n_req, n_sets = self._host_batch(request_offsets, pubkeys, pk_offsets, messages, sig_blob,
+                                                  sig_offsets, seed, batchable, pk_indices)
+        pc = PendingCall(0, n_req, n_sets, np.zeros(max(n_req, 1), np.uint8), np.zeros(max(n_req, 1), np.uint8),
+                         np.zeros(max(n_sets, 1), np.uint8), keep, partial)
+        t = ctypes.c_uint64(0)
+        if partial:
+            rc = self.lib.lb_verify_requests_partial_async(self._h, ctypes.byref(b), 0, _ptr(pc.valid), _ptr(pc.err),
+                                                           _ptr(pc.sst), ctypes.byref(t))
+            self._check(rc, "lb_verify_requests_partial_async")
+        else:
+            rc = self.lib.lb_verify_requests_async(self._h, ctypes.byref(b), _ptr(pc.valid), _ptr(pc.err),
+                                                   _ptr(pc.sst), ctypes.byref(t))
+            self._check(rc, "lb_verify_requests_async")
+        pc.ticket = int(t.value)
+        return pc
+
+    def wait_call(self, pc: "PendingCall") -> VerifyResult:
+        st = _Stats()
+        self._check(self.lib.lb_wait(self._h, pc.ticket, ctypes.byref(st)), "lb_wait")
+        pc.keep = None
+        return VerifyResult(pc.valid[:pc.n_req], pc.err[:pc.n_req], pc.sst[:pc.n_sets], st.device_ms,
+                            int(st.batch_retries), int(st.batch_sigs_success))
+
+    # -- multi-GPU combine (two-phase calls, SURVEY §8e) ----------------------------
+    def partial_wait(self, pc: "PendingCall") -> bytes:
+        """The shard's merged Miller product (576 bytes) once it is ready."""
+        return self.partial_wait_t(pc.ticket)
+
+    def verify_finish(self, pc: "PendingCall", merged_ok: bool) -> None:
+        self.finish_t(pc.ticket, merged_ok)
+
+    def gt_check(self, partials: Sequence[bytes]) -> bool:
+        """final_exp(prod of the partials) == 1 (the host-side combine, run on this GPU)."""
+        if any(len(p) != LB_GT_BYTES for p in partials):
+            raise ValueError("partials are 576 bytes each")
+        blob = _u8(b"".join(partials)) if partials else np.zeros(1, np.uint8)
+        out = ctypes.c_int32(0)
+        self._check(self.lib.lb_gt_check(self._h, len(partials), _ptr(blob), ctypes.byref(out)), "lb_gt_check")
+        return bool(out.value)
+
+    def verify_same_message_batch(self, jobs: Sequence[Tuple[Sequence, Sequence[bytes], bytes]], seed: bytes,
+                                  by_index: bool = False) -> Tuple[List[List[bool]], List[bool], Tuple[int, int]]:
+        """jobs: (pubkeys, signatures, message) per same-message job; pubkeys are
+        96-byte encodings, or validator indices when by_index.  Returns per-set
+        verdicts per job, the per-job fast-path flags and (retried jobs, sets
+        verified by a passing aggregate)."""
+        nj = len(jobs)
+        if nj == 0:
+            return [], [], (0, 0)
+        job_off = np.zeros(nj + 1, np.uint32)
+        for j, (pks, sigs, msg) in enumerate(jobs):
+            if len(pks) != len(sigs):
+                raise ValueError("one signature per pubkey")
+            if len(msg) != 32:
+                raise ValueError("signing root must be 32 bytes")
+            job_off[j + 1] = job_off[j] + len(pks)
+        ns = int(job_off[-1])
+        all_sigs = [bytes(s) for _, sigs, _ in jobs for s in sigs]
+        blob, offs = pack_blobs(all_sigs)
+        msgs = _u8(b"".join(bytes(m) for _, _, m in jobs))
+        if by_index:
+            idx = np.ascontiguousarray([int(k) for pks, _, _ in jobs for k in pks] or [0], dtype=np.uint32)
+            pk = None
+        else:
+            pk = _u8(b"".join(bytes(k) for pks, _, _ in jobs for k in pks) or b"\0")
+            idx = None
+        sd = _u8(seed)
+        b = _SameMessageBatch(nj, ns, _ptr(job_off), _ptr(pk), _ptr(idx), _ptr(blob), _ptr(offs), _ptr(msgs),
+                              _ptr(sd))
+        out = np.zeros(max(ns, 1), np.uint8)
+        fast = np.zeros(nj, np.uint8)
+        st = _Stats()
+        rc = self.lib.lb_verify_same_message_batch(self._h, ctypes.byref(b), _ptr(out), _ptr(fast), ctypes.byref(st))
+        self._check(rc, "lb_verify_same_message_batch")
+        res = [[bool(x) for x in out[job_off[j]:job_off[j + 1]]] for j in range(nj)]
+        return res, [bool(x) for x in fast], (int(st.batch_retries), int(st.batch_sigs_success))
 
     def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
                                d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,
@@ -236,17 +385,33 @@ class Device:
     def verify_requests_device_async(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int,
                                      d_pk_off: Optional[int], d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int,
                                      d_valid: int, d_err: int, d_set_status: Optional[int] = None,
-                                     d_pk_idx: Optional[int] = None) -> int:
-        """Enqueue; returns a ticket for wait().  All arguments are device pointers."""
+                                     d_pk_idx: Optional[int] = None, partial: bool = False) -> int:
+        """Enqueue; returns a ticket for wait().  All arguments are device pointers.
+        partial=True: the two-phase call (partial_wait_t / finish_t before wait)."""
         b = _RequestBatch(n_req, n_sets, d_req_off, None, d_pubkeys, d_pk_off, d_msgs, d_sigs, d_sig_off, d_seed,
                           d_pk_idx)
         t = ctypes.c_uint64(0)
-        rc = self.lib.lb_verify_requests_device_async(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
-                                                      ctypes.byref(t))
-        self._check(rc, "lb_verify_requests_device_async")
+        if partial:
+            rc = self.lib.lb_verify_requests_partial_async(self._h, ctypes.byref(b), LB_BATCH_DEVICE, d_valid, d_err,
+                                                           d_set_status, ctypes.byref(t))
+            self._check(rc, "lb_verify_requests_partial_async")
+        else:
+            rc = self.lib.lb_verify_requests_device_async(self._h, ctypes.byref(b), d_valid, d_err, d_set_status,
+                                                          ctypes.byref(t))
+            self._check(rc, "lb_verify_requests_device_async")
         return int(t.value)
 
+    def partial_wait_t(self, ticket: int) -> bytes:
+        out = np.zeros(LB_GT_BYTES, np.uint8)
+        self._check(self.lib.lb_partial_wait(self._h, ticket, _ptr(out)), "lb_partial_wait")
+        return out.tobytes()
+
+    def finish_t(self, ticket: int, merged_ok: bool) -> None:
+        self._check(self.lib.lb_verify_requests_finish(self._h, ticket, 1 if merged_ok else 0),
+                    "lb_verify_requests_finish")
+
     def wait(self, ticket: int) -> float:
+        """lb_wait on a ticket; returns device_ms (the call's stats in self.last_stats)."""
         st = _Stats()
         self._check(self.lib.lb_wait(self._h, ticket, ctypes.byref(st)), "lb_wait")
         self.last_stats = (int(st.batch_retries), int(st.batch_sigs_success))
@@ -434,10 +599,10 @@ class Device:
         return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
 
     def last_stage_times(self) -> List[Tuple[str, float]]:
-        ms = (ctypes.c_float * 16)()
-        names = (ctypes.c_char_p * 16)()
-        n = self.lib.lb_last_stage_times(self._h, ms, names, 16)
-        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 16))]
+        ms = (ctypes.c_float * 24)()
+        names = (ctypes.c_char_p * 24)()
+        n = self.lib.lb_last_stage_times(self._h, ms, names, 24)
+        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 24))]
 
 
 def device_count() -> int:

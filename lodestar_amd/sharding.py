@@ -1,23 +1,31 @@
 """Multi-GPU sharding of verification requests.
 
-Sets are independent, so a batch of requests shards across GPUs with no
-data-path collective: each GPU gets a contiguous range of whole requests
-(a request -- one BlsWorkReq of <= 128 sets, multithread/index.ts:57 -- is
-never split, so its verdict needs no cross-GPU Fp12 combination), verifies it
-locally and the per-request verdict bytes are gathered.
+Sets are independent and the batch equation is multiplicative, so a batch of
+requests shards across GPUs with no data-path collective: each GPU gets a
+contiguous range of whole requests (a request -- one BlsWorkReq of <= 128
+sets, multithread/index.ts:57 -- is never split) and runs it up to its merged
+Miller product P_g (576 bytes, lb_verify_requests_partial_async).  The host
+gathers the <= 8 partials and checks final_exp(prod_g P_g) == 1 ONCE
+(lb_gt_check); every shard then resumes with that verdict: all requests valid
+with no further work, or -- only when the combined check fails -- each shard
+verifies its requests alone (worker.ts:74-85 after a failed merged batch).
+RCCL over xGMI is not used: per GPU the exchange is 576 bytes.
 
 * ``shard_requests``: balance ranges by set count.
 * ``ShardedVerifier``: one process driving several local GPUs (one lb_ctx and
-  one host thread per GPU).
-* ``verify_distributed``: one process per GPU under torch.distributed; only
-  the verdict bytes travel (gloo all_gather), never points or Fp12 values.
+  one submission thread per GPU), with the Fp12-partial combine.
+* ``verify_distributed``: one process per GPU under torch.distributed (gloo,
+  host memory): the partials are all-gathered (576 B per rank), every rank runs
+  the same combined check on its own GPU, then the verdict bytes are gathered.
 """
 from __future__ import annotations
 
 import threading
-from typing import Callable, List, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
+
+GT_BYTES = 576  # LB_GT_BYTES: one Fp12 partial
 
 
 def shard_requests(request_sizes: Sequence[int], n_shards: int) -> List[Tuple[int, int]]:
@@ -45,18 +53,30 @@ def slice_requests(requests: Sequence, lo: int, hi: int) -> list:
     return list(requests[lo:hi])
 
 
+def _two_phase(backend) -> bool:
+    return all(hasattr(backend, a) for a in ("submit_requests", "finish", "gt_check"))
+
+
 class ShardedVerifier:
     """Verify a list of requests on several local GPUs concurrently.
 
-    ``backends[g]`` must offer ``verify_requests(requests) -> (valid, errors)``
-    (lodestar_amd.verifier.DeviceBackend does).
+    ``backends[g]`` offers ``verify_requests(requests) -> (valid, errors)``;
+    when every backend also offers the two-phase protocol
+    (lodestar_amd.verifier.DeviceBackend: ``submit_requests(partial=True)``,
+    ``finish``, ``gt_check``) and ``combine`` is set, the shards' Fp12 partials
+    are combined on the host with ONE final exponentiation (north_star).
+    ``last_combine`` records the combined check of the last call.
     """
 
-    def __init__(self, backends: Sequence[object]):
+    def __init__(self, backends: Sequence[object], combine: bool = True):
         self.backends = list(backends)
+        self.combine = combine and all(_two_phase(b) for b in self.backends)
+        self.last_combine: Optional[dict] = None
 
     def verify_requests(self, requests: Sequence) -> Tuple[List[bool], List[int]]:
         shards = shard_requests([len(r) for r in requests], len(self.backends))
+        if self.combine:
+            return self._verify_combined(requests, shards)
         out_valid: List[bool] = [False] * len(requests)
         out_err: List[int] = [0] * len(requests)
         errors: List[BaseException] = []
@@ -64,9 +84,9 @@ class ShardedVerifier:
         def run(g, lo, hi):
             try:
                 if hi > lo:
-                    v, e = self.backends[g].verify_requests(list(requests[lo:hi]))
-                    out_valid[lo:hi] = v
-                    out_err[lo:hi] = e
+                    r = self.backends[g].verify_requests(list(requests[lo:hi]))
+                    out_valid[lo:hi] = r[0]
+                    out_err[lo:hi] = r[1]
             except BaseException as ex:  # surfaced after join
                 errors.append(ex)
 
@@ -79,21 +99,59 @@ class ShardedVerifier:
             raise errors[0]
         return out_valid, out_err
 
+    def _verify_combined(self, requests, shards):
+        live = [(g, lo, hi) for g, (lo, hi) in enumerate(shards) if hi > lo]
+        # phase 1: every GPU runs its shard up to the merged Miller product
+        futs = [(g, lo, hi, self.backends[g].submit_requests(list(requests[lo:hi]), partial=True))
+                for g, lo, hi in live]
+        calls = [(g, lo, hi, f.result()) for g, lo, hi, f in futs]
+        # host combine: prod of the <= 8 partials, one final exponentiation (on GPU 0)
+        partials = [c.partial for _, _, _, c in calls]
+        ok = bool(self.backends[calls[0][0]].gt_check(partials).result()) if calls else True
+        self.last_combine = {"merged_ok": ok, "n_partials": len(partials)}
+        # phase 2: resume every shard with the combined verdict
+        fins = [(lo, hi, c.backend.finish(c, ok)) for _, lo, hi, c in calls]
+        out_valid: List[bool] = [False] * len(requests)
+        out_err: List[int] = [0] * len(requests)
+        for lo, hi, f in fins:
+            v, e, _ = f.result()
+            out_valid[lo:hi] = v
+            out_err[lo:hi] = e
+        return out_valid, out_err
 
-def verify_distributed(requests: Sequence, verify_local: Callable[[list], Tuple[List[bool], List[int]]],
-                       rank: int, world: int) -> Tuple[List[bool], List[int]]:
-    """torch.distributed version: every rank holds the same request list,
-    verifies its own shard with ``verify_local`` and all ranks receive every
-    verdict (gloo all_gather of one byte per request)."""
+
+def verify_distributed(requests: Sequence, verify_local: Optional[Callable[[list], Tuple[List[bool], List[int]]]],
+                       rank: int, world: int, backend: Optional[object] = None) -> Tuple[List[bool], List[int]]:
+    """torch.distributed version (one process per GPU): every rank holds the
+    same request list and verifies its own shard.  With a two-phase ``backend``
+    the ranks all-gather their 576-byte partials (gloo, host memory), each runs
+    the same combined check on its own GPU (no broadcast needed) and resumes its
+    shard; otherwise ``verify_local`` verifies the shard alone.  All ranks
+    receive every verdict (gloo all_gather of one int per request)."""
     import torch
     import torch.distributed as dist
     shards = shard_requests([len(r) for r in requests], world)
     lo, hi = shards[rank]
-    v, e = verify_local(list(requests[lo:hi])) if hi > lo else ([], [])
+    if backend is not None and _two_phase(backend):
+        call = backend.submit_requests(list(requests[lo:hi]), partial=True).result() if hi > lo else None
+        part = torch.zeros(GT_BYTES + 1, dtype=torch.uint8)
+        if call is not None:
+            part[:GT_BYTES] = torch.frombuffer(bytearray(call.partial), dtype=torch.uint8)
+            part[GT_BYTES] = 1
+        parts = [torch.zeros(GT_BYTES + 1, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, part)
+        partials = [bytes(p[:GT_BYTES].tolist()) for p in parts if int(p[GT_BYTES]) == 1]
+        ok = bool(backend.gt_check(partials).result())
+        if call is not None:
+            v, e, _ = backend.finish(call, ok).result()
+        else:
+            v, e = [], []
+    else:
+        v, e = verify_local(list(requests[lo:hi])) if hi > lo else ([], [])
     n = len(requests)
     mine = torch.zeros(n, dtype=torch.int32)
-    mine[lo:hi] = torch.tensor([int(x) | (int(y) << 8) for x, y in zip(v, e)], dtype=torch.int32) if hi > lo \
-        else mine[lo:hi]
+    if hi > lo:
+        mine[lo:hi] = torch.tensor([int(x) | (int(y) << 8) for x, y in zip(v, e)], dtype=torch.int32)
     gathered = [torch.zeros(n, dtype=torch.int32) for _ in range(world)]
     dist.all_gather(gathered, mine)
     combined = np.zeros(n, dtype=np.int32)

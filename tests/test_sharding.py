@@ -22,6 +22,41 @@ class TableBackend:
                [1 if any(s.get("empty_agg") for s in r) else 0 for r in requests]
 
 
+class TwoPhaseBackend(TableBackend):
+    """TableBackend with the two-phase protocol of DeviceBackend: the 576-byte
+    "partial" of a shard is 1 iff none of its requests holds a bad set (the
+    multiplicative combine in miniature), gt_check = AND of the partials."""
+
+    def __init__(self):
+        super().__init__()
+        self.finished = []
+
+    def submit_requests(self, requests, partial=False, priority=False):
+        import concurrent.futures
+        from types import SimpleNamespace
+        f = concurrent.futures.Future()
+        v, e = self.verify_requests(requests)
+        if partial:
+            ok = all(not s["bad"] for r in requests for s in r)
+            f.set_result(SimpleNamespace(backend=self, partial=bytes([ok]) + bytes(575), verdicts=(v, e)))
+        else:
+            f.set_result((v, e, None))
+        return f
+
+    def gt_check(self, partials):
+        import concurrent.futures
+        f = concurrent.futures.Future()
+        f.set_result(all(p[0] == 1 for p in partials))
+        return f
+
+    def finish(self, call, ok):
+        import concurrent.futures
+        self.finished.append(ok)
+        f = concurrent.futures.Future()
+        f.set_result((*call.verdicts, None))
+        return f
+
+
 def make_requests(seed=0, n=37):
     rnd = random.Random(seed)
     reqs, k = [], 0
@@ -59,25 +94,45 @@ def test_sharded_verifier_equals_single():
     assert sum(len(b.seen) for b in backs) >= 1
 
 
-def _worker(rank, world, port, reqs, out_q):
+@pytest.mark.parametrize("bad", [False, True])
+def test_sharded_verifier_combines_partials(bad):
+    reqs = make_requests(4)
+    for r in reqs:
+        for st in r:
+            st["bad"] = False
+            st["empty_agg"] = False
+    if bad:
+        next(r for r in reqs if r)[0]["bad"] = True
+    want = TableBackend().verify_requests(reqs)
+    backs = [TwoPhaseBackend() for _ in range(3)]
+    sv = ShardedVerifier(backs)
+    assert sv.combine
+    assert sv.verify_requests(reqs) == want
+    assert sv.last_combine["merged_ok"] is (not bad) and sv.last_combine["n_partials"] == 3
+    assert all(b.finished == [not bad] for b in backs)
+
+
+def _worker(rank, world, port, reqs, out_q, two_phase=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b = TableBackend()
-    v, e = verify_distributed(reqs, b.verify_requests, rank, world)
+    b = TwoPhaseBackend() if two_phase else TableBackend()
+    v, e = verify_distributed(reqs, b.verify_requests, rank, world, backend=b if two_phase else None)
     out_q.put((rank, v, e, b.seen))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_verify_distributed_gloo_world2():
+@pytest.mark.parametrize("two_phase", [False, True])
+def test_verify_distributed_gloo_world2(two_phase):
     reqs = make_requests(3)
     want = TableBackend().verify_requests(reqs)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.Random(os.getpid()).randrange(2000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, reqs, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port + (7 if two_phase else 0), reqs, q, two_phase))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -209,34 +209,56 @@ def test_public_key_index_or_bytes():
         PublicKey(b"\0" * 95, index=1)
 
 
+class FakeDev:
+    """Stand-in for native.Device (no GPU): records the arrays a call ships."""
+
+    def __init__(self, slow=0.0):
+        self.calls = []
+        self.slow = slow
+        self.closed = False
+        self.active = 0
+
+    def verify_requests_async(self, req_off, pks, pk_off, msgs, blob, offs, seed, pk_indices=None, partial=False):
+        import numpy as np
+        from lodestar_amd.native import PendingCall
+        assert not self.closed, "call on a destroyed context"
+        self.calls.append((pks, None if pk_indices is None else list(pk_indices), list(pk_off)))
+        n = len(req_off) - 1
+        self.active += 1
+        return PendingCall(len(self.calls), n, 0, np.ones(max(n, 1), np.uint8), np.zeros(max(n, 1), np.uint8),
+                           np.zeros(1, np.uint8), None, partial)
+
+    def wait_call(self, pc):
+        import time as _t
+
+        import numpy as np
+        from lodestar_amd.native import VerifyResult
+        assert not self.closed, "wait on a destroyed context"
+        _t.sleep(self.slow)
+        self.active -= 1
+        return VerifyResult(pc.valid[:pc.n_req], pc.err[:pc.n_req], np.zeros(0, np.uint8), 0.0)
+
+    def last_stage_times(self):
+        return [("pubkeys_agg", 0.5)]
+
+    def pubkey_table_size(self):
+        return 10
+
+    def pubkey_table_read(self, first, n):
+        return [bytes([first]) * 96]
+
+    def close(self):
+        assert self.active == 0, "context destroyed with a call in flight"
+        self.closed = True
+
+
 def test_device_backend_ships_indices_when_every_key_has_one():
-    import threading
-
-    import numpy as np
-
-    from lodestar_amd.native import VerifyResult
     from lodestar_amd.verifier import DeviceBackend, PublicKey, aggregate_set, single_set
 
-    class FakeDev:
-        def __init__(self):
-            self.calls = []
-
-        def verify_requests(self, req_off, pks, pk_off, msgs, blob, offs, seed, pk_indices=None):
-            self.calls.append((pks, None if pk_indices is None else list(pk_indices), list(pk_off)))
-            n = len(req_off) - 1
-            return VerifyResult(np.ones(n, np.uint8), np.zeros(n, np.uint8), np.zeros(0, np.uint8), 0.0)
-
-        def pubkey_table_size(self):
-            return 10
-
-        def pubkey_table_read(self, first, n):
-            return [bytes([first]) * 96]
-
-    b = object.__new__(DeviceBackend)
-    b.dev, b.seed_source, b.lock = FakeDev(), (lambda: bytes(32)), threading.Lock()
+    b = DeviceBackend(seed_source=lambda: bytes(32), dev=FakeDev())
     s1 = single_set(PublicKey(index=4), bytes(32), bytes(96))
     s2 = aggregate_set([PublicKey(index=1), PublicKey(index=2)], bytes(32), bytes(96))
-    b.verify_requests([[s1, s2]])
+    assert b.verify_requests([[s1, s2]]) == ([True], [0])
     pks, idx, pk_off = b.dev.calls[-1]
     assert pks is None and idx == [4, 1, 2] and pk_off == [0, 1, 3]
     # mixed: index-only keys are materialised from the table, bytes shipped
@@ -244,6 +266,63 @@ def test_device_backend_ships_indices_when_every_key_has_one():
     b.verify_requests([[s1, s3]])
     pks, idx, _ = b.dev.calls[-1]
     assert idx is None and pks.tobytes() == bytes([4]) * 96 + bytes([7]) * 96
+    b.close()
+
+
+def test_signing_root_length_is_checked():
+    from lodestar_amd.verifier import DeviceBackend, PublicKey, single_set
+
+    b = DeviceBackend(seed_source=lambda: bytes(32), dev=FakeDev())
+    with pytest.raises(ValueError):
+        b.verify_requests([[single_set(PublicKey(index=1), bytes(31), bytes(96))]])
+    b.close()
+
+    async def main():
+        v = BlsGpuVerifier(backends=[MockBackend()])
+        with pytest.raises(ValueError):
+            await v.verify_signature_sets([single_set(PK, bytes(33), GOOD)])
+        await v.close()
+    run(main())
+
+
+def test_close_waits_for_calls_in_flight():
+    """close() must never destroy the context under a running call
+    (index.ts:244-265 awaits the workers)."""
+    from lodestar_amd.verifier import DeviceBackend
+
+    async def main():
+        dev = FakeDev(slow=0.2)
+        v = BlsGpuVerifier(backends=[DeviceBackend(seed_source=lambda: bytes(32), dev=dev)])
+        futs = [asyncio.ensure_future(v.verify_signature_sets(sets(3))) for _ in range(6)]
+        await asyncio.sleep(0.05)  # dispatched, the fake device still busy
+        await v.close()
+        assert dev.closed and dev.active == 0
+        done = [f.result() if not f.exception() else f.exception() for f in futs]
+        assert all(d is True or isinstance(d, QueueError) for d in done)
+    run(main())
+
+
+def test_device_backend_keeps_several_calls_in_flight():
+    from lodestar_amd.verifier import DeviceBackend
+
+    dev = FakeDev(slow=0.05)
+    b = DeviceBackend(seed_source=lambda: bytes(32), dev=dev, capacity=4)
+    futs = [b.submit_requests([sets(2)]) for _ in range(8)]
+    assert [f.result()[0] for f in futs] == [[True]] * 8
+    b.close()
+
+
+def test_worker_batch_stats_match_reference_chunking():
+    """worker.ts:41-85: batchable requests in chunks of >= 16, one retry per failed chunk."""
+    from lodestar_amd.verifier import worker_batch_stats
+    assert worker_batch_stats([3] * 10, [True] * 10, [True] * 10) == (0, 30)
+    assert worker_batch_stats([3] * 10, [True] * 10, [True] * 9 + [False]) == (1, 0)
+    # 40 batchable requests -> chunkify(40, 16) = 2 chunks of 20; one bad request fails one chunk
+    v = [True] * 40
+    v[25] = False
+    assert worker_batch_stats([2] * 40, [True] * 40, v) == (1, 40)
+    # non-batchable requests never count
+    assert worker_batch_stats([5, 5], [False, False], [False, True]) == (0, 0)
 
 
 # ---- metrics parity (lodestar.ts:380-495 names, index.ts update sites) -------------
@@ -252,7 +331,6 @@ def test_pool_metrics_reference_names():
 
     async def main():
         b = MockBackend()
-        b.last_stats = (1, 0)
         v = BlsGpuVerifier(backends=[b])
         assert await v.verify_signature_sets(sets(300), VerifySignatureOpts(batchable=True, priority=True)) is True
         with pytest.raises(EmptyAggregateError):
@@ -268,7 +346,7 @@ def test_pool_metrics_reference_names():
         assert pm.get(M.ERROR_AGGREGATE_SETS, type="default") == 1
         assert pm.get(M.ERROR_JOBS_SETS) == 1 and pm.get(M.SUCCESS_JOBS_SETS) == 301
         assert pm.get(M.SAME_MESSAGE_RETRY_JOBS) == 1 and pm.get(M.SAME_MESSAGE_RETRY_SETS) == 2
-        assert pm.get(M.BATCH_RETRIES) >= 1
+        assert pm.get(M.BATCH_RETRIES) == 0 and pm.get(M.BATCH_SIGS_SUCCESS) == 300  # one passing chunk
         assert pm.histogram(M.JOB_WAIT_TIME)[0] == 4
         names = set(pm.collect())
         assert "lodestar_bls_thread_pool_sig_sets_total" in names
