@@ -1,0 +1,576 @@
+"use strict";
+/**
+ * BlsGpuVerifier: IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:25-68)
+ * over MI355X GPUs, through the N-API addon (lodestar_amd/napi/addon.cc).  It is
+ * what chain.ts:206-208 would construct beside BlsMultiThreadWorkerPool; its
+ * scheduling is the pool's (chain/bls/multithread/index.ts:114-580) with GPUs in
+ * place of worker threads:
+ *
+ *  - verifySignatureSets(sets, opts) -> Promise<boolean>            (index.ts:163-213)
+ *  - verifySignatureSetsSameMessage(sets, message, opts) -> boolean[] (index.ts:218-242)
+ *  - close() / canAcceptWork()                                       (index.ts:244-265,155-161)
+ *  - sets chunked to <= 128 per job (chunkifyMaximizeChunkSize, utils.ts:4-19)
+ *  - batchable jobs buffered up to 100 ms or > 32 sig sets (index.ts:327-343),
+ *    priority jobs to the queue front (index.ts:544-555)
+ *  - an aggregate set with zero pubkeys rejects its job (index.ts:403-409)
+ *  - a same-message job that fails is retried set by set (index.ts:473-484,557-568)
+ *    -- on the GPU, inside the same batched call (lb_verify_same_message_batch)
+ *
+ * What changes for a GPU: a package may hold up to maxSetsPerDispatch (65,536)
+ * sig sets, because the GPU wants tens of thousands of sets per call; every job
+ * keeps its own verdict (per-request verdicts on the device), so merging never
+ * changes a verdict (worker.ts:74-85 guarantees the same on CPU by re-verifying).
+ * Each GPU takes up to `capacity` packages at once (the addon's in-flight slots).
+ *
+ * Sets: {type: "single", pubkey, signingRoot, signature} or
+ *       {type: "aggregate", pubkeys, signingRoot, signature}
+ * (ISignatureSet, state-transition/src/util/signatureSets.ts:5-24).  A pubkey is a
+ * 96-byte uncompressed Uint8Array, an object with .toBytes() returning one, or
+ * {index} -- a validator index into the device pubkey table (syncPubkeys, the
+ * index2pubkey mirror of state-transition/src/cache/pubkeyCache.ts:56-77).
+ */
+const crypto = require("crypto");
+const path = require("path");
+
+const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:57
+const MAX_BUFFERED_SIGS = 32; // index.ts:66
+const MAX_BUFFER_WAIT_MS = 100; // index.ts:75
+const MAX_JOBS_CAN_ACCEPT_WORK = 512; // index.ts:80
+const BATCHABLE_MIN_PER_CHUNK = 16; // worker.ts:17
+const LB_REQ_EMPTY_AGGREGATE = 1;
+const LB_REQ_BAD_PUBKEY = 2;
+const GT_BYTES = 576;
+
+const QueueErrorCode = {QUEUE_ABORTED: "QUEUE_ERROR_QUEUE_ABORTED"};
+
+class QueueError extends Error {
+  constructor(code) {
+    super(code);
+    this.type = {code};
+  }
+}
+
+function loadAddon() {
+  return require(path.join(__dirname, "..", "napi", "lodestar_bls.node"));
+}
+
+/** utils.ts:4-19 */
+function chunkifyMaximizeChunkSize(arr, minPerChunk) {
+  const chunkCount = Math.floor(arr.length / minPerChunk);
+  if (chunkCount <= 1) return [arr];
+  const perChunk = Math.ceil(arr.length / chunkCount);
+  const out = [];
+  for (let i = 0; i < arr.length; i += perChunk) out.push(arr.slice(i, i + perChunk));
+  return out;
+}
+
+/** (batchRetries, batchSigsSuccess) of one package as the reference worker counts them
+ * (worker.ts:41-85): batchable requests chunked by >= 16, one retry per failed chunk. */
+function workerBatchStats(requestSizes, batchable, valid) {
+  const idx = [];
+  for (let k = 0; k < batchable.length; k++) if (batchable[k]) idx.push(k);
+  let retries = 0;
+  let sigsOk = 0;
+  if (idx.length === 0) return {retries, sigsOk};
+  for (const chunk of chunkifyMaximizeChunkSize(idx, BATCHABLE_MIN_PER_CHUNK)) {
+    const n = chunk.reduce((s, k) => s + requestSizes[k], 0);
+    if (n > 0 && chunk.every((k) => valid[k])) sigsOk += n;
+    else retries++;
+  }
+  return {retries, sigsOk};
+}
+
+function pubkeyRef(pk) {
+  if (pk instanceof Uint8Array) {
+    if (pk.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
+    return {bytes: pk};
+  }
+  if (pk && typeof pk.index === "number") return {index: pk.index, bytes: pk.bytes || null};
+  if (pk && typeof pk.toBytes === "function") return pubkeyRef(pk.toBytes(false));
+  throw new TypeError("pubkey: Uint8Array(96), {index} or an object with toBytes()");
+}
+
+function concat(arrays, total) {
+  const out = new Uint8Array(total);
+  let o = 0;
+  for (const a of arrays) {
+    out.set(a, o);
+    o += a.length;
+  }
+  return out;
+}
+
+/** Requests (arrays of sets) -> the addon's batch (lb_request_batch layout). */
+function packRequests(requests, seed) {
+  const keys = [];
+  const pkOff = [0];
+  const msgs = [];
+  const sigs = [];
+  const sigOff = [0];
+  const reqOff = [0];
+  let sigBytes = 0;
+  for (const req of requests) {
+    for (const s of req) {
+      const ks = s.type === "aggregate" ? s.pubkeys || [] : [s.pubkey];
+      for (const k of ks) keys.push(pubkeyRef(k));
+      pkOff.push(keys.length);
+      if (!(s.signingRoot instanceof Uint8Array) || s.signingRoot.length !== 32)
+        throw new TypeError("signingRoot must be 32 bytes");
+      msgs.push(s.signingRoot);
+      sigs.push(s.signature);
+      sigBytes += s.signature.length;
+      sigOff.push(sigBytes);
+    }
+    reqOff.push(msgs.length);
+  }
+  const batch = {
+    requestOffsets: Uint32Array.from(reqOff),
+    pkOffsets: Uint32Array.from(pkOff),
+    messages: concat(msgs, 32 * msgs.length),
+    signatures: concat(sigs, sigBytes),
+    sigOffsets: Uint32Array.from(sigOff),
+    seed,
+  };
+  if (keys.length > 0 && keys.every((k) => k.index !== undefined)) {
+    batch.pubkeyIndices = Uint32Array.from(keys.map((k) => k.index));
+  } else {
+    if (keys.some((k) => !k.bytes)) throw new TypeError("mixed package: index-only pubkeys need their bytes");
+    batch.pubkeys = concat(
+      keys.map((k) => k.bytes),
+      96 * keys.length
+    );
+  }
+  return batch;
+}
+
+/** Same-message jobs -> the addon's lb_same_message_batch layout. */
+function packSameMessage(jobs, seed) {
+  const jobOff = [0];
+  const keys = [];
+  const sigs = [];
+  const sigOff = [0];
+  let sigBytes = 0;
+  for (const job of jobs) {
+    for (const s of job.sets) {
+      keys.push(pubkeyRef(s.publicKey));
+      sigs.push(s.signature);
+      sigBytes += s.signature.length;
+      sigOff.push(sigBytes);
+    }
+    jobOff.push(keys.length);
+  }
+  const batch = {
+    jobOffsets: Uint32Array.from(jobOff),
+    signatures: concat(sigs, sigBytes),
+    sigOffsets: Uint32Array.from(sigOff),
+    messages: concat(
+      jobs.map((j) => j.message),
+      32 * jobs.length
+    ),
+    seed,
+  };
+  if (keys.length > 0 && keys.every((k) => k.index !== undefined)) {
+    batch.pubkeyIndices = Uint32Array.from(keys.map((k) => k.index));
+  } else {
+    batch.pubkeys = concat(
+      keys.map((k) => k.bytes),
+      96 * keys.length
+    );
+  }
+  return batch;
+}
+
+/** The reference's metric names (metrics/metrics/lodestar.ts:379-510), in-process. */
+class PoolMetrics {
+  constructor() {
+    this.values = new Map();
+    this.hist = new Map();
+  }
+  key(name, labels) {
+    const l = labels ? Object.keys(labels).sort().map((k) => `${k}="${labels[k]}"`).join(",") : "";
+    return l ? `${name}{${l}}` : name;
+  }
+  inc(name, v = 1, labels) {
+    const k = this.key(name, labels);
+    this.values.set(k, (this.values.get(k) || 0) + v);
+  }
+  set(name, v, labels) {
+    this.values.set(this.key(name, labels), v);
+  }
+  observe(name, v, labels) {
+    const k = this.key(name, labels);
+    const h = this.hist.get(k) || {count: 0, sum: 0};
+    h.count++;
+    h.sum += v;
+    this.hist.set(k, h);
+  }
+  get(name, labels) {
+    return this.values.get(this.key(name, labels)) || 0;
+  }
+}
+
+const P = "lodestar_bls_thread_pool_";
+const M = {
+  AGGREGATED_PUBKEYS: "lodestar_bls_aggregated_pubkeys_total",
+  JOBS_WORKER_TIME: P + "time_seconds_sum",
+  SUCCESS_JOBS_SETS: P + "success_jobs_signature_sets_count",
+  ERROR_AGGREGATE_SETS: P + "error_aggregate_signature_sets_count",
+  ERROR_JOBS_SETS: P + "error_jobs_signature_sets_count",
+  JOB_WAIT_TIME: P + "queue_job_wait_time_seconds",
+  QUEUE_LENGTH: P + "queue_length",
+  WORKERS_BUSY: P + "workers_busy",
+  JOB_GROUPS_STARTED: P + "job_groups_started_total",
+  JOBS_STARTED: P + "jobs_started_total",
+  SIG_SETS_STARTED: P + "sig_sets_started_total",
+  BATCH_RETRIES: P + "batch_retries_total",
+  BATCH_SIGS_SUCCESS: P + "batch_sigs_success_total",
+  SAME_MESSAGE_RETRY_JOBS: P + "same_message_jobs_retries_total",
+  SAME_MESSAGE_RETRY_SETS: P + "same_message_sets_retries_total",
+  LATENCY_TO_WORKER: P + "latency_to_worker",
+  LATENCY_FROM_WORKER: P + "latency_from_worker",
+  MAIN_THREAD_TIME: P + "main_thread_time_seconds",
+  TIME_PER_SIG_SET: "lodestar_bls_worker_thread_time_per_sigset_seconds",
+  TOTAL_SIG_SETS: P + "sig_sets_total",
+  PRIORITIZED_SIG_SETS: P + "prioritized_sig_sets_total",
+  BATCHABLE_SIG_SETS: P + "batchable_sig_sets_total",
+};
+
+function hrNowNs() {
+  const [s, ns] = process.hrtime();
+  return s * 1e9 + ns;
+}
+
+class BlsGpuVerifier {
+  /**
+   * @param {object} o
+   * @param {number[]} [o.devices]  GPU ordinals, one addon Context each (default [0])
+   * @param {object[]} [o.backends] Context-like objects instead (tests: mocks)
+   * @param {boolean} [o.blsVerifyAllMultiThread]
+   * @param {number} [o.maxSetsPerDispatch]
+   * @param {() => Uint8Array} [o.seedSource] 32-byte batch-randomness seed per call
+   */
+  constructor(o = {}) {
+    if (o.backends) this.backends = o.backends;
+    else {
+      const addon = loadAddon();
+      this.backends = (o.devices || [0]).map((d) => new addon.Context(d, {capacity: o.capacity || 4}));
+    }
+    if (this.backends.length === 0) throw new Error("at least one GPU backend is required");
+    this.blsVerifyAllMultiThread = Boolean(o.blsVerifyAllMultiThread);
+    this.maxSetsPerDispatch = o.maxSetsPerDispatch || 65536;
+    this.seedSource = o.seedSource || (() => new Uint8Array(crypto.randomBytes(32)));
+    this.metrics = new PoolMetrics();
+    this.jobs = [];
+    this.buffered = null;
+    this.idle = [];
+    this.backends.forEach((b, i) => {
+      for (let k = 0; k < (b.capacity || 4); k++) this.idle.push(i);
+    });
+    this.capacity = this.idle.length;
+    this.running = new Set();
+    this.closed = false;
+  }
+
+  canAcceptWork() {
+    return this.idle.length > 0 && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
+  }
+
+  /** index2pubkey mirror on every GPU (pubkeyCache.ts:56-77): keys 48-byte compressed. */
+  async syncPubkeys(keys, pkLen = 48) {
+    const blob = concat(keys, keys.length * pkLen);
+    const sizes = await Promise.all(this.backends.map((b) => b.syncPubkeys(blob, pkLen)));
+    if (new Set(sizes).size !== 1) throw new Error(`pubkey tables out of sync: ${sizes}`);
+    return sizes[0];
+  }
+
+  async verifySignatureSets(sets, opts = {}) {
+    const m = this.metrics;
+    m.inc(M.AGGREGATED_PUBKEYS, sets.reduce((s, x) => s + (x.type === "aggregate" ? (x.pubkeys || []).length : 0), 0));
+    m.inc(M.TOTAL_SIG_SETS, sets.length);
+    if (opts.priority) m.inc(M.PRIORITIZED_SIG_SETS, sets.length);
+    if (opts.batchable) m.inc(M.BATCHABLE_SIG_SETS, sets.length);
+    if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
+      // index.ts:174-187: verified at once, bypassing the queue (the GPU call does
+      // not block the event loop, unlike blst on the reference's main thread)
+      const t0 = process.hrtime();
+      try {
+        const r = await this.backends[0].verifyRequests(packRequests([sets], this.seedSource()));
+        return this.requestVerdict(r, 0);
+      } finally {
+        const [s, ns] = process.hrtime(t0);
+        m.observe(M.MAIN_THREAD_TIME, s + ns / 1e9);
+      }
+    }
+    const results = await Promise.all(
+      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map(
+        (chunk) => new Promise((resolve, reject) => this.queueBlsWork({type: "default", resolve, reject, opts, sets: chunk, added: Date.now()}))
+      )
+    );
+    if (results.length === 0) throw Error("Empty results array");
+    return results.every((v) => v === true);
+  }
+
+  async verifySignatureSetsSameMessage(sets, message, opts = {}) {
+    if (!(message instanceof Uint8Array) || message.length !== 32) throw new TypeError("message must be 32 bytes");
+    const results = await Promise.all(
+      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map(
+        (chunk) =>
+          new Promise((resolve, reject) =>
+            this.queueBlsWork({type: "sameMessage", resolve, reject, opts, sets: chunk, message, added: Date.now()})
+          )
+      )
+    );
+    return results.flat();
+  }
+
+  async close() {
+    if (this.buffered) {
+      clearTimeout(this.buffered.timeout);
+      for (const job of this.buffered.jobs.concat(this.buffered.prioritizedJobs))
+        job.reject(new QueueError(QueueErrorCode.QUEUE_ABORTED));
+      this.buffered = null;
+    }
+    for (const job of this.jobs) job.reject(new QueueError(QueueErrorCode.QUEUE_ABORTED));
+    this.jobs = [];
+    this.closed = true;
+    await Promise.all([...this.running].map((p) => p.catch(() => undefined)));
+    await Promise.all(this.backends.map((b) => (b.close ? b.close() : undefined)));
+  }
+
+  // ---- scheduling (index.ts:308-568) --------------------------------------------
+  queueBlsWork(job) {
+    if (this.closed) throw new QueueError(QueueErrorCode.QUEUE_ABORTED);
+    const sigSets = job.type === "default" ? job.sets.length : 1; // jobItemSigSets, jobItem.ts:39-46
+    if (job.opts.batchable) {
+      if (!this.buffered) {
+        this.buffered = {jobs: [], prioritizedJobs: [], sigCount: 0, timeout: setTimeout(this.runBufferedJobs, MAX_BUFFER_WAIT_MS)};
+      }
+      (job.opts.priority ? this.buffered.prioritizedJobs : this.buffered.jobs).push(job);
+      this.buffered.sigCount += sigSets;
+      if (this.buffered.sigCount > MAX_BUFFERED_SIGS) {
+        clearTimeout(this.buffered.timeout);
+        this.runBufferedJobs();
+      }
+    } else {
+      if (job.opts.priority) this.jobs.unshift(job);
+      else this.jobs.push(job);
+      setTimeout(this.runJob, 0);
+    }
+  }
+
+  runBufferedJobs = () => {
+    if (!this.buffered) return;
+    for (const job of this.buffered.jobs) this.jobs.push(job);
+    for (const job of this.buffered.prioritizedJobs) this.jobs.unshift(job);
+    this.buffered = null;
+    setTimeout(this.runJob, 0);
+  };
+
+  prepareWork() {
+    const jobs = [];
+    let total = 0;
+    while (total < this.maxSetsPerDispatch && this.jobs.length > 0) {
+      const job = this.jobs.shift();
+      jobs.push(job);
+      total += job.type === "default" ? job.sets.length : 1;
+    }
+    return jobs;
+  }
+
+  runJob = () => {
+    if (this.closed || this.idle.length === 0 || this.jobs.length === 0) return;
+    const jobs = this.prepareWork();
+    if (jobs.length === 0) return;
+    const bi = this.idle.shift();
+    const m = this.metrics;
+    m.inc(M.JOB_GROUPS_STARTED);
+    for (const type of ["default", "sameMessage"]) {
+      m.inc(M.JOBS_STARTED, jobs.filter((j) => j.type === type).length, {type});
+      m.inc(M.SIG_SETS_STARTED, jobs.filter((j) => j.type === type).reduce((s, j) => s + j.sets.length, 0), {type});
+    }
+    const now = Date.now();
+    for (const j of jobs) m.observe(M.JOB_WAIT_TIME, (now - j.added) / 1000);
+    m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+    m.set(M.QUEUE_LENGTH, this.jobs.length);
+    const p = this.dispatch(bi, jobs).finally(() => this.running.delete(p));
+    this.running.add(p);
+    if (this.idle.length > 0 && this.jobs.length > 0) setTimeout(this.runJob, 0);
+  };
+
+  requestVerdict(r, k) {
+    if (r.errors[k] === LB_REQ_EMPTY_AGGREGATE) throw new Error("EMPTY_AGGREGATE_ARRAY");
+    if (r.errors[k] === LB_REQ_BAD_PUBKEY) throw new Error("invalid pubkey encoding");
+    return r.valid[k] === 1;
+  }
+
+  async dispatch(bi, jobs) {
+    const backend = this.backends[bi];
+    const m = this.metrics;
+    const dispatchNs = hrNowNs();
+    const def = jobs.filter((j) => j.type === "default");
+    const same = jobs.filter((j) => j.type === "sameMessage");
+    let outs;
+    try {
+      const waits = [];
+      if (def.length) waits.push(backend.verifyRequests(packRequests(def.map((j) => j.sets), this.seedSource())));
+      if (same.length) waits.push(backend.verifySameMessage(packSameMessage(same, this.seedSource())));
+      outs = await Promise.all(waits);
+    } catch (e) {
+      // device failure rejects every job of the package (index.ts:503-512)
+      this.idle.push(bi);
+      m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+      for (const job of jobs) job.reject(e);
+      setTimeout(this.runJob, 0);
+      return;
+    }
+    const backNs = hrNowNs();
+    this.idle.push(bi);
+    m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+    let k = 0;
+    let success = 0;
+    let errors = 0;
+    const started = jobs.reduce((s, j) => s + j.sets.length, 0);
+    const observeWorker = (r) => {
+      if (!r.workerEndNs) return;
+      const sec = (r.workerEndNs - r.workerStartNs) / 1e9;
+      m.inc(M.JOBS_WORKER_TIME, sec, {workerId: bi});
+      if (started) m.observe(M.TIME_PER_SIG_SET, sec / started);
+      m.observe(M.LATENCY_TO_WORKER, Math.max(0, (r.workerStartNs - dispatchNs) / 1e9));
+      m.observe(M.LATENCY_FROM_WORKER, Math.max(0, (backNs - r.workerEndNs) / 1e9));
+    };
+    if (def.length) {
+      const r = outs[k++];
+      observeWorker(r);
+      const ok = [];
+      def.forEach((job, n) => {
+        try {
+          const v = this.requestVerdict(r, n);
+          ok.push(v);
+          job.resolve(v);
+          success += job.sets.length;
+        } catch (e) {
+          ok.push(false);
+          if (r.errors[n] === LB_REQ_EMPTY_AGGREGATE) m.inc(M.ERROR_AGGREGATE_SETS, job.sets.length, {type: "default"});
+          job.reject(e);
+          errors += job.sets.length;
+        }
+      });
+      const st = workerBatchStats(def.map((j) => j.sets.length), def.map((j) => Boolean(j.opts.batchable)), ok);
+      m.inc(M.BATCH_RETRIES, st.retries);
+      m.inc(M.BATCH_SIGS_SUCCESS, st.sigsOk);
+    }
+    if (same.length) {
+      const r = outs[k++];
+      observeWorker(r);
+      let at = 0;
+      same.forEach((job, n) => {
+        const verdicts = Array.from(r.valid.subarray(at, at + job.sets.length), (v) => v === 1);
+        at += job.sets.length;
+        if (!r.jobFast[n] && job.sets.length) {
+          m.inc(M.SAME_MESSAGE_RETRY_JOBS); // index.ts:566-567
+          m.inc(M.SAME_MESSAGE_RETRY_SETS, job.sets.length);
+        }
+        success += 1;
+        job.resolve(verdicts);
+      });
+      const st = workerBatchStats(same.map(() => 1), same.map((j) => Boolean(j.opts.batchable)), Array.from(r.jobFast, (f) => f === 1));
+      m.inc(M.BATCH_RETRIES, st.retries);
+      m.inc(M.BATCH_SIGS_SUCCESS, st.sigsOk);
+    }
+    m.inc(M.SUCCESS_JOBS_SETS, success);
+    m.inc(M.ERROR_JOBS_SETS, errors);
+    setTimeout(this.runJob, 0);
+  }
+}
+
+/** BlsSingleThreadVerifier (chain/bls/singleThread.ts:10-89) on one GPU: no queue,
+ * no buffering, every call goes straight to the device. */
+class BlsGpuSingleThreadVerifier {
+  constructor(o = {}) {
+    this.backend = o.backend || new (loadAddon().Context)(o.device || 0);
+    this.seedSource = o.seedSource || (() => new Uint8Array(crypto.randomBytes(32)));
+  }
+  async verifySignatureSets(sets) {
+    const r = await this.backend.verifyRequests(packRequests([sets], this.seedSource()));
+    if (r.errors[0] === LB_REQ_EMPTY_AGGREGATE) throw new Error("EMPTY_AGGREGATE_ARRAY");
+    if (r.errors[0] === LB_REQ_BAD_PUBKEY) throw new Error("invalid pubkey encoding");
+    return r.valid[0] === 1;
+  }
+  async verifySignatureSetsSameMessage(sets, message) {
+    if (sets.length === 0) throw new Error("EMPTY_AGGREGATE_ARRAY"); // PublicKey.aggregate([]) throws (singleThread.ts:43)
+    const r = await this.backend.verifySameMessage(packSameMessage([{sets, message}], this.seedSource()));
+    return Array.from(r.valid.subarray(0, sets.length), (v) => v === 1);
+  }
+  async close() {
+    if (this.backend.close) await this.backend.close();
+  }
+  canAcceptWork() {
+    return true;
+  }
+}
+
+/** Contiguous shards of whole requests balanced by set count (sharding.py:shard_requests). */
+function shardRequests(sizes, nShards) {
+  const total = sizes.reduce((a, b) => a + b, 0);
+  const bounds = [0];
+  let acc = 0;
+  let k = 1;
+  sizes.forEach((s, i) => {
+    acc += s;
+    while (k < nShards && acc * nShards >= total * k && bounds[bounds.length - 1] <= i) {
+      bounds.push(i + 1);
+      k++;
+    }
+  });
+  while (bounds.length < nShards) bounds.push(sizes.length);
+  bounds.push(sizes.length);
+  const out = [];
+  for (let j = 0; j < nShards; j++) out.push([bounds[j], bounds[j + 1]]);
+  return out;
+}
+
+/** One call over several GPUs (SURVEY §8e): each shard runs to its 576-byte Fp12
+ * partial, the host combines them with ONE final exponentiation (gtCheck on the first
+ * GPU) and resumes every shard with the verdict.  Returns {valid, errors, mergedOk}. */
+async function verifyRequestsSharded(backends, requests, seedSource) {
+  const shards = shardRequests(
+    requests.map((r) => r.length),
+    backends.length
+  ).filter(([lo, hi]) => hi > lo);
+  const calls = await Promise.all(
+    shards.map(([lo, hi], g) => backends[g].verifyRequestsPartial(packRequests(requests.slice(lo, hi), seedSource())))
+  );
+  const partials = concat(
+    calls.map((c) => c.partial),
+    GT_BYTES * calls.length
+  );
+  const mergedOk = calls.length === 0 ? true : await backends[0].gtCheck(partials);
+  const res = await Promise.all(calls.map((c, g) => backends[g].finish(c.id, mergedOk)));
+  const valid = new Uint8Array(requests.length);
+  const errors = new Uint8Array(requests.length);
+  shards.forEach(([lo], g) => {
+    valid.set(res[g].valid, lo);
+    errors.set(res[g].errors, lo);
+  });
+  return {valid, errors, mergedOk};
+}
+
+module.exports = {
+  BlsGpuVerifier,
+  BlsGpuSingleThreadVerifier,
+  QueueError,
+  QueueErrorCode,
+  PoolMetrics,
+  METRICS: M,
+  chunkifyMaximizeChunkSize,
+  workerBatchStats,
+  packRequests,
+  packSameMessage,
+  shardRequests,
+  verifyRequestsSharded,
+  loadAddon,
+  MAX_SIGNATURE_SETS_PER_JOB,
+  MAX_BUFFERED_SIGS,
+  MAX_BUFFER_WAIT_MS,
+  MAX_JOBS_CAN_ACCEPT_WORK,
+};

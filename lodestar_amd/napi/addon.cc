@@ -1,0 +1,819 @@
+// N-API addon: the Lodestar-side binding of the MI355X BLS verifier C ABI
+// (include/lodestar_bls.h).  This is what a BlsGpuVerifier beside
+// BlsMultiThreadWorkerPool (packages/beacon-node/src/chain/bls, chosen at
+// BN/chain/chain.ts:206-208) requires: it replaces the worker boundary
+// workerApi.verifyManySignatureSets(workReqs) (chain/bls/multithread/index.ts:444,
+// worker.ts:24-30) with one call per package on a GPU.
+//
+// Threading: JS calls arrive on the main thread; their
+// inputs are copied there (the reference structured-clones them to the worker,
+// index.ts:444) and handed to ONE host submission thread per GPU, which owns
+// the lb_ctx (not thread-safe) and keeps up to `capacity` calls in flight
+// (lb_verify_requests_async + lb_wait).  Completions come back to the event
+// loop through a threadsafe function; the event loop never blocks on the GPU.
+// Every native method returns a Promise; bad arguments and device errors
+// reject it (a malformed signature is a verdict, never an error).
+//
+// Exports:
+//   deviceCount() -> number
+//   validateRequests(batch) -> {nRequests, nSets, nPubkeys, byIndex}   (marshalling dry run, no device)
+//   new Context(device, {capacity?}) (throws Error{code: "LB_ERR_NO_DEVICE", ...} without a GPU)
+//     .verifyRequests(batch) -> Promise<{valid, errors, setStatus, batchRetries, batchSigsSuccess,
+//                                        deviceMs, workerStartNs, workerEndNs}>
+//     .verifyRequestsPartial(batch) -> Promise<{id, partial: Uint8Array(576)}>  (two-phase, multi-GPU)
+//     .finish(id, mergedOk) -> Promise<result of verifyRequests>
+//     .gtCheck(Uint8Array n*576) -> Promise<boolean>
+//     .verifySameMessage({jobOffsets, pubkeys|pubkeyIndices, signatures, sigOffsets, messages, seed})
+//         -> Promise<{valid, jobFast, retriedJobs, fastSets, deviceMs}>
+//     .syncPubkeys(Uint8Array keys, pkLen) -> Promise<number>          (index2pubkey mirror)
+//     .aggregatePubkeys(Uint8Array n*96 | Uint32Array indices) -> Promise<Uint8Array(96)>
+//     .close() -> Promise<void>                                      (waits for calls in flight)
+//   batch = {requestOffsets: Uint32Array, pubkeys?: Uint8Array, pubkeyIndices?: Uint32Array,
+//            pkOffsets?: Uint32Array, messages: Uint8Array, signatures: Uint8Array,
+//            sigOffsets: Uint32Array, seed: Uint8Array(32), batchable?: Uint8Array}
+#define NAPI_VERSION 8
+#include <node_api.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/lodestar_bls.h"
+
+namespace {
+
+#define NAPI_OK(call)                       \
+  do {                                      \
+    if ((call) != napi_ok) return nullptr;  \
+  } while (0)
+
+struct ArgError {
+  std::string msg;
+};
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// ---- marshalling --------------------------------------------------------------
+bool has_prop(napi_env env, napi_value obj, const char* name, napi_value* out) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, name, &has) != napi_ok || !has) return false;
+  if (napi_get_named_property(env, obj, name, out) != napi_ok) return false;
+  napi_valuetype t;
+  napi_typeof(env, *out, &t);
+  return t != napi_undefined && t != napi_null;
+}
+
+template <class T>
+void typed(napi_env env, napi_value v, napi_typedarray_type want, const char* name, std::vector<T>& out) {
+  bool is = false;
+  napi_is_typedarray(env, v, &is);
+  if (!is) throw ArgError{std::string(name) + " must be a typed array"};
+  napi_typedarray_type t;
+  size_t len = 0;
+  void* data = nullptr;
+  napi_value ab;
+  size_t off = 0;
+  napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+  if (t != want && !(want == napi_uint8_array && t == napi_uint8_clamped_array))
+    throw ArgError{std::string(name) + (want == napi_uint8_array ? " must be a Uint8Array" : " must be a Uint32Array")};
+  out.resize(len);
+  if (len) memcpy(out.data(), data, len * sizeof(T));
+}
+
+template <class T>
+void req_typed(napi_env env, napi_value obj, const char* name, napi_typedarray_type want, std::vector<T>& out) {
+  napi_value v;
+  if (!has_prop(env, obj, name, &v)) throw ArgError{std::string("missing ") + name};
+  typed(env, v, want, name, out);
+}
+
+template <class T>
+bool opt_typed(napi_env env, napi_value obj, const char* name, napi_typedarray_type want, std::vector<T>& out) {
+  napi_value v;
+  if (!has_prop(env, obj, name, &v)) return false;
+  typed(env, v, want, name, out);
+  return true;
+}
+
+void check_offsets(const std::vector<uint32_t>& off, size_t n, uint32_t last, const char* name) {
+  if (off.size() != n + 1) throw ArgError{std::string(name) + ": wrong length"};
+  if (off[0] != 0) throw ArgError{std::string(name) + " must start at 0"};
+  for (size_t i = 0; i < n; i++)
+    if (off[i + 1] < off[i]) throw ArgError{std::string(name) + " not monotone"};
+  if (last != UINT32_MAX && off[n] != last) throw ArgError{std::string(name) + ": wrong end"};
+}
+
+// ---- tasks ---------------------------------------------------------------------
+enum class Kind { Verify, Partial, Finish, SameMessage, SyncPubkeys, AggPubkeys, GtCheck, Close };
+
+struct Task {
+  Kind kind = Kind::Verify;
+  napi_deferred deferred = nullptr;
+  // inputs (copied on the JS thread)
+  std::vector<uint32_t> req_off, pk_off, sig_off, pk_idx, job_off;
+  std::vector<uint8_t> pubkeys, messages, signatures, seed, batchable;
+  bool has_pk_off = false, by_index = false, has_batchable = false;
+  uint32_t n_req = 0, n_sets = 0, n_jobs = 0, pk_len = 0, n_keys = 0;
+  int merged_ok = 0;
+  uint64_t partial_id = 0;
+  // outputs
+  std::vector<uint8_t> valid, err, sst, job_fast, out_bytes;
+  lb_verify_stats stats{0, 0, 0.0};
+  int32_t i32 = 0;
+  uint32_t u32 = 0;
+  uint64_t ticket = 0;
+  uint64_t t_start = 0, t_end = 0;
+  int rc = LB_OK;
+  std::string errmsg;
+  Task* target = nullptr;  // Finish: the two-phase call it resumes
+};
+
+void parse_requests(napi_env env, napi_value obj, Task& t) {
+  napi_valuetype ty;
+  napi_typeof(env, obj, &ty);
+  if (ty != napi_object) throw ArgError{"batch must be an object"};
+  req_typed(env, obj, "requestOffsets", napi_uint32_array, t.req_off);
+  if (t.req_off.empty()) throw ArgError{"requestOffsets: wrong length"};
+  t.n_req = (uint32_t)t.req_off.size() - 1;
+  t.n_sets = t.req_off.back();
+  check_offsets(t.req_off, t.n_req, UINT32_MAX, "requestOffsets");
+  req_typed(env, obj, "messages", napi_uint8_array, t.messages);
+  if (t.messages.size() != (size_t)t.n_sets * 32) throw ArgError{"messages: 32 bytes per set"};
+  req_typed(env, obj, "signatures", napi_uint8_array, t.signatures);
+  req_typed(env, obj, "sigOffsets", napi_uint32_array, t.sig_off);
+  check_offsets(t.sig_off, t.n_sets, (uint32_t)t.signatures.size(), "sigOffsets");
+  req_typed(env, obj, "seed", napi_uint8_array, t.seed);
+  if (t.seed.size() != 32) throw ArgError{"seed must be 32 bytes"};
+  t.has_pk_off = opt_typed(env, obj, "pkOffsets", napi_uint32_array, t.pk_off);
+  if (t.has_pk_off) check_offsets(t.pk_off, t.n_sets, UINT32_MAX, "pkOffsets");
+  const size_t n_pk = t.has_pk_off ? t.pk_off[t.n_sets] : t.n_sets;
+  t.by_index = opt_typed(env, obj, "pubkeyIndices", napi_uint32_array, t.pk_idx);
+  if (t.by_index) {
+    if (t.pk_idx.size() != n_pk) throw ArgError{"pubkeyIndices: one index per pubkey"};
+  } else {
+    if (!opt_typed(env, obj, "pubkeys", napi_uint8_array, t.pubkeys) && n_pk)
+      throw ArgError{"missing pubkeys (or pubkeyIndices)"};
+    if (t.pubkeys.size() != n_pk * LB_PUBKEY_BYTES) throw ArgError{"pubkeys: 96 bytes per pubkey"};
+  }
+  t.has_batchable = opt_typed(env, obj, "batchable", napi_uint8_array, t.batchable);
+  if (t.has_batchable && t.batchable.size() != t.n_req) throw ArgError{"batchable: one flag per request"};
+  if (t.signatures.empty()) t.signatures.push_back(0);
+  if (t.messages.empty()) t.messages.push_back(0);
+  if (t.pubkeys.empty()) t.pubkeys.push_back(0);
+  if (t.pk_idx.empty()) t.pk_idx.push_back(0);
+}
+
+lb_request_batch batch_of(Task& t) {
+  lb_request_batch b{};
+  b.n_requests = t.n_req;
+  b.n_sets = t.n_sets;
+  b.request_offsets = t.req_off.data();
+  b.request_batchable = t.has_batchable ? t.batchable.data() : nullptr;
+  b.pubkeys = t.by_index ? nullptr : t.pubkeys.data();
+  b.pk_offsets = t.has_pk_off ? t.pk_off.data() : nullptr;
+  b.messages = t.messages.data();
+  b.signatures = t.signatures.data();
+  b.sig_offsets = t.sig_off.data();
+  b.seed = t.seed.data();
+  b.pubkey_indices = t.by_index ? t.pk_idx.data() : nullptr;
+  return b;
+}
+
+void alloc_outputs(Task& t) {
+  t.valid.assign(t.n_req ? t.n_req : 1, 0);
+  t.err.assign(t.n_req ? t.n_req : 1, 0);
+  t.sst.assign(t.n_sets ? t.n_sets : 1, 0);
+}
+
+// ---- the per-GPU context ---------------------------------------------------------
+struct Context {
+  lb_ctx* ctx = nullptr;
+  int device = 0;
+  int capacity = 4;
+  napi_env env = nullptr;
+  napi_threadsafe_function tsfn = nullptr;
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Task*> queue;
+  bool closing = false;   // no new work accepted
+  bool finalizing = false;
+  bool joined = false;
+  int pending = 0;        // JS thread only: tasks not yet completed
+  uint64_t next_partial = 1;
+  std::map<uint64_t, Task*> partials;  // worker thread only
+};
+
+void complete(Context* c, Task* t) {
+  if (c->finalizing) {
+    delete t;
+    return;
+  }
+  napi_call_threadsafe_function(c->tsfn, t, napi_tsfn_blocking);
+}
+
+void fail(Task* t, int rc, lb_ctx* ctx) {
+  t->rc = rc;
+  t->errmsg = ctx ? lb_last_error(ctx) : "no context";
+}
+
+// Worker thread: owns c->ctx.
+void worker_loop(Context* c) {
+  std::deque<Task*> inflight;  // submitted, waiting for lb_wait
+  for (;;) {
+    Task* t = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv.wait(lk, [&] { return !c->queue.empty() || !inflight.empty() || c->finalizing; });
+      if (!c->queue.empty() && ((int)inflight.size() < c->capacity || c->queue.front()->kind == Kind::Close)) {
+        t = c->queue.front();
+        c->queue.pop_front();
+      } else if (inflight.empty() && c->finalizing) {
+        break;
+      }
+    }
+    if (!t) {  // retire the oldest call in flight
+      Task* w = inflight.front();
+      inflight.pop_front();
+      Task* owner = w->kind == Kind::Finish ? w->target : w;
+      const int rc = lb_wait(c->ctx, owner->ticket, &owner->stats);
+      if (rc != LB_OK) fail(w, rc, c->ctx);
+      if (w->kind == Kind::Finish) {
+        w->valid.swap(owner->valid);
+        w->err.swap(owner->err);
+        w->sst.swap(owner->sst);
+        w->stats = owner->stats;
+        w->n_req = owner->n_req;
+        w->n_sets = owner->n_sets;
+        w->t_start = owner->t_start;
+        c->partials.erase(owner->partial_id);
+        delete owner;
+      }
+      w->t_end = now_ns();
+      complete(c, w);
+      continue;
+    }
+    t->t_start = now_ns();
+    switch (t->kind) {
+      case Kind::Verify: {
+        alloc_outputs(*t);
+        lb_request_batch b = batch_of(*t);
+        const int rc = lb_verify_requests_async(c->ctx, &b, t->valid.data(), t->err.data(), t->sst.data(), &t->ticket);
+        if (rc != LB_OK) {
+          fail(t, rc, c->ctx);
+          complete(c, t);
+        } else {
+          inflight.push_back(t);
+        }
+        break;
+      }
+      case Kind::Partial: {
+        // the two-phase call stays in the map (its outputs are written when it
+        // retires); the JS promise resolves with its partial
+        Task* call = new Task(std::move(*t));
+        call->deferred = nullptr;
+        alloc_outputs(*call);
+        lb_request_batch b = batch_of(*call);
+        int rc = lb_verify_requests_partial_async(c->ctx, &b, 0, call->valid.data(), call->err.data(),
+                                                  call->sst.data(), &call->ticket);
+        t->out_bytes.assign(LB_GT_BYTES, 0);
+        if (rc == LB_OK) rc = lb_partial_wait(c->ctx, call->ticket, t->out_bytes.data());
+        if (rc != LB_OK) {
+          fail(t, rc, c->ctx);
+          delete call;
+        } else {
+          call->partial_id = t->partial_id;
+          c->partials[t->partial_id] = call;
+        }
+        complete(c, t);
+        break;
+      }
+      case Kind::Finish: {
+        auto it = c->partials.find(t->partial_id);
+        if (it == c->partials.end()) {
+          t->rc = LB_ERR_INVALID_ARGUMENT;
+          t->errmsg = "unknown or already finished two-phase call";
+          complete(c, t);
+          break;
+        }
+        t->target = it->second;
+        // a call whose slot was reused meanwhile has already resumed with merged_ok = 0
+        (void)lb_verify_requests_finish(c->ctx, t->target->ticket, t->merged_ok);
+        inflight.push_back(t);
+        break;
+      }
+      case Kind::SameMessage: {
+        lb_same_message_batch b{};
+        b.n_jobs = t->n_jobs;
+        b.n_sets = t->n_sets;
+        b.job_offsets = t->job_off.data();
+        b.pubkeys = t->by_index ? nullptr : t->pubkeys.data();
+        b.pubkey_indices = t->by_index ? t->pk_idx.data() : nullptr;
+        b.signatures = t->signatures.data();
+        b.sig_offsets = t->sig_off.data();
+        b.messages = t->messages.data();
+        b.seed = t->seed.data();
+        t->valid.assign(t->n_sets ? t->n_sets : 1, 0);
+        t->job_fast.assign(t->n_jobs ? t->n_jobs : 1, 0);
+        const int rc = lb_verify_same_message_batch(c->ctx, &b, t->valid.data(), t->job_fast.data(), &t->stats);
+        if (rc != LB_OK) fail(t, rc, c->ctx);
+        t->t_end = now_ns();
+        complete(c, t);
+        break;
+      }
+      case Kind::SyncPubkeys: {
+        int32_t bad = -1;
+        const int rc = lb_pubkey_table_append(c->ctx, t->n_keys, t->pubkeys.data(), t->pk_len, &bad);
+        if (rc != LB_OK) {
+          fail(t, rc, c->ctx);
+          if (bad >= 0) t->errmsg += " (pubkey " + std::to_string(bad) + ")";
+        } else {
+          lb_pubkey_table_size(c->ctx, &t->u32);
+        }
+        complete(c, t);
+        break;
+      }
+      case Kind::AggPubkeys: {
+        t->out_bytes.assign(LB_PUBKEY_BYTES, 0);
+        uint8_t st = 0;
+        const int rc = t->by_index
+                           ? lb_aggregate_pubkeys_indexed(c->ctx, t->n_keys, t->pk_idx.data(), t->out_bytes.data(), &st)
+                           : lb_aggregate_pubkeys(c->ctx, t->n_keys, t->pubkeys.data(), t->out_bytes.data(), &st);
+        if (rc != LB_OK)
+          fail(t, rc, c->ctx);
+        else if (st != LB_SET_OK) {
+          t->rc = LB_ERR_INVALID_ARGUMENT;
+          t->errmsg = "invalid pubkey";
+        }
+        complete(c, t);
+        break;
+      }
+      case Kind::GtCheck: {
+        const int rc = lb_gt_check(c->ctx, t->n_keys, t->out_bytes.data(), &t->i32);
+        if (rc != LB_OK) fail(t, rc, c->ctx);
+        complete(c, t);
+        break;
+      }
+      case Kind::Close: {
+        while (!inflight.empty()) {  // never destroy the context under a call in flight
+          Task* w = inflight.front();
+          inflight.pop_front();
+          Task* owner = w->kind == Kind::Finish ? w->target : w;
+          const int rc = lb_wait(c->ctx, owner->ticket, &owner->stats);
+          if (rc != LB_OK) fail(w, rc, c->ctx);
+          if (w->kind == Kind::Finish) {
+            w->valid.swap(owner->valid);
+            w->err.swap(owner->err);
+            w->sst.swap(owner->sst);
+            w->stats = owner->stats;
+            w->n_req = owner->n_req;
+            w->n_sets = owner->n_sets;
+            c->partials.erase(owner->partial_id);
+            delete owner;
+          }
+          complete(c, w);
+        }
+        for (auto& kv : c->partials) delete kv.second;
+        c->partials.clear();
+        lb_destroy(c->ctx);
+        c->ctx = nullptr;
+        complete(c, t);
+        return;
+      }
+    }
+  }
+  // finalizer path (Context garbage-collected without close())
+  for (Task* w : inflight) {
+    Task* owner = w->kind == Kind::Finish ? w->target : w;
+    lb_wait(c->ctx, owner->ticket, nullptr);
+    delete w;
+  }
+  for (auto& kv : c->partials) delete kv.second;
+  lb_destroy(c->ctx);
+  c->ctx = nullptr;
+}
+
+// ---- JS side -----------------------------------------------------------------------
+napi_value make_u8(napi_env env, const uint8_t* p, size_t n) {
+  napi_value ab, arr;
+  void* data = nullptr;
+  NAPI_OK(napi_create_arraybuffer(env, n, &data, &ab));
+  if (n) memcpy(data, p, n);
+  NAPI_OK(napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &arr));
+  return arr;
+}
+
+void set_num(napi_env env, napi_value obj, const char* k, double v) {
+  napi_value x;
+  napi_create_double(env, v, &x);
+  napi_set_named_property(env, obj, k, x);
+}
+
+napi_value make_error(napi_env env, int rc, const std::string& msg) {
+  const char* code = rc == LB_ERR_INVALID_ARGUMENT ? "LB_ERR_INVALID_ARGUMENT"
+                     : rc == LB_ERR_DEVICE         ? "LB_ERR_DEVICE"
+                     : rc == LB_ERR_NO_DEVICE      ? "LB_ERR_NO_DEVICE"
+                     : rc == LB_ERR_OUT_OF_MEMORY  ? "LB_ERR_OUT_OF_MEMORY"
+                                                   : "LB_ERR";
+  napi_value c, m, e;
+  napi_create_string_utf8(env, code, NAPI_AUTO_LENGTH, &c);
+  napi_create_string_utf8(env, msg.c_str(), NAPI_AUTO_LENGTH, &m);
+  napi_create_error(env, c, m, &e);
+  return e;
+}
+
+napi_value verify_result(napi_env env, Task* t) {
+  napi_value o;
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "valid", make_u8(env, t->valid.data(), t->n_req));
+  napi_set_named_property(env, o, "errors", make_u8(env, t->err.data(), t->n_req));
+  napi_set_named_property(env, o, "setStatus", make_u8(env, t->sst.data(), t->n_sets));
+  set_num(env, o, "batchRetries", t->stats.batch_retries);
+  set_num(env, o, "batchSigsSuccess", t->stats.batch_sigs_success);
+  set_num(env, o, "deviceMs", t->stats.device_ms);
+  set_num(env, o, "workerStartNs", (double)t->t_start);
+  set_num(env, o, "workerEndNs", (double)t->t_end);
+  return o;
+}
+
+void call_js(napi_env env, napi_value /*cb*/, void* context, void* data) {
+  Context* c = static_cast<Context*>(context);
+  Task* t = static_cast<Task*>(data);
+  if (env == nullptr) {  // environment tearing down
+    delete t;
+    return;
+  }
+  napi_value result = nullptr;
+  if (t->rc != LB_OK) {
+    napi_reject_deferred(env, t->deferred, make_error(env, t->rc, t->errmsg));
+  } else {
+    switch (t->kind) {
+      case Kind::Verify:
+      case Kind::Finish:
+        result = verify_result(env, t);
+        break;
+      case Kind::Partial: {
+        napi_create_object(env, &result);
+        set_num(env, result, "id", (double)t->partial_id);
+        napi_set_named_property(env, result, "partial", make_u8(env, t->out_bytes.data(), LB_GT_BYTES));
+        break;
+      }
+      case Kind::SameMessage:
+        napi_create_object(env, &result);
+        napi_set_named_property(env, result, "valid", make_u8(env, t->valid.data(), t->n_sets));
+        napi_set_named_property(env, result, "jobFast", make_u8(env, t->job_fast.data(), t->n_jobs));
+        set_num(env, result, "retriedJobs", t->stats.batch_retries);
+        set_num(env, result, "fastSets", t->stats.batch_sigs_success);
+        set_num(env, result, "deviceMs", t->stats.device_ms);
+        set_num(env, result, "workerStartNs", (double)t->t_start);
+        set_num(env, result, "workerEndNs", (double)t->t_end);
+        break;
+      case Kind::SyncPubkeys:
+        napi_create_uint32(env, t->u32, &result);
+        break;
+      case Kind::AggPubkeys:
+        result = make_u8(env, t->out_bytes.data(), LB_PUBKEY_BYTES);
+        break;
+      case Kind::GtCheck:
+        napi_get_boolean(env, t->i32 != 0, &result);
+        break;
+      case Kind::Close:
+        napi_get_undefined(env, &result);
+        break;
+    }
+    napi_resolve_deferred(env, t->deferred, result);
+  }
+  const bool closed = t->kind == Kind::Close;
+  delete t;
+  if (--c->pending == 0 && !closed) napi_unref_threadsafe_function(env, c->tsfn);
+  if (closed) {
+    if (c->worker.joinable()) c->worker.join();
+    c->joined = true;
+    napi_release_threadsafe_function(c->tsfn, napi_tsfn_release);
+    c->tsfn = nullptr;
+  }
+}
+
+Context* unwrap(napi_env env, napi_callback_info info, size_t* argc, napi_value* argv) {
+  napi_value self;
+  napi_get_cb_info(env, info, argc, argv, &self, nullptr);
+  void* p = nullptr;
+  napi_unwrap(env, self, &p);
+  return static_cast<Context*>(p);
+}
+
+// Queue a task; returns its promise (rejected at once when the context is closed).
+napi_value submit(napi_env env, Context* c, Task* t) {
+  napi_value promise;
+  napi_create_promise(env, &t->deferred, &promise);
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->closing) {
+      napi_reject_deferred(env, t->deferred, make_error(env, LB_ERR_INVALID_ARGUMENT, "QUEUE_ERROR_QUEUE_ABORTED: context closed"));
+      delete t;
+      return promise;
+    }
+    if (t->kind == Kind::Close) c->closing = true;
+    c->queue.push_back(t);
+  }
+  if (c->pending++ == 0) napi_ref_threadsafe_function(env, c->tsfn);
+  c->cv.notify_one();
+  return promise;
+}
+
+napi_value rejected(napi_env env, const std::string& msg) {
+  napi_deferred d;
+  napi_value promise, m, e;
+  napi_create_promise(env, &d, &promise);
+  napi_create_string_utf8(env, msg.c_str(), NAPI_AUTO_LENGTH, &m);
+  napi_create_type_error(env, nullptr, m, &e);
+  napi_reject_deferred(env, d, e);
+  return promise;
+}
+
+napi_value m_verify(napi_env env, napi_callback_info info, Kind kind) {
+  size_t argc = 1;
+  napi_value argv[1];
+  Context* c = unwrap(env, info, &argc, argv);
+  if (!c) return rejected(env, "not a Context");
+  Task* t = new Task();
+  t->kind = kind;
+  try {
+    if (argc < 1) throw ArgError{"verifyRequests(batch)"};
+    parse_requests(env, argv[0], *t);
+  } catch (const ArgError& e) {
+    delete t;
+    return rejected(env, e.msg);
+  }
+  if (kind == Kind::Partial) t->partial_id = c->next_partial++;
+  return submit(env, c, t);
+}
+napi_value VerifyRequests(napi_env env, napi_callback_info info) { return m_verify(env, info, Kind::Verify); }
+napi_value VerifyRequestsPartial(napi_env env, napi_callback_info info) { return m_verify(env, info, Kind::Partial); }
+
+napi_value Finish(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  Context* c = unwrap(env, info, &argc, argv);
+  if (!c || argc < 2) return rejected(env, "finish(id, mergedOk)");
+  double id = 0;
+  bool ok = false;
+  if (napi_get_value_double(env, argv[0], &id) != napi_ok || napi_get_value_bool(env, argv[1], &ok) != napi_ok)
+    return rejected(env, "finish(id: number, mergedOk: boolean)");
+  Task* t = new Task();
+  t->kind = Kind::Finish;
+  t->partial_id = (uint64_t)id;
+  t->merged_ok = ok ? 1 : 0;
+  return submit(env, c, t);
+}
+
+napi_value GtCheck(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  Context* c = unwrap(env, info, &argc, argv);
+  Task* t = new Task();
+  t->kind = Kind::GtCheck;
+  try {
+    if (!c || argc < 1) throw ArgError{"gtCheck(partials: Uint8Array)"};
+    typed(env, argv[0], napi_uint8_array, "partials", t->out_bytes);
+    if (t->out_bytes.size() % LB_GT_BYTES) throw ArgError{"partials: 576 bytes each"};
+    t->n_keys = (uint32_t)(t->out_bytes.size() / LB_GT_BYTES);
+    if (t->out_bytes.empty()) t->out_bytes.push_back(0);
+  } catch (const ArgError& e) {
+    delete t;
+    return rejected(env, e.msg);
+  }
+  return submit(env, c, t);
+}
+
+napi_value VerifySameMessage(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  Context* c = unwrap(env, info, &argc, argv);
+  Task* t = new Task();
+  t->kind = Kind::SameMessage;
+  try {
+    if (!c || argc < 1) throw ArgError{"verifySameMessage(batch)"};
+    napi_value o = argv[0];
+    req_typed(env, o, "jobOffsets", napi_uint32_array, t->job_off);
+    if (t->job_off.empty()) throw ArgError{"jobOffsets: wrong length"};
+    t->n_jobs = (uint32_t)t->job_off.size() - 1;
+    t->n_sets = t->job_off.back();
+    check_offsets(t->job_off, t->n_jobs, UINT32_MAX, "jobOffsets");
+    req_typed(env, o, "signatures", napi_uint8_array, t->signatures);
+    req_typed(env, o, "sigOffsets", napi_uint32_array, t->sig_off);
+    check_offsets(t->sig_off, t->n_sets, (uint32_t)t->signatures.size(), "sigOffsets");
+    req_typed(env, o, "messages", napi_uint8_array, t->messages);
+    if (t->messages.size() != (size_t)t->n_jobs * 32) throw ArgError{"messages: 32 bytes per job"};
+    req_typed(env, o, "seed", napi_uint8_array, t->seed);
+    if (t->seed.size() != 32) throw ArgError{"seed must be 32 bytes"};
+    t->by_index = opt_typed(env, o, "pubkeyIndices", napi_uint32_array, t->pk_idx);
+    if (t->by_index) {
+      if (t->pk_idx.size() != t->n_sets) throw ArgError{"pubkeyIndices: one per set"};
+    } else {
+      if (!opt_typed(env, o, "pubkeys", napi_uint8_array, t->pubkeys) && t->n_sets)
+        throw ArgError{"missing pubkeys (or pubkeyIndices)"};
+      if (t->pubkeys.size() != (size_t)t->n_sets * LB_PUBKEY_BYTES) throw ArgError{"pubkeys: 96 bytes per set"};
+    }
+    for (auto* v : {&t->signatures, &t->messages, &t->pubkeys}) if (v->empty()) v->push_back(0);
+    if (t->pk_idx.empty()) t->pk_idx.push_back(0);
+  } catch (const ArgError& e) {
+    delete t;
+    return rejected(env, e.msg);
+  }
+  return submit(env, c, t);
+}
+
+napi_value SyncPubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  Context* c = unwrap(env, info, &argc, argv);
+  Task* t = new Task();
+  t->kind = Kind::SyncPubkeys;
+  try {
+    if (!c || argc < 2) throw ArgError{"syncPubkeys(keys: Uint8Array, pkLen: 48 | 96)"};
+    typed(env, argv[0], napi_uint8_array, "keys", t->pubkeys);
+    napi_get_value_uint32(env, argv[1], &t->pk_len);
+    if (t->pk_len != 48 && t->pk_len != 96) throw ArgError{"pkLen must be 48 or 96"};
+    if (t->pubkeys.size() % t->pk_len) throw ArgError{"keys: a whole number of keys"};
+    t->n_keys = (uint32_t)(t->pubkeys.size() / t->pk_len);
+    if (t->pubkeys.empty()) t->pubkeys.push_back(0);
+  } catch (const ArgError& e) {
+    delete t;
+    return rejected(env, e.msg);
+  }
+  return submit(env, c, t);
+}
+
+napi_value AggregatePubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  Context* c = unwrap(env, info, &argc, argv);
+  Task* t = new Task();
+  t->kind = Kind::AggPubkeys;
+  try {
+    if (!c || argc < 1) throw ArgError{"aggregatePubkeys(keys: Uint8Array | indices: Uint32Array)"};
+    napi_typedarray_type ty;
+    size_t len;
+    void* d;
+    napi_value ab;
+    size_t off;
+    bool is = false;
+    napi_is_typedarray(env, argv[0], &is);
+    if (!is) throw ArgError{"aggregatePubkeys expects a typed array"};
+    napi_get_typedarray_info(env, argv[0], &ty, &len, &d, &ab, &off);
+    t->by_index = ty == napi_uint32_array;
+    if (t->by_index) {
+      typed(env, argv[0], napi_uint32_array, "indices", t->pk_idx);
+      t->n_keys = (uint32_t)t->pk_idx.size();
+    } else {
+      typed(env, argv[0], napi_uint8_array, "keys", t->pubkeys);
+      if (t->pubkeys.size() % LB_PUBKEY_BYTES) throw ArgError{"keys: 96 bytes each"};
+      t->n_keys = (uint32_t)(t->pubkeys.size() / LB_PUBKEY_BYTES);
+    }
+    if (t->n_keys == 0) throw ArgError{"EMPTY_AGGREGATE_ARRAY"};
+  } catch (const ArgError& e) {
+    delete t;
+    return rejected(env, e.msg);
+  }
+  return submit(env, c, t);
+}
+
+napi_value Close(napi_env env, napi_callback_info info) {
+  size_t argc = 0;
+  Context* c = unwrap(env, info, &argc, nullptr);
+  if (!c) return rejected(env, "not a Context");
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->closing) {  // second close(): already resolved or pending
+      napi_deferred d;
+      napi_value p, u;
+      napi_create_promise(env, &d, &p);
+      napi_get_undefined(env, &u);
+      napi_resolve_deferred(env, d, u);
+      return p;
+    }
+  }
+  Task* t = new Task();
+  t->kind = Kind::Close;
+  return submit(env, c, t);
+}
+
+void finalize_ctx(napi_env env, void* data, void* /*hint*/) {
+  Context* c = static_cast<Context*>(data);
+  if (!c->joined) {
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->finalizing = true;
+      c->closing = true;
+      for (Task* t : c->queue) delete t;
+      c->queue.clear();
+    }
+    c->cv.notify_one();
+    if (c->worker.joinable()) c->worker.join();
+    if (c->tsfn) napi_release_threadsafe_function(c->tsfn, napi_tsfn_abort);
+  }
+  delete c;
+}
+
+napi_value New(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], self;
+  napi_get_cb_info(env, info, &argc, argv, &self, nullptr);
+  int32_t device = 0;
+  if (argc >= 1) napi_get_value_int32(env, argv[0], &device);
+  int32_t capacity = 4;
+  napi_value v;
+  if (argc >= 2 && has_prop(env, argv[1], "capacity", &v)) napi_get_value_int32(env, v, &capacity);
+  lb_ctx* ctx = nullptr;
+  const int rc = lb_create(device, &ctx);
+  if (rc != LB_OK) {
+    napi_throw(env, make_error(env, rc, "lb_create(" + std::to_string(device) + ") failed: no usable HIP device"));
+    return nullptr;
+  }
+  Context* c = new Context();
+  c->ctx = ctx;
+  c->device = device;
+  c->capacity = capacity < 1 ? 1 : capacity;
+  c->env = env;
+  napi_value name;
+  napi_create_string_utf8(env, "lodestar_bls_gpu", NAPI_AUTO_LENGTH, &name);
+  napi_create_threadsafe_function(env, nullptr, nullptr, name, 0, 1, nullptr, nullptr, c, call_js, &c->tsfn);
+  napi_unref_threadsafe_function(env, c->tsfn);  // idle contexts do not keep the process alive
+  c->worker = std::thread(worker_loop, c);
+  napi_wrap(env, self, c, finalize_ctx, nullptr, nullptr);
+  napi_value dev;
+  napi_create_int32(env, device, &dev);
+  napi_set_named_property(env, self, "device", dev);
+  return self;
+}
+
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+  napi_value r;
+  napi_create_int32(env, lb_device_count(), &r);
+  return r;
+}
+
+// Marshalling dry run (no device): the same checks verifyRequests applies.
+napi_value ValidateRequests(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  Task t;
+  try {
+    if (argc < 1) throw ArgError{"validateRequests(batch)"};
+    parse_requests(env, argv[0], t);
+  } catch (const ArgError& e) {
+    napi_throw_type_error(env, nullptr, e.msg.c_str());
+    return nullptr;
+  }
+  napi_value o;
+  napi_create_object(env, &o);
+  set_num(env, o, "nRequests", t.n_req);
+  set_num(env, o, "nSets", t.n_sets);
+  set_num(env, o, "nPubkeys", t.has_pk_off ? t.pk_off[t.n_sets] : t.n_sets);
+  napi_value b;
+  napi_get_boolean(env, t.by_index, &b);
+  napi_set_named_property(env, o, "byIndex", b);
+  return o;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor methods[] = {
+      {"verifyRequests", nullptr, VerifyRequests, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"verifyRequestsPartial", nullptr, VerifyRequestsPartial, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"finish", nullptr, Finish, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"gtCheck", nullptr, GtCheck, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"verifySameMessage", nullptr, VerifySameMessage, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"syncPubkeys", nullptr, SyncPubkeys, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"aggregatePubkeys", nullptr, AggregatePubkeys, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_value cls;
+  napi_define_class(env, "Context", NAPI_AUTO_LENGTH, New, nullptr, sizeof(methods) / sizeof(methods[0]), methods,
+                    &cls);
+  napi_set_named_property(env, exports, "Context", cls);
+  napi_value f;
+  napi_create_function(env, "deviceCount", NAPI_AUTO_LENGTH, DeviceCount, nullptr, &f);
+  napi_set_named_property(env, exports, "deviceCount", f);
+  napi_create_function(env, "validateRequests", NAPI_AUTO_LENGTH, ValidateRequests, nullptr, &f);
+  napi_set_named_property(env, exports, "validateRequests", f);
+  napi_value sz;
+  napi_create_int32(env, LB_GT_BYTES, &sz);
+  napi_set_named_property(env, exports, "GT_BYTES", sz);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -1,0 +1,271 @@
+"use strict";
+// BlsGpuVerifier scheduling semantics with a mock backend (the pattern of the
+// reference's test/mocks/mockedBls.ts), on node without a GPU:
+// chunking, buffering, priority, same-message flattening, rejection rules,
+// close(), metrics, the worker's batch accounting and the sharded combine.
+const assert = require("assert");
+const path = require("path");
+const V = require(path.join(__dirname, "..", "..", "lodestar_amd", "js", "bls_gpu_verifier.js"));
+
+const GOOD = new Uint8Array(96).fill(1);
+const BAD = new Uint8Array(96).fill(2);
+const PK = new Uint8Array(96);
+
+class MockBackend {
+  constructor(capacity = 1) {
+    this.capacity = capacity;
+    this.dispatches = [];
+    this.sameCalls = [];
+    this.closed = false;
+    this.partials = new Map();
+    this.nextId = 1;
+  }
+  verdicts(b) {
+    const nReq = b.requestOffsets.length - 1;
+    const valid = new Uint8Array(nReq);
+    const errors = new Uint8Array(nReq);
+    const sizes = [];
+    for (let k = 0; k < nReq; k++) {
+      const a = b.requestOffsets[k];
+      const e = b.requestOffsets[k + 1];
+      sizes.push(e - a);
+      let ok = e > a;
+      for (let i = a; i < e; i++) {
+        if (b.pkOffsets && b.pkOffsets[i + 1] === b.pkOffsets[i]) errors[k] = 1;
+        if (b.signatures[b.sigOffsets[i]] !== 1) ok = false;
+      }
+      valid[k] = ok ? 1 : 0;
+    }
+    return {valid, errors, sizes};
+  }
+  async verifyRequests(b) {
+    assert(!this.closed);
+    const {valid, errors, sizes} = this.verdicts(b);
+    this.dispatches.push(sizes);
+    await new Promise((r) => setTimeout(r, 1));
+    return {valid, errors, setStatus: new Uint8Array(0), batchRetries: 0, batchSigsSuccess: 0, deviceMs: 0};
+  }
+  async verifySameMessage(b) {
+    const nJobs = b.jobOffsets.length - 1;
+    const nSets = b.jobOffsets[nJobs];
+    const valid = new Uint8Array(nSets);
+    const jobFast = new Uint8Array(nJobs);
+    for (let i = 0; i < nSets; i++) valid[i] = b.signatures[b.sigOffsets[i]] === 1 ? 1 : 0;
+    for (let j = 0; j < nJobs; j++) {
+      this.sameCalls.push(b.jobOffsets[j + 1] - b.jobOffsets[j]);
+      jobFast[j] = valid.subarray(b.jobOffsets[j], b.jobOffsets[j + 1]).every((v) => v === 1) ? 1 : 0;
+    }
+    return {valid, jobFast, retriedJobs: 0, fastSets: 0, deviceMs: 0};
+  }
+  // two-phase protocol (addon Context.verifyRequestsPartial / gtCheck / finish)
+  async verifyRequestsPartial(b) {
+    const v = this.verdicts(b);
+    const id = this.nextId++;
+    this.partials.set(id, v);
+    const partial = new Uint8Array(576);
+    partial[0] = v.valid.every((x) => x === 1) ? 1 : 0;
+    return {id, partial};
+  }
+  async gtCheck(partials) {
+    for (let i = 0; i < partials.length; i += 576) if (partials[i] !== 1) return false;
+    return true;
+  }
+  async finish(id, ok) {
+    const v = this.partials.get(id);
+    this.partials.delete(id);
+    this.lastFinish = ok;
+    return {valid: v.valid, errors: v.errors};
+  }
+  async close() {
+    this.closed = true;
+  }
+}
+
+function sets(n, bad = new Set()) {
+  const out = [];
+  for (let i = 0; i < n; i++)
+    out.push({type: "single", pubkey: PK, signingRoot: new Uint8Array(32).fill(i % 256), signature: bad.has(i) ? BAD : GOOD});
+  return out;
+}
+const seed = () => new Uint8Array(32);
+
+const tests = [];
+function test(name, fn) {
+  tests.push([name, fn]);
+}
+
+test("chunkify matches the reference", () => {
+  const r = (n, m) => V.chunkifyMaximizeChunkSize(Array.from({length: n}, (_, i) => i), m).map((c) => c.length);
+  assert.deepStrictEqual(r(300, 128), [150, 150]);
+  assert.deepStrictEqual(r(100, 128), [100]);
+  assert.deepStrictEqual(r(0, 128), [0]);
+});
+
+test("valid and invalid calls", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  assert.strictEqual(await v.verifySignatureSets(sets(3)), true);
+  assert.strictEqual(await v.verifySignatureSets(sets(3, new Set([1]))), false);
+  await v.close();
+});
+
+test("large call chunked into jobs of <= 128", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  assert.strictEqual(await v.verifySignatureSets(sets(300)), true);
+  assert.deepStrictEqual(b.dispatches.flat().sort(), [150, 150]);
+  await v.close();
+});
+
+test("batchable calls buffered into one package", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  const opts = {batchable: true};
+  const r = await Promise.all([
+    v.verifySignatureSets(sets(3), opts),
+    v.verifySignatureSets(sets(4), opts),
+    v.verifySignatureSets(sets(2, new Set([0])), opts),
+  ]);
+  assert.deepStrictEqual(r, [true, true, false]);
+  assert.deepStrictEqual(b.dispatches, [[3, 4, 2]]);
+  await v.close();
+});
+
+test("batchable waits for the buffer timeout, > 32 sigs flushes at once", async () => {
+  const v = new V.BlsGpuVerifier({backends: [new MockBackend()], seedSource: seed});
+  let t0 = Date.now();
+  await v.verifySignatureSets(sets(2), {batchable: true});
+  assert(Date.now() - t0 >= V.MAX_BUFFER_WAIT_MS * 0.9);
+  t0 = Date.now();
+  await v.verifySignatureSets(sets(33), {batchable: true});
+  assert(Date.now() - t0 < V.MAX_BUFFER_WAIT_MS / 2);
+  await v.close();
+});
+
+test("priority jobs run first", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed, maxSetsPerDispatch: 1});
+  const hold = v.idle;
+  v.idle = [];
+  const f1 = v.verifySignatureSets(sets(2));
+  const f2 = v.verifySignatureSets(sets(5), {priority: true});
+  await new Promise((r) => setTimeout(r, 5));
+  v.idle = hold;
+  v.runJob();
+  await Promise.all([f1, f2]);
+  assert.deepStrictEqual(b.dispatches[0], [5]);
+  await v.close();
+});
+
+test("empty aggregate rejects the job; empty sets are false", async () => {
+  const v = new V.BlsGpuVerifier({backends: [new MockBackend()], seedSource: seed});
+  await assert.rejects(
+    v.verifySignatureSets([{type: "aggregate", pubkeys: [], signingRoot: new Uint8Array(32), signature: GOOD}]),
+    /EMPTY_AGGREGATE_ARRAY/
+  );
+  assert.strictEqual(await v.verifySignatureSets([]), false);
+  await v.close();
+});
+
+test("same-message chunks flatten; one package, one device call", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  const pairs = [];
+  for (let i = 0; i < 300; i++) pairs.push({publicKey: PK, signature: i === 299 ? BAD : GOOD});
+  const out = await v.verifySignatureSetsSameMessage(pairs, new Uint8Array(32));
+  assert.deepStrictEqual(out, Array(299).fill(true).concat([false]));
+  assert.deepStrictEqual(b.sameCalls.sort(), [150, 150]);
+  assert.deepStrictEqual(await v.verifySignatureSetsSameMessage([], new Uint8Array(32)), []);
+  assert.strictEqual(v.metrics.get(V.METRICS.SAME_MESSAGE_RETRY_JOBS), 1);
+  await v.close();
+});
+
+test("close rejects queued jobs and new work, waits for packages in flight", async () => {
+  const b = new MockBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  const f = v.verifySignatureSets(sets(2), {batchable: true});
+  await v.close();
+  await assert.rejects(f, (e) => e instanceof V.QueueError);
+  await assert.rejects(v.verifySignatureSets(sets(1)), (e) => e instanceof V.QueueError);
+  assert(b.closed);
+});
+
+test("canAcceptWork and several GPUs share the load", async () => {
+  const bs = [new MockBackend(2), new MockBackend(2)];
+  const v = new V.BlsGpuVerifier({backends: bs, seedSource: seed, maxSetsPerDispatch: 128});
+  assert(v.canAcceptWork());
+  assert.strictEqual(v.capacity, 4);
+  const r = await Promise.all(Array.from({length: 6}, () => v.verifySignatureSets(sets(128))));
+  assert(r.every((x) => x));
+  assert(bs.every((b) => b.dispatches.length > 0));
+  await v.close();
+});
+
+test("pubkeys by validator index ship as indices", () => {
+  const s1 = {type: "single", pubkey: {index: 4}, signingRoot: new Uint8Array(32), signature: GOOD};
+  const s2 = {type: "aggregate", pubkeys: [{index: 1}, {index: 2}], signingRoot: new Uint8Array(32), signature: GOOD};
+  const b = V.packRequests([[s1, s2]], new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(b.pubkeyIndices), [4, 1, 2]);
+  assert.deepStrictEqual(Array.from(b.pkOffsets), [0, 1, 3]);
+  assert.strictEqual(b.pubkeys, undefined);
+  assert.throws(() => V.packRequests([[{...s1, signingRoot: new Uint8Array(31)}]], new Uint8Array(32)), TypeError);
+});
+
+test("worker batch accounting (worker.ts:41-85)", () => {
+  const w = V.workerBatchStats;
+  assert.deepStrictEqual(w(Array(10).fill(3), Array(10).fill(true), Array(10).fill(true)), {retries: 0, sigsOk: 30});
+  const v = Array(40).fill(true);
+  v[25] = false;
+  assert.deepStrictEqual(w(Array(40).fill(2), Array(40).fill(true), v), {retries: 1, sigsOk: 40});
+  assert.deepStrictEqual(w([5, 5], [false, false], [false, true]), {retries: 0, sigsOk: 0});
+});
+
+test("metrics carry the reference's names", async () => {
+  const v = new V.BlsGpuVerifier({backends: [new MockBackend()], seedSource: seed});
+  await v.verifySignatureSets(sets(300), {batchable: true, priority: true});
+  const M = V.METRICS;
+  assert.strictEqual(v.metrics.get(M.TOTAL_SIG_SETS), 300);
+  assert.strictEqual(v.metrics.get(M.BATCHABLE_SIG_SETS), 300);
+  assert.strictEqual(v.metrics.get(M.SIG_SETS_STARTED, {type: "default"}), 300);
+  assert.strictEqual(v.metrics.get(M.BATCH_SIGS_SUCCESS), 300);
+  assert.strictEqual(v.metrics.get(M.JOBS_STARTED, {type: "default"}), 2);
+  await v.close();
+});
+
+test("sharded call combines the shards' partials", async () => {
+  const reqs = [];
+  for (let k = 0; k < 9; k++) reqs.push(sets(k % 4 + 1));
+  let bs = [new MockBackend(), new MockBackend(), new MockBackend()];
+  let r = await V.verifyRequestsSharded(bs, reqs, seed);
+  assert.strictEqual(r.mergedOk, true);
+  assert(Array.from(r.valid).every((x) => x === 1));
+  assert(bs.every((b) => b.lastFinish === true));
+  reqs[5] = sets(2, new Set([1]));
+  bs = [new MockBackend(), new MockBackend()];
+  r = await V.verifyRequestsSharded(bs, reqs, seed);
+  assert.strictEqual(r.mergedOk, false);
+  assert.deepStrictEqual(Array.from(r.valid), [1, 1, 1, 1, 1, 0, 1, 1, 1]);
+});
+
+test("single-thread verifier", async () => {
+  const v = new V.BlsGpuSingleThreadVerifier({backend: new MockBackend(), seedSource: seed});
+  assert.strictEqual(await v.verifySignatureSets(sets(2)), true);
+  assert.deepStrictEqual(await v.verifySignatureSetsSameMessage([{publicKey: PK, signature: BAD}], new Uint8Array(32)), [false]);
+  await assert.rejects(v.verifySignatureSetsSameMessage([], new Uint8Array(32)), /EMPTY_AGGREGATE_ARRAY/);
+  assert(v.canAcceptWork());
+});
+
+(async () => {
+  let failed = 0;
+  for (const [name, fn] of tests) {
+    try {
+      await fn();
+      console.log("ok   " + name);
+    } catch (e) {
+      failed++;
+      console.log("FAIL " + name + "\n" + (e && e.stack));
+    }
+  }
+  console.log(`${tests.length - failed} passed, ${failed} failed`);
+  process.exit(failed ? 1 : 0);
+})();
