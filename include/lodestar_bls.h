@@ -21,7 +21,13 @@
  *   lb_aggregate_signatures <- Signature.fromBytes(validate) x n + bls.Signature.aggregate(sigs).toBytes()
  *                              (jobItem.ts:73,81)
  *   lb_create / lb_destroy  <- BlsMultiThreadWorkerPool constructor / close() (index.ts:132-153,244-265)
+ *   lb_verify_requests_partial_async .. lb_gt_check  <- the pool's fan-out over workers
+ *                              (index.ts:191-205) as a multi-GPU combine of Fp12 partials
+ *   lb_verify_same_message_batch <- every same-message job of a worker package
+ *                              (jobItem.ts:64-125, index.ts:455-489,557-568)
  *
+ * The Lodestar-side binding is the N-API addon lodestar_amd/napi/addon.cc
+ * (INTEGRATION.md).
  * Threading: a context is bound to one GPU and is not thread-safe; use one
  * context per host submission thread (one process per GPU for multi-GPU).
  */
@@ -119,8 +125,11 @@ typedef struct {
 } lb_request_batch;
 
 typedef struct {
-  uint32_t batch_retries;      /* merged checks that failed, so requests were re-verified alone
-                                  (worker.ts:80; 0 or 1 per call, 0 below LB_MERGE_MIN requests) */
+  uint32_t batch_retries;      /* the DEVICE's merged check: 1 when it failed and requests were
+                                  re-verified alone, else 0 (0 below LB_MERGE_MIN requests).  The
+                                  reference counts per 16-request chunk of batchable requests
+                                  (worker.ts:54,75); the hosts derive that figure from the verdicts
+                                  (verifier.worker_batch_stats, js workerBatchStats) for the metric */
   uint32_t batch_sigs_success; /* sets verified inside a passing merged check (worker.ts:71)   */
   double device_ms;            /* wall time of the device pipeline for this call              */
 } lb_verify_stats;

@@ -125,6 +125,7 @@ struct lb_ctx {
   uint32_t wave_max_sets = 1024;
   int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
   int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
+  int acc_split = -1;   // LB_ACC_SPLIT: 1 always / 0 never split requests in halves; -1 = lone calls only
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
   // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
   bool tail_wave = true;
@@ -377,10 +378,39 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   const fp12* fS_in = tail_wave ? nullptr : (const fp12*)d_fS;
   LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
   if (by_lines) {
-    const uint32_t rpw = TPB / ctx->acc_lpr, grid = (n_req + rpw - 1) / rpw;
+    // a lone call on an otherwise idle GPU splits every request in two halves:
+    // twice the waves (one per SIMD for a 65,536-set call instead of one per
+    // two SIMDs) at the price of the halves' separate Fp12 squarings; with
+    // other calls in flight the idle SIMDs run their stages instead and the
+    // work-efficient form is kept (LB_ACC_SPLIT=0|1 forces one)
+    bool lone = true;
+    for (int s = 0; s < ctx->n_slots; s++)
+      if (&ctx->slots[s] != &sl && ctx->slots[s].busy) lone = false;
+    const bool split = ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64);
+    const uint32_t nr = split ? 2 * n_req : n_req;
+    const uint32_t* acc_off = d_req_off;
+    fp12* acc_F = d_F;
+    uint8_t* acc_bad = d_bad;
+    uint8_t* acc_err = d_req_err;
+    if (split) {
+      uint32_t* off2 = ws.take<uint32_t>(2 * (size_t)n_req + 1);
+      acc_F = ws.take<fp12>(2 * (size_t)n_req);
+      acc_bad = ws.take<uint8_t>(2 * (size_t)n_req);
+      acc_err = ws.take<uint8_t>(2 * (size_t)n_req);
+      if (ws.off > ws.cap) {
+        ctx->err = "workspace overflow";
+        return LB_ERR_OUT_OF_MEMORY;
+      }
+      hipLaunchKernelGGL(k_split_requests, dim3(blocks_for(n_req + 1)), dim3(TPB), 0, sl.st[0], n_req, d_req_off, off2);
+      LB_HIP(hipGetLastError());
+      acc_off = off2;
+    }
+    const uint32_t rpw = TPB / ctx->acc_lpr, grid = (nr + rpw - 1) / rpw;
+    const fp12* acc_fS = split ? nullptr : fS_in;
+    const uint32_t halves = split ? 1u : 0u;
 #define LB_ACC_STAGE(L)                                                                                       \
-  LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, n_req, d_req_off, n_pairs, (const uint32_t*)d_lines, \
-           fS_in, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err)
+  LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, nr, acc_off, n_pairs, (const uint32_t*)d_lines, acc_fS, \
+           (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, acc_F, acc_bad, acc_err, halves)
     if (ctx->acc_lpr == 16)
       LB_ACC_STAGE(16);
     else if (ctx->acc_lpr == 32)
@@ -388,6 +418,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     else
       LB_ACC_STAGE(64);
 #undef LB_ACC_STAGE
+    if (split)
+      LB_STAGE("join_halves", 0, k_join_halves, blocks_for(n_req), TPB, n_req, d_req_off, (const fp12*)acc_F,
+               (const uint8_t*)acc_bad, (const uint8_t*)acc_err, fS_in, d_F, d_bad, d_req_err);
   } else
     LB_STAGE("prod_tree", 0, k_prod_tree, n_req, TPB, n_req, d_req_off, (const fp12*)d_f, fS_in,
              (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_F, d_bad, d_req_err);
@@ -432,7 +465,8 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
                    (size_t)LB_MILLER_LINES * 72 * 4;
-  size_t per_req = sizeof(g2a) + 2 * sizeof(fp12) + 1 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
+  // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
+  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
   return ns * per_set + (size_t)(n_req + 1) * per_req + 64 * 256 + 4096;
 }
 
@@ -593,6 +627,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);
     if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;

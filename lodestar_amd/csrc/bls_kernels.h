@@ -135,7 +135,14 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
                                                                     const uint8_t* __restrict__ sig_status,
                                                                     const uint8_t* __restrict__ pk_status,
                                                                     fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
-                                                                    uint8_t* __restrict__ req_err);
+                                                                    uint8_t* __restrict__ req_err, uint32_t halves);
+__global__ void __launch_bounds__(TPB) k_split_requests(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                        uint32_t* __restrict__ off2);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_join_halves(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                               const fp12* __restrict__ F2, const uint8_t* __restrict__ bad2,
+                                                               const uint8_t* __restrict__ err2,
+                                                               const fp12* __restrict__ fS, fp12* __restrict__ F,
+                                                               uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_lines_S(uint32_t n_req, uint32_t n_pairs, uint32_t base,
                                                           const g2a* __restrict__ S, uint32_t* __restrict__ lines,
                                                           const uint8_t* __restrict__ skip);

@@ -55,6 +55,9 @@ __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pai
 // so the Fp12 squaring of each loop step is shared by ~128 / LPR pairs; the
 // lane values are then multiplied in an LDS tree.  Also reduces the request's
 // set statuses (verdict / rejection flags) as k_prod_tree did.
+// halves != 0: the "requests" are the halves of the call's requests (a lone call
+// on an idle GPU runs twice as many waves, k_split_requests / k_join_halves); an
+// empty half is then not a false verdict.
 template <int LPR>
 __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                                     uint32_t n_pairs, const uint32_t* __restrict__ lines,
@@ -62,7 +65,7 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
                                                                     const uint8_t* __restrict__ sig_status,
                                                                     const uint8_t* __restrict__ pk_status,
                                                                     fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
-                                                                    uint8_t* __restrict__ req_err) {
+                                                                    uint8_t* __restrict__ req_err, uint32_t halves) {
   constexpr uint32_t RPW = TPB / LPR;  // requests per workgroup
   __shared__ fp12 sh[TPB];
   __shared__ uint32_t bad[RPW], err_empty[RPW], err_pk[RPW];
@@ -71,7 +74,7 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
   const bool live = k < n_req;
   const uint32_t a = live ? req_off[k] : 0, b = live ? req_off[k + 1] : 0;
   if (lane == 0) {
-    bad[sub] = (a == b) ? 1u : 0u;
+    bad[sub] = (a == b && !halves) ? 1u : 0u;
     err_empty[sub] = 0;
     err_pk[sub] = 0;
   }
@@ -127,6 +130,39 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
   }
 }
 
+// Request halves for a lone call: off2[2k] = off[k], off2[2k+1] = off[k] + ceil(n_k / 2).
+__global__ void __launch_bounds__(TPB) k_split_requests(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                        uint32_t* __restrict__ off2) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n_req) return;
+  const uint32_t a = req_off[k];
+  off2[2 * k] = a;
+  if (k < n_req) off2[2 * k + 1] = a + (req_off[k + 1] - a + 1) / 2;
+}
+
+// Join the halves: F_k = F2[2k] F2[2k+1] (x Miller(-g1, S_k) when fS is given),
+// verdict / rejection flags OR-ed; an empty request is false (maybeBatch.ts:31-33).
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_join_halves(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                               const fp12* __restrict__ F2, const uint8_t* __restrict__ bad2,
+                                                               const uint8_t* __restrict__ err2,
+                                                               const fp12* __restrict__ fS, fp12* __restrict__ F,
+                                                               uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  fp12 x = F2[2 * k], y = F2[2 * k + 1];
+  fp12_mul(x, x, y);
+  if (fS) {
+    fp12 s = fS[k];
+    fp12_mul(x, x, s);
+  }
+  F[k] = x;
+  req_bad[k] = (bad2[2 * k] | bad2[2 * k + 1] | (req_off[k + 1] == req_off[k] ? 1 : 0)) ? 1 : 0;
+  const uint8_t e0 = err2[2 * k], e1 = err2[2 * k + 1];
+  req_err[k] = (e0 == LB_REQ_EMPTY_AGGREGATE || e1 == LB_REQ_EMPTY_AGGREGATE) ? LB_REQ_EMPTY_AGGREGATE
+               : (e0 == LB_REQ_BAD_PUBKEY || e1 == LB_REQ_BAD_PUBKEY)     ? LB_REQ_BAD_PUBKEY
+                                                                            : LB_REQ_OK;
+}
+
 // tuning variants selected at run time (LB_LINES_WAVES, LB_ACC_LPR)
 #define LB_INST_LINES(W)                                                                                       \
   template __global__ void k_lines<W>(uint32_t, uint32_t, uint32_t, const g1j* __restrict__, const g2j* __restrict__, \
@@ -137,7 +173,7 @@ LB_INST_LINES(2)
   template __global__ void k_miller_acc<L>(uint32_t, const uint32_t* __restrict__, uint32_t,                    \
                                            const uint32_t* __restrict__, const fp12* __restrict__,              \
                                            const uint8_t* __restrict__, const uint8_t* __restrict__,            \
-                                           fp12* __restrict__, uint8_t* __restrict__, uint8_t* __restrict__);
+                                           fp12* __restrict__, uint8_t* __restrict__, uint8_t* __restrict__, uint32_t);
 LB_INST_ACC(64)
 LB_INST_ACC(32)
 LB_INST_ACC(16)

@@ -317,3 +317,35 @@ def test_mixed_workload_vs_c_oracle(device_modes, mixed_workload):
     assert list(res.errors) == list(err)
     assert list(res.valid) == list(valid)
     assert 0 < int(valid.sum()) < len(valid)  # the injections hit some requests, not all
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split):
+    """The Miller accumulation with every request split in two halves (what a lone
+    large call on an idle GPU runs: k_split_requests / k_join_halves, LB_ACC_SPLIT=1)
+    and never split, both forced onto the stored-lines organisation: verdicts and
+    rejection codes == the C oracle's (1-set requests have an empty half)."""
+    import os
+
+    from lodestar_amd.native import Device
+    from oracle import c_oracle as C
+    old = {k: os.environ.get(k) for k in ("LB_MILLER", "LB_ACC_SPLIT")}
+    os.environ.update(LB_MILLER="lines", LB_ACC_SPLIT=split)
+    try:
+        dev = Device(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        seed = hashlib.sha256(b"split-seed").digest()
+        res = dev.verify_requests(*mixed_workload, seed)
+        valid, err = C.verify_requests(*mixed_workload, seed, threads=16)
+        assert list(res.errors) == list(err)
+        assert list(res.valid) == list(valid)
+        if split == "1":
+            assert "join_halves" in dict(dev.last_stage_times())
+    finally:
+        dev.close()
