@@ -6,7 +6,9 @@ Run (GPU box):          python tools/opcount.py --run  -> profiles/op_counts.jso
 Uses a separate build of the same sources with -DLB_COUNT_OPS (every fp_mul /
 fp_sqr does one device atomicAdd).  The counts are exact for the data used:
 the only data-dependent branches are the 64-bit scalar bits (add or not) and
-the SSWU square/non-square path, both averaged over 256 random sets.
+the SSWU square/non-square path, both averaged over 256 random sets.  An Fp
+inversion (binary GCD, bls_inv.h) counts as 10 products: its 3,000 v_mad_u64_u32
+(25 rounds x 120) / 288, plus the one product that returns it to Montgomery form.
 """
 import argparse
 import ctypes
