@@ -32,6 +32,40 @@ def mad_one(x, y, t):
     return f"  LB_PS_MAD1_{t.upper()}(A, H, {x}, {y});\n"
 
 
+def emit_column(prods, acc="A", hi="H"):
+    """ONE asm statement for all products of a column: n v_mad_u64_u32 into the
+    96-bit accumulator (hi:acc), each carry-out folded into hi by a
+    v_addc_co_u32 issued one instruction later (the VALU-SGPR-write ->
+    carry-read wait state is filled by the next product or carry), the 64-bit
+    accumulator ping-ponging between acc and a temporary.  One statement per
+    column instead of one per two products: the compiler's hazard recognizer
+    pads every inline-asm boundary with an s_nop, ~140 of them per product."""
+    n = len(prods)
+    if n == 0:
+        return ""
+    ins, lines = [], []
+    for i, (x, y, t) in enumerate(prods):
+        ins.append(f'[x{i}] "v"({x})')
+        ins.append(f'[y{i}] "{t}"({y})')
+    for i in range(n):
+        dst, add = ("t", "a") if i % 2 == 0 else ("a", "t")
+        lines.append(f"v_mad_u64_u32 %[{dst}], %[c{i % 2}], %[x{i}], %[y{i}], %[{add}]")
+        if i >= 1:
+            lines.append(f"v_addc_co_u32_e64 %[h], %[c{(i - 1) % 2}], 0, %[h], %[c{(i - 1) % 2}]")
+    if n == 1:
+        lines.append("s_nop 0")
+    lines.append(f"v_addc_co_u32_e64 %[h], %[c{(n - 1) % 2}], 0, %[h], %[c{(n - 1) % 2}]")
+    body = "\\n\\t".join(lines)
+    out = "  {\n    uint64_t T_, c0_, c1_;\n"
+    out += f'    asm("{body}"\n'
+    out += f'        : [a] "+v"({acc}), [h] "+v"({hi}), [t] "=&v"(T_), [c0] "=&s"(c0_), [c1] "=&s"(c1_)\n'
+    out += f'        : {", ".join(ins)});\n'
+    if n % 2 == 1:
+        out += f"    {acc} = T_;\n"
+    out += "  }\n"
+    return out
+
+
 def emit_products(prods):
     out = ""
     i = 0
@@ -59,12 +93,12 @@ def gen_mul():
         prods = [(f"a.l[{j}]", f"b.l[{k - j}]", "v") for j in range(lo, hi + 1)]
         if k < N:
             prods += [(f"m{j}", f"LB_PS_P{k - j}", "s") for j in range(lo, k)]
-            s += emit_products(prods)
+            s += emit_column(prods)
             s += f"  m{k} = (uint32_t)A * (uint32_t)LB_P_INV32;\n"
-            s += mad_one(f"m{k}", "LB_PS_P0", "s")
+            s += emit_column([(f"m{k}", "LB_PS_P0", "s")])
         else:
             prods += [(f"m{j}", f"LB_PS_P{k - j}", "s") for j in range(lo, hi + 1)]
-            s += emit_products(prods)
+            s += emit_column(prods)
             s += f"  t[{k - N}] = (uint32_t)A;\n"
         s += "  A = (A >> 32) | ((uint64_t)H << 32);\n  H = 0;\n"
     s += "  t[11] = (uint32_t)A;\n"
@@ -95,12 +129,12 @@ def gen_sqr():
             prods = cross + cross + prods
         elif cross:
             s += "  C = 0;\n  G = 0;\n"
-            s += emit_products(cross).replace("(A, H,", "(C, G,")
+            s += emit_column(cross, acc="C", hi="G")
             s += "  LB_PS_ADD96(A, H, C, G);\n  LB_PS_ADD96(A, H, C, G);\n"
-        s += emit_products(prods)
+        s += emit_column(prods)
         if k < N:
             s += f"  m{k} = (uint32_t)A * (uint32_t)LB_P_INV32;\n"
-            s += mad_one(f"m{k}", "LB_PS_P0", "s")
+            s += emit_column([(f"m{k}", "LB_PS_P0", "s")])
         else:
             s += f"  t[{k - N}] = (uint32_t)A;\n"
         s += "  A = (A >> 32) | ((uint64_t)H << 32);\n  H = 0;\n"
