@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--per-request", type=int, default=128)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "op_counts.json"))
     a = ap.parse_args()
     from lodestar_amd import build as b
     if a.build:
@@ -58,8 +59,8 @@ def main():
                               blob, offs, bytes(32))
     assert res.valid.all(), res.valid
     names = [nm for nm, _ in dev.last_stage_times()]
-    buf = (ctypes.c_ulonglong * 16)()
-    k = lib.lb_opcount_stages(dev._h, buf, 16)
+    buf = (ctypes.c_ulonglong * 24)()
+    k = lib.lb_opcount_stages(dev._h, buf, 24)
     n_req = len(req) - 1
     per = {}
     tot_mul = tot_sqr = 0
@@ -73,8 +74,8 @@ def main():
            "mads_per_fp_sqr": MADS_PER_FPSQR, "organisation": "LB_MILLER=lines, merged check",
            "stages": per, "fp_mul_per_set_total": (tot_mul + tot_sqr) / n,
            "mads_per_set_total": (tot_mul * MADS_PER_FPMUL + tot_sqr * MADS_PER_FPSQR) / n}
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "op_counts.json"), "w") as f:
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
