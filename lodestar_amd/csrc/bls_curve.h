@@ -304,32 +304,78 @@ LB_DEV void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
   r = acc;
 }
 
+// Field element times an Fp scalar (an Fp2 scales coefficient-wise).
+LB_DEV void fmul_fp(fp& r, const fp& a, const fp& k) { fp_mul(r, a, k); }
+LB_DEV void fmul_fp(fp2& r, const fp2& a, const fp& k) { fp2_mul_fp(r, a, k); }
+
+// Shared-Z ladders.  A Jacobian point P = (X, Y, Z) is the affine point (X, Y)
+// of the isomorphic curve y^2 = x^3 + b Z^6, and so is every point (c X, +-Y, Z)
+// of the same Z; dbl-2009-l and madd-2007-bl do not involve b, so a ladder over
+// such points runs on that curve with mixed additions (7M + 4S instead of the
+// 11M + 5S of a Jacobian addition), and its result (X', Y', Z') there is
+// (X', Y', Z' Z) here.
+
 // [a + b lambda]P for the batch-randomness scalar r = a + b lambda (mod r),
-// a, b = the 32-bit halves of the 64-bit DRBG output, lambda = -x^2, given
-// E = [lambda]P (phi(P) on G1, -psi^2(P) on G2; both cost a few products).
-// Straus-Shamir joint double-and-add over 32 bit pairs with the table
-// {O, P, E, P + E}: 32 doublings + 32 additions.  The plain 64-bit
-// double-and-add it replaces ran 64 doublings + 64 additions per wave, since a
-// wave executes an addition as soon as ONE of its lanes has the bit set.
-// The table lives in private memory (dynamic index): 288 B per G2 entry.
+// a, b = the 32-bit halves of the 64-bit DRBG output, lambda = -x^2.  lambda is
+// a primitive cube root of unity mod r (lambda^2 + lambda + 1 = x^4 - x^2 + 1 =
+// r), so with [lambda]P = (w X, Y, Z) (phi on G1: w = beta; -psi^2 on G2: w in
+// Fp, LB_G2_OMEGA) the joint table is free: P + [lambda]P = -[lambda^2]P =
+// (w^2 X, -Y, Z).  Straus-Shamir over 32 bit pairs: 32 doublings + 32 mixed
+// additions per wave (a wave adds as soon as ONE lane's bit pair is non-zero),
+// the table selected with conditional moves (no private-memory table).
+// The ladder runs on the shared-Z curve; the caller multiplies the result's Z
+// by P's Z (jac_mul_glv), or knows it is 1.  LB_GLV_TABLE_REGS keeps w X and
+// w^2 X in registers; by default they are recomputed per step (2 Fp products)
+// to keep the live state at acc + (X, Y).
 template <class F>
-LB_DEV void jac_mul_glv(jac<F>& r, const jac<F>& p, const jac<F>& e, uint64_t raw) {
+LB_DEV void jac_mul_glv_xy(jac<F>& r, const F& X, const F& Y, const uint32_t* w_c, const uint32_t* w2_c,
+                           uint64_t raw) {
   const uint32_t a = (uint32_t)raw, b = (uint32_t)(raw >> 32);
-  jac<F> tab[4];
-  jac_set_inf(tab[0]);
-  tab[1] = p;
-  tab[2] = e;
-  jac_add(tab[3], p, e);
+#ifdef LB_GLV_TABLE_REGS
+  F xw, xw2;
+  {
+    fp w;
+    fp_set(w, w_c);
+    fmul_fp(xw, X, w);
+    fp_set(w, w2_c);
+    fmul_fp(xw2, X, w);
+  }
+#endif
   jac<F> acc;
   jac_set_inf(acc);
 #pragma unroll 1
   for (int i = 31; i >= 0; i--) {
     jac_dbl(acc, acc);
     const uint32_t sel = ((a >> i) & 1u) | (((b >> i) & 1u) << 1);
-    const jac<F> t = tab[sel];
-    jac_add(acc, acc, t);
+    if (sel) {
+      aff<F> q;
+      q.inf = false;
+#ifdef LB_GLV_TABLE_REGS
+      q.x = sel == 1 ? X : sel == 2 ? xw : xw2;
+#else
+      if (sel == 1) {
+        q.x = X;
+      } else {
+        fp w;
+        fp_set(w, sel == 2 ? w_c : w2_c);
+        fmul_fp(q.x, X, w);
+      }
+#endif
+      q.y = Y;
+      if (sel == 3) fneg(q.y, Y);
+      jac_add_aff(acc, acc, q);
+    }
   }
   r = acc;
+}
+template <class F>
+LB_DEV void jac_mul_glv(jac<F>& r, const jac<F>& p, const uint32_t* w_c, const uint32_t* w2_c, uint64_t raw) {
+  if (jac_is_inf(p)) {
+    jac_set_inf(r);
+    return;
+  }
+  jac_mul_glv_xy(r, p.X, p.Y, w_c, w2_c, raw);
+  fmul(r.Z, r.Z, p.Z);
 }
 
 // [k]P for a 32-byte big-endian scalar (secret keys: SecretKey.fromBytes is BE)
@@ -346,13 +392,24 @@ LB_DEV void jac_mul_be32(jac<F>& r, const jac<F>& p, const uint8_t k[32]) {
 
 // [|x|]P for the BLS parameter |x| = 0xd201000000010000 (fixed bit pattern:
 // 63 doublings, 5 additions; the branch is wave-uniform).
+// Shared-Z ladder (above): the 5 additions are mixed additions of (X, Y).
 template <class F>
 LB_DEV void jac_mul_xabs(jac<F>& r, const jac<F>& p) {
-  jac<F> acc = p;
+  if (jac_is_inf(p)) {
+    r = p;
+    return;
+  }
+  aff<F> q;
+  q.x = p.X;
+  q.y = p.Y;
+  q.inf = false;
+  jac<F> acc;
+  jac_from_aff(acc, q);
   for (int i = 62; i >= 0; i--) {
     jac_dbl(acc, acc);
-    if ((LB_X_ABS >> i) & 1ull) jac_add(acc, acc, p);
+    if ((LB_X_ABS >> i) & 1ull) jac_add_aff(acc, acc, q);
   }
+  fmul(acc.Z, acc.Z, p.Z);
   r = acc;
 }
 

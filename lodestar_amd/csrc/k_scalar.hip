@@ -4,7 +4,7 @@
 
 namespace lb {
 
-// r_i sig_i  (r_i = a_i + b_i lambda, jac_mul_glv)
+// r_i sig_i  (r_i = a_i + b_i lambda, jac_mul_glv: shared-Z ladder, free cube-root table)
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
@@ -17,9 +17,9 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, con
     uint8_t sd[32];
     for (int k = 0; k < 32; k++) sd[k] = seed[k];
     const uint64_t r = batch_scalar(sd, i);
-    g2j s = sig[i], e;
-    g2_glv_endo(e, s);
-    jac_mul_glv(rs, s, e, r);
+    jac_mul_glv_xy(rs, sig[i].X, sig[i].Y, LB_G2_OMEGA, LB_G2_OMEGA2, r);
+    fp2 z = sig[i].Z;  // 1 for decoded signatures; reloaded rather than kept live
+    fp2_mul(rs.Z, rs.Z, z);
   }
   rsig[i] = rs;
 }
@@ -40,9 +40,7 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, cons
     uint8_t sd[32];
     for (int k = 0; k < 32; k++) sd[k] = seed[k];
     const uint64_t r = batch_scalar(sd, i);
-    g1j e;
-    g1_glv_endo(e, p);
-    jac_mul_glv(rp, p, e, r);
+    jac_mul_glv(rp, p, LB_G1_BETA, LB_G1_BETA2, r);
   }
   rpk[i] = rp;
   pk_status[i] = st;
