@@ -79,29 +79,34 @@ LB_DEV void jac_neg(jac<F>& r, const jac<F>& p) {
   r.Z = p.Z;
 }
 
+// The group law below is written register-lean: each formula computes Z3 as
+// soon as its inputs allow, so the input Z (and Z^2) die early; a G2 point is
+// 72 VGPRs and every out-of-line Fp product clobbers v0-v50, so the order in
+// which intermediates die decides whether a 2-waves/SIMD kernel spills.
+
 // dbl-2009-l (a = 0): 2M + 5S.  Z3 = 2YZ, so 2-torsion and infinity map to Z3 = 0.
 template <class F>
 LB_DEV void jac_dbl_impl(jac<F>& r, const jac<F>& p) {
-  F A, B, C, D, E, Fq, t;
-  fsqr(A, p.X);
+  F A, B, C, D, E, t;
+  F Z3;
+  fmul(Z3, p.Y, p.Z);  // first: p.Z dies here
+  fdbl(Z3, Z3);
   fsqr(B, p.Y);
-  fsqr(C, B);
+  fsqr(A, p.X);
   fadd(t, p.X, B);
+  fsqr(C, B);
   fsqr(t, t);
   fsub(t, t, A);
   fsub(t, t, C);
   fdbl(D, t);
   fdbl(E, A);
   fadd(E, E, A);
-  fsqr(Fq, E);
-  F Z3;
-  fmul(Z3, p.Y, p.Z);
-  fdbl(Z3, Z3);
+  fsqr(t, E);  // F = E^2
   F X3;
-  fdbl(t, D);
-  fsub(X3, Fq, t);
-  F Y3;
+  fsub(X3, t, D);
+  fsub(X3, X3, D);
   fsub(t, D, X3);
+  F Y3;
   fmul(Y3, E, t);
   fdbl(C, C);
   fdbl(C, C);
@@ -112,7 +117,8 @@ LB_DEV void jac_dbl_impl(jac<F>& r, const jac<F>& p) {
   r.Z = Z3;
 }
 
-// add-2007-bl with the exceptional cases resolved (P == Q -> dbl, P == -Q -> O)
+// add-2007-bl with the exceptional cases resolved (P == Q -> dbl, P == -Q -> O);
+// W = 2 Z1 Z2 = (Z1 + Z2)^2 - Z1Z1 - Z2Z2 first, so Z1, Z2 die early.
 template <class F>
 LB_DEV void jac_add_impl(jac<F>& r, const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) {
@@ -123,15 +129,19 @@ LB_DEV void jac_add_impl(jac<F>& r, const jac<F>& p, const jac<F>& q) {
     r = p;
     return;
   }
-  F Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, Rr, V, t;
+  F Z1Z1, Z2Z2, W, U1, U2, S1, S2, H, Rr, t;
   fsqr(Z1Z1, p.Z);
   fsqr(Z2Z2, q.Z);
+  fadd(W, p.Z, q.Z);
+  fsqr(W, W);
+  fsub(W, W, Z1Z1);
+  fsub(W, W, Z2Z2);
+  fmul(t, q.Z, Z2Z2);
+  fmul(S1, p.Y, t);
+  fmul(t, p.Z, Z1Z1);
+  fmul(S2, q.Y, t);
   fmul(U1, p.X, Z2Z2);
   fmul(U2, q.X, Z1Z1);
-  fmul(S1, p.Y, q.Z);
-  fmul(S1, S1, Z2Z2);
-  fmul(S2, q.Y, p.Z);
-  fmul(S2, S2, Z1Z1);
   fsub(H, U2, U1);
   fsub(Rr, S2, S1);
   if (fis_zero(H)) {
@@ -142,30 +152,27 @@ LB_DEV void jac_add_impl(jac<F>& r, const jac<F>& p, const jac<F>& q) {
     }
     return;
   }
+  jac<F> o;
+  fmul(o.Z, W, H);
+  F I, J, V;
   fdbl(I, H);
   fsqr(I, I);
   fmul(J, H, I);
-  fdbl(Rr, Rr);
   fmul(V, U1, I);
-  jac<F> o;
+  fdbl(Rr, Rr);
   fsqr(o.X, Rr);
   fsub(o.X, o.X, J);
-  fdbl(t, V);
-  fsub(o.X, o.X, t);
+  fsub(o.X, o.X, V);
+  fsub(o.X, o.X, V);
   fsub(t, V, o.X);
   fmul(o.Y, Rr, t);
   fmul(t, S1, J);
   fdbl(t, t);
   fsub(o.Y, o.Y, t);
-  fadd(t, p.Z, q.Z);
-  fsqr(t, t);
-  fsub(t, t, Z1Z1);
-  fsub(t, t, Z2Z2);
-  fmul(o.Z, t, H);
   r = o;
 }
 
-// madd-2007-bl: p Jacobian + q affine
+// madd-2007-bl: p Jacobian + q affine; Z3 = (Z1 + H)^2 - Z1Z1 - HH as soon as H is known.
 template <class F>
 LB_DEV void jac_add_aff_impl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (q.inf) {
@@ -176,11 +183,11 @@ LB_DEV void jac_add_aff_impl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
     jac_from_aff(r, q);
     return;
   }
-  F Z1Z1, U2, S2, H, HH, I, J, Rr, V, t;
+  F Z1Z1, U2, S2, H, HH, Rr, t;
   fsqr(Z1Z1, p.Z);
+  fmul(t, p.Z, Z1Z1);
+  fmul(S2, q.y, t);
   fmul(U2, q.x, Z1Z1);
-  fmul(S2, q.y, p.Z);
-  fmul(S2, S2, Z1Z1);
   fsub(H, U2, p.X);
   fsub(Rr, S2, p.Y);
   if (fis_zero(H)) {
@@ -191,26 +198,27 @@ LB_DEV void jac_add_aff_impl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
     }
     return;
   }
+  jac<F> o;
   fsqr(HH, H);
+  fadd(t, p.Z, H);
+  fsqr(t, t);
+  fsub(t, t, Z1Z1);
+  fsub(o.Z, t, HH);
+  F I, J, V;
   fdbl(I, HH);
   fdbl(I, I);
   fmul(J, H, I);
-  fdbl(Rr, Rr);
   fmul(V, p.X, I);
-  jac<F> o;
+  fdbl(Rr, Rr);
   fsqr(o.X, Rr);
   fsub(o.X, o.X, J);
-  fdbl(t, V);
-  fsub(o.X, o.X, t);
+  fsub(o.X, o.X, V);
+  fsub(o.X, o.X, V);
   fsub(t, V, o.X);
   fmul(o.Y, Rr, t);
   fmul(t, p.Y, J);
   fdbl(t, t);
   fsub(o.Y, o.Y, t);
-  fadd(t, p.Z, H);
-  fsqr(t, t);
-  fsub(t, t, Z1Z1);
-  fsub(o.Z, t, HH);
   r = o;
 }
 

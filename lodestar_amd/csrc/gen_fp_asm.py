@@ -143,6 +143,78 @@ def gen_sqr():
     return s
 
 
+# ---- modular additions: interleaved carry chains ---------------------------
+# A VALU carry (SGPR lane mask) written by one v_add/v_sub *_co instruction
+# needs two wait states before the next carry-chain instruction reads it; the
+# compiler's lowering of a 12-limb chain therefore pads every step with
+# s_nop 1 (~3,600 s_nop per Fp12 squaring).  Here the four chains of an Fp2
+# addition or subtraction -- (c0, c1) x (sum, reduction) -- are interleaved so
+# that every carry is read four instructions after it is written: no s_nop.
+#   add: t = a + b; s = t - p (borrow = t < p); r = borrow ? t : s
+#   sub: t = a - b (borrow = a < b); u = t + p; r = borrow ? u : t
+# (a + b < 2p < 2^382: no carry out of the top limb.)
+
+ADD_I = ("v_add_co_u32_e64", "v_addc_co_u32_e64")
+SUB_I = ("v_sub_co_u32_e64", "v_subb_co_u32_e64")
+
+
+def gen_addsub(name, op, nc):
+    """r = a op b mod p over nc = 1 (fp) or 2 (fp2) coefficients; op is 'add',
+    'sub', or a tuple of one of them per coefficient (e.g. multiply by xi)."""
+    ops = (op,) * nc if isinstance(op, str) else tuple(op)
+    L = []
+
+    def chain1(c, j):  # r_c[j] = r_c[j] op b_c[j]   (carry k1_c)
+        first, nxt = ADD_I if ops[c] == "add" else SUB_I
+        if j == 0:
+            return f"{first} %[r{c}_{j}], %[k1{c}], %[r{c}_{j}], %[b{c}_{j}]"
+        return f"{nxt} %[r{c}_{j}], %[k1{c}], %[r{c}_{j}], %[b{c}_{j}], %[k1{c}]"
+
+    def chain2(c, j):  # x_c[j] = r_c[j] -/+ p[j]   (carry k2_c)
+        first, nxt = SUB_I if ops[c] == "add" else ADD_I
+        if j == 0:
+            return f"{first} %[x{c}_{j}], %[k2{c}], %[r{c}_{j}], %[p{j}]"
+        return f"{nxt} %[x{c}_{j}], %[k2{c}], %[r{c}_{j}], %[p{j}], %[k2{c}]"
+    for j in range(13):
+        if j < 12:
+            L += [chain1(c, j) for c in range(nc)]
+        if j == 12:
+            L.append("s_nop 0")  # the last step has no chain-1 instructions
+        if j >= 1:
+            L += [chain2(c, j - 1) for c in range(nc)]
+        # pad to the two wait states where fewer than two instructions separate
+        # a carry from its reader: the first step, and every step of a lone Fp
+        if j == 0:
+            L.append("s_nop 1" if nc == 1 else "s_nop 0")
+        elif nc == 1 and j < 12:
+            L.append("s_nop 0")
+    L.append("s_nop 1")
+    for c in range(nc):
+        for j in range(12):
+            if ops[c] == "add":  # keep t when t - p borrowed
+                L.append(f"v_cndmask_b32_e64 %[r{c}_{j}], %[x{c}_{j}], %[r{c}_{j}], %[k2{c}]")
+            else:            # take t + p when a - b borrowed
+                L.append(f"v_cndmask_b32_e64 %[r{c}_{j}], %[r{c}_{j}], %[x{c}_{j}], %[k1{c}]")
+    body = "\\n\\t".join(L)
+    T = "fp2" if nc == 2 else "fp"
+    acc = (lambda c: f"t.c{c}") if nc == 2 else (lambda c: "t")
+    bcc = (lambda c: f"b.c{c}") if nc == 2 else (lambda c: "b")
+    outs = [f'[r{c}_{j}] "+&v"({acc(c)}.l[{j}])' for c in range(nc) for j in range(12)]
+    outs += [f'[x{c}_{j}] "=&v"(x{c}[{j}])' for c in range(nc) for j in range(12)]
+    outs += [f'[k1{c}] "=&s"(k1{c})' for c in range(nc)] + [f'[k2{c}] "=&s"(k2{c})' for c in range(nc)]
+    ins = [f'[b{c}_{j}] "v"({bcc(c)}.l[{j}])' for c in range(nc) for j in range(12)]
+    ins += [f'[p{j}] "v"(LB_PS_P{j})' for j in range(12)]
+    sym = "".join("+" if o == "add" else "-" for o in ops)
+    out = f"// {T} r = a ({sym}) b mod p per coefficient: {2 * nc} interleaved carry chains\n"
+    out += f"LB_DEV void {name}({T}& r, const {T}& a, const {T}& b) {{\n"
+    out += "  uint32_t " + ", ".join(f"x{c}[12]" for c in range(nc)) + ";\n"
+    out += "  uint64_t " + ", ".join(f"k1{c}, k2{c}" for c in range(nc)) + ";\n"
+    out += f"  {T} t = a;\n"
+    out += f'  asm("{body}"\n      : {", ".join(outs)}\n      : {", ".join(ins)});\n'
+    out += "  r = t;\n}\n\n"
+    return out
+
+
 HEADER = r'''// GENERATED by gen_fp_asm.py -- do not edit.
 //
 // Product-scanning Montgomery multiplication / squaring for gfx950: every
@@ -223,7 +295,10 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "bls_fp_ps.h"
     consts = "".join(f"#define LB_PS_P{j} ((uint32_t)P_[{j}])\n" for j in range(N))
     with open(out, "w") as f:
-        f.write(HEADER + consts + "\n" + gen_mul() + gen_sqr())
+        f.write(HEADER + consts + "\n" + gen_mul() + gen_sqr() + gen_addsub("fp_add_ps", "add", 1)
+                + gen_addsub("fp_sub_ps", "sub", 1) + gen_addsub("fp2_add_ps", "add", 2)
+                + gen_addsub("fp2_sub_ps", "sub", 2)
+                + gen_addsub("fp2_subadd_ps", ("sub", "add"), 2))
 
 
 if __name__ == "__main__":
