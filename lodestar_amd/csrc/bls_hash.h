@@ -315,25 +315,33 @@ LB_DEV void iso_map_g2(g2j& r, const g2a& p) {
   fp2_mul(r.Y, t, yd2);
 }
 
-// clear_cofactor (RFC 9380 G.3): (x^2 - x - 1)P + (x - 1)psi(P) + psi^2(2P), x < 0
-LB_DEV void clear_cofactor_g2(g2j& r, const g2j& p) {
-  g2j t1, t2, t3, n;
-  jac_mul_xabs(t1, p);
-  jac_neg(t1, t1);  // t1 = [x]P
-  g2_psi(t2, p);    // t2 = psi(P)
-  jac_dbl(t3, p);
-  g2_psi(t3, t3);
-  g2_psi(t3, t3);  // psi^2(2P)
-  jac_neg(n, t2);
-  jac_add(t3, t3, n);  // psi^2(2P) - psi(P)
-  jac_add(t2, t1, t2);  // [x]P + psi(P)
-  jac_mul_xabs(t2, t2);
-  jac_neg(t2, t2);  // [x]([x]P + psi(P))
-  jac_add(t3, t3, t2);
-  jac_neg(n, t1);
-  jac_add(t3, t3, n);
-  jac_neg(n, p);
-  jac_add(r, t3, n);
+// clear_cofactor (RFC 9380 G.3): (x^2 - x - 1)P + (x - 1)psi(P) + psi^2(2P), x < 0.
+// With z = |x|, A = [z]P, B = psi(P) - A, C = [z]B:
+//   h = D - C,  D = psi^2(2P) - P - B,
+// ordered so that at most two points are live around each ladder; D is parked
+// in `stash` (the output slot, when the caller has one) across the second
+// ladder instead of occupying 72 VGPRs there.
+LB_DEV void clear_cofactor_g2(g2j& r, const g2j& p, g2j* stash = nullptr) {
+  g2j A, B, D, t;
+  jac_mul_xabs(A, p);
+  g2_psi(B, p);
+  jac_neg(A, A);
+  jac_add(B, B, A);  // B = psi(P) - A
+  jac_dbl(t, p);
+  g2_psi(t, t);
+  g2_psi(t, t);      // psi^2(2P)
+  jac_neg(D, p);
+  jac_add(t, t, D);  // psi^2(2P) - P
+  jac_neg(D, B);
+  jac_add(D, t, D);  // D
+  if (stash) {
+    *stash = D;
+    __asm__ volatile("" ::: "memory");  // reload D after the ladder, not kept live
+  }
+  jac_mul_xabs(t, B);  // C
+  jac_neg(t, t);
+  if (stash) D = *stash;
+  jac_add(r, D, t);
 }
 
 // One half of hash_to_curve: u_j = hash_to_field(msg)[j] -> SSWU -> iso (Jacobian).
@@ -349,10 +357,10 @@ LB_DEV void hash_to_g2_half(g2j& r, const uint8_t msg[32], int j) {
   iso_map_g2(r, q);
 }
 // Q0 + Q1 -> clear_cofactor
-LB_DEV void hash_to_g2_finish(g2j& r, const g2j& q0, const g2j& q1) {
+LB_DEV void hash_to_g2_finish(g2j& r, const g2j& q0, const g2j& q1, g2j* stash = nullptr) {
   g2j s;
   jac_add(s, q0, q1);
-  clear_cofactor_g2(r, s);
+  clear_cofactor_g2(r, s, stash);
 }
 
 // hash_to_curve(msg) -> Jacobian point of G2

@@ -22,7 +22,7 @@ __global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, cons
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
-  hash_to_g2_finish(h, q0, q1);
+  hash_to_g2_finish(h, q0, q1, out_h + i);  // out_h[i] doubles as the stash
   out_h[i] = h;
 }
 
