@@ -128,8 +128,8 @@ def launch_ranks(a) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--sets", type=int, default=65536)
     ap.add_argument("--per-request", type=int, default=128)
     ap.add_argument("--latency-reps", type=int, default=10)

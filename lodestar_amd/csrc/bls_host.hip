@@ -868,7 +868,7 @@ static void fill_stats(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   }
 }
 
-Slot& next_async_slot(lb_ctx* ctx) {
+static Slot& next_async_slot(lb_ctx* ctx) {  // internal: not part of the C ABI
   Slot& sl = ctx->slots[ctx->next_slot];
   ctx->next_slot = (ctx->next_slot + 1) % ctx->n_slots;
   return sl;
