@@ -215,6 +215,145 @@ def gen_addsub(name, op, nc):
     return out
 
 
+# ---- lazy reduction: double-width products and one Montgomery reduction ----
+# An Fp2 product by Karatsuba needs three 12x12-limb products but only TWO
+# reductions when the products are kept double width (Aranha et al., "Faster
+# explicit formulas for computing pairings over ordinary curves", EUROCRYPT
+# 2011): T0 = a0 b0, T1 = a1 b1, T2 = (a0 + a1)(b0 + b1) (plain sums < 2p),
+#   W0 = T0 - T1 mod pR  (add p to the upper 12 limbs when it borrows)
+#   W1 = T2 - T0 - T1 = a0 b1 + a1 b0 < 2p^2
+# and c = REDC(W) < 2p for any W < pR (pR ~ 9.8 p^2), one conditional
+# subtraction.  720 v_mad_u64_u32 per Fp2 product instead of 864.
+
+def gen_mulw():
+    s = "// w = a b (24 limbs, no reduction; a, b < 2^384): 144 v_mad_u64_u32\n"
+    s += "LB_DEV void fp_mulw_ps_body(uint32_t* w, const fp& a, const fp& b) {\n"
+    s += "  uint64_t A = 0;\n  uint32_t H = 0;\n"
+    for k in range(2 * N - 1):
+        lo, hi = max(0, k - N + 1), min(k, N - 1)
+        s += emit_column([(f"a.l[{j}]", f"b.l[{k - j}]", "v") for j in range(lo, hi + 1)])
+        s += f"  w[{k}] = (uint32_t)A;\n"
+        s += "  A = (A >> 32) | ((uint64_t)H << 32);\n  H = 0;\n"
+    s += f"  w[{2 * N - 1}] = (uint32_t)A;\n}}\n\n"
+    return s
+
+
+def gen_redc():
+    s = "// r = w R^-1 mod p for w < p R (24 limbs): 144 v_mad_u64_u32, one conditional subtraction\n"
+    s += "LB_DEV void fp_redc_ps_body(fp& r, const uint32_t* w) {\n"
+    s += "  uint64_t A = w[0];\n  uint32_t H = 0;\n"
+    s += "  uint32_t " + ", ".join(f"m{j}" for j in range(N)) + ";\n"
+    s += "  uint32_t t[12];\n"
+    for k in range(2 * N - 1):
+        if k < N:
+            s += emit_column([(f"m{j}", f"LB_PS_P{k - j}", "s") for j in range(0, k)])
+            s += f"  m{k} = (uint32_t)A * (uint32_t)LB_P_INV32;\n"
+            s += emit_column([(f"m{k}", "LB_PS_P0", "s")])
+        else:
+            s += emit_column([(f"m{j}", f"LB_PS_P{k - j}", "s") for j in range(k - N + 1, N)])
+            s += f"  t[{k - N}] = (uint32_t)A;\n"
+        # the shifted accumulator is < 2^38: adding the next input limb cannot carry out
+        s += f"  A = ((A >> 32) | ((uint64_t)H << 32)) + w[{k + 1}];\n  H = 0;\n"
+    s += "  t[11] = (uint32_t)A;\n"
+    s += "  fp_csub_p(r, t);\n}\n\n"
+    return s
+
+
+class ChainSched:
+    """Interleave independent carry chains into one asm body.  A VALU-written
+    carry (SGPR lane mask) may be read by a VALU instruction only two
+    instructions later: before each reader the scheduler inserts the s_nop the
+    gap still needs.  Instructions are (text, reads_carry, writes_carry)."""
+
+    def __init__(self):
+        self.lines = []
+        self.pos = 0
+        self.written = {}
+
+    def emit(self, text, reads=None, writes=None):
+        if reads is not None and reads in self.written:
+            gap = self.pos - self.written[reads] - 1
+            if gap < 2:
+                self.lines.append(f"s_nop {1 - gap}")
+        self.lines.append(text)
+        if writes is not None:
+            self.written[writes] = self.pos
+        self.pos += 1
+
+
+def chain_op(op, j, d, c, a, b):
+    """Step j of a carry chain: d = a op b (+/- carry c)."""
+    first, nxt = ADD_I if op == "add" else SUB_I
+    if j == 0:
+        return (f"{first} {d}, {c}, {a}, {b}", None, c)
+    return (f"{nxt} {d}, {c}, {a}, {b}, {c}", c, c)
+
+
+def kcombine_program():
+    """Karatsuba combine in place: (T0, T1, T2) -> W0 in T0, W1 in T2.
+      B: T0[j] = T0[j] - T1[j]             (borrow kb)
+      C: T2[j] = T2[j] - T0_old[j]          (kc; runs before B in each round)
+      D: T2[j] = T2[j] - T1[j]              (kd; one round behind C)
+      E: T1[12+j] = T0[12+j] + p[j]         (ke; after D has read T1[12+j])
+      W0[12+j] = kb ? T1[12+j] : T0[12+j]   (add p R when T0 - T1 borrowed)
+    Returns the list of asm lines (operands %[t0_j], %[t1_j], %[t2_j], %[p_j],
+    SGPR pairs %[kb], %[kc], %[kd], %[ke])."""
+    S = ChainSched()
+    n = 2 * N
+    for r in range(n + 2):
+        step = []
+        if r < n:
+            step.append(chain_op("sub", r, f"%[t2_{r}]", "%[kc]", f"%[t2_{r}]", f"%[t0_{r}]"))
+            step.append(chain_op("sub", r, f"%[t0_{r}]", "%[kb]", f"%[t0_{r}]", f"%[t1_{r}]"))
+        if 1 <= r <= n:
+            j = r - 1
+            step.append(chain_op("sub", j, f"%[t2_{j}]", "%[kd]", f"%[t2_{j}]", f"%[t1_{j}]"))
+        if r >= N + 2 and r - N - 2 < N:
+            j = r - N - 2  # T1[12+j] was last read by D at round 13+j
+            step.append(chain_op("add", j, f"%[t1_{N + j}]", "%[ke]", f"%[t0_{N + j}]", f"%[p_{j}]"))
+        for text, rd, wr in step:
+            S.emit(text, rd, wr)
+    for j in range(N):
+        S.emit(f"v_cndmask_b32_e64 %[t0_{N + j}], %[t0_{N + j}], %[t1_{N + j}], %[kb]", "%[kb]")
+    return S.lines
+
+
+def gen_kcombine():
+    L = kcombine_program()
+    body = "\\n\\t".join(L)
+    outs = [f'[t{i}_{j}] "+&v"(t{i}[{j}])' for i in range(3) for j in range(2 * N)]
+    outs += [f'[k{c}] "=&s"(k{c})' for c in "bcde"]
+    ins = [f'[p_{j}] "v"(LB_PS_P{j})' for j in range(N)]
+    s = "// Karatsuba combine of three double-width products, in place (see kcombine_program):\n"
+    s += "// t0 <- t0 - t1 mod pR, t2 <- t2 - t0 - t1.  t1's upper half is clobbered.\n"
+    s += "LB_DEV void fpw_kcombine_ps(uint32_t* t0, uint32_t* t1, uint32_t* t2) {\n"
+    s += "  uint64_t kb, kc, kd, ke;\n"
+    s += f'  asm("{body}"\n      : {", ".join(outs)}\n      : {", ".join(ins)});\n}}\n\n'
+    return s
+
+
+def plain_add2_program():
+    """(s, t) = (a0 + a1, b0 + b1) without reduction (inputs < p, sums < 2^382)."""
+    S = ChainSched()
+    for j in range(N):
+        for x, c in (("s", "%[ks]"), ("t", "%[kt]")):
+            text, rd, wr = chain_op("add", j, f"%[{x}{j}]", c, f"%[{x}{j}]", f"%[{x}b{j}]")
+            S.emit(text, rd, wr)
+    return S.lines
+
+
+def gen_plain_add2():
+    body = "\\n\\t".join(plain_add2_program())
+    outs = [f'[{x}{j}] "+&v"({x}.l[{j}])' for x in "st" for j in range(N)]
+    outs += ['[ks] "=&s"(ks)', '[kt] "=&s"(kt)']
+    ins = [f'[{x}b{j}] "v"({y}.l[{j}])' for x, y in (("s", "a1"), ("t", "b1")) for j in range(N)]
+    s = "// (s, t) = (a0 + a1, b0 + b1), no reduction (Karatsuba operands, < 2p)\n"
+    s += "LB_DEV void fp_add2_plain_ps(fp& s, fp& t, const fp& a0, const fp& a1, const fp& b0, const fp& b1) {\n"
+    s += "  uint64_t ks, kt;\n  s = a0;\n  t = b0;\n"
+    s += f'  asm("{body}"\n      : {", ".join(outs)}\n      : {", ".join(ins)});\n}}\n\n'
+    return s
+
+
 HEADER = r'''// GENERATED by gen_fp_asm.py -- do not edit.
 //
 // Product-scanning Montgomery multiplication / squaring for gfx950: every
@@ -298,7 +437,8 @@ def main():
         f.write(HEADER + consts + "\n" + gen_mul() + gen_sqr() + gen_addsub("fp_add_ps", "add", 1)
                 + gen_addsub("fp_sub_ps", "sub", 1) + gen_addsub("fp2_add_ps", "add", 2)
                 + gen_addsub("fp2_sub_ps", "sub", 2)
-                + gen_addsub("fp2_subadd_ps", ("sub", "add"), 2))
+                + gen_addsub("fp2_subadd_ps", ("sub", "add"), 2)
+                + gen_mulw() + gen_redc() + gen_kcombine() + gen_plain_add2())
 
 
 if __name__ == "__main__":
