@@ -49,6 +49,31 @@ __global__ void __launch_bounds__(TPB, WAVES) k_lines(uint32_t n, uint32_t n_pai
   miller_lines(p, q, lines, n_pairs, base + i);
 }
 
+// f *= line j of the pairs a + lane, a + lane + LPR, ... < b: two pairs at a time
+// through the sparse x sparse product (23 Fp2 products per two lines instead of 26)
+template <int LPR>
+LB_DEV void acc_lines(fp12& f, const uint32_t* __restrict__ lines, uint32_t n_pairs, uint32_t a, uint32_t b,
+                      uint32_t lane, int j) {
+  fp2 l0, l1, l4;
+  uint32_t i = a + lane;
+#ifndef LB_NO_LINE_PAIRS
+#pragma unroll 1
+  for (; i + LPR < b; i += 2 * LPR) {
+    fp2 m0, m1, m4, y1, y2;
+    fp6 x;
+    line_get(lines, n_pairs, i, j, l0, l1, l4);
+    line_get(lines, n_pairs, i + LPR, j, m0, m1, m4);
+    line_mul_line(x, y1, y2, l0, l1, l4, m0, m1, m4);
+    fp12_mul_by_sparse2(f, f, x, y1, y2);
+  }
+#endif
+#pragma unroll 1
+  for (; i < b; i += LPR) {
+    line_get(lines, n_pairs, i, j, l0, l1, l4);
+    fp12_mul_line(f, f, l0, l1, l4);
+  }
+}
+
 // Per request k: F_k = f_S[k] * prod_{i in request} Miller(r_i pk_i, H_i), from
 // the stored lines.  LB_ACC_LPR lanes per request (64 / LB_ACC_LPR requests per
 // wave); lane l accumulates the set pairs a + l, a + l + LPR, ... into ONE f,
@@ -87,23 +112,16 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
   }
   fp12 f;
   fp12_one(f);
-  fp2 l0, l1, l4;
   int j = 0;
 #pragma unroll 1
   for (int bit = 62; bit >= 0; bit--) {
-    if (bit < 62) fp12_sqr(f, f);
+    // the doubling line, then the addition line when bit is set: one loop body,
+    // so the (large) line accumulation is instantiated once
+    const int reps = 1 + (int)((LB_X_ABS >> bit) & 1ull);
 #pragma unroll 1
-    for (uint32_t i = a + lane; i < b; i += LPR) {
-      line_get(lines, n_pairs, i, j, l0, l1, l4);
-      fp12_mul_line(f, f, l0, l1, l4);
-    }
-    j++;
-    if ((LB_X_ABS >> bit) & 1ull) {
-#pragma unroll 1
-      for (uint32_t i = a + lane; i < b; i += LPR) {
-        line_get(lines, n_pairs, i, j, l0, l1, l4);
-        fp12_mul_line(f, f, l0, l1, l4);
-      }
+    for (int rep = 0; rep < reps; rep++) {
+      if (rep == 0 && bit < 62) fp12_sqr(f, f);
+      acc_lines<LPR>(f, lines, n_pairs, a, b, lane, j);
       j++;
     }
   }
