@@ -37,6 +37,9 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #ifndef LB_W_SCALAR
 #define LB_W_SCALAR 2
 #endif
+#ifndef LB_W_SSIG  // k_scalar_sig (r sigma: two live G2 points)
+#define LB_W_SSIG LB_W_SCALAR
+#endif
 #ifndef LB_W_ACC
 #define LB_W_ACC 1
 #endif
@@ -88,7 +91,7 @@ __global__ void k_g1a_serialize(uint32_t n, const g1a* __restrict__ in, uint8_t*
 __global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
 __global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);
-__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_SSIG) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig);

@@ -5,7 +5,7 @@
 namespace lb {
 
 // r_i sig_i  (r_i = a_i + b_i lambda, jac_mul_glv: shared-Z ladder, free cube-root table)
-__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
+__global__ void __launch_bounds__(TPB, LB_W_SSIG) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
                                                     g2j* __restrict__ rsig) {

@@ -25,6 +25,22 @@ STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
 }
 
 
+# Algorithmic HBM bytes per SET of each per-set stage (C2: one pubkey and one
+# 96-byte signature per set): what the stage must read and write, no spills.
+# Jacobian G1 = 144 B, Jacobian G2 = 288 B, a stored line = 288 B (68 per pair).
+ALG_BYTES_PER_SET = {
+    "hash_half": 32 + 2 * 288,        # message -> Q0, Q1
+    "hash_finish": 2 * 288 + 288,     # Q0, Q1 -> H(m)
+    "pubkeys": 96 + 144 + 1,          # encoding -> point + status
+    "scalar_pk": 144 + 144 + 1,       # pk -> r pk (+ G1 check flag)
+    "decode_sigs": 96 + 288 + 1,      # compressed signature -> point + status
+    "scalar_sig": 288 + 288,          # sigma -> r sigma
+    "lines": 144 + 288 + 68 * 288,    # r pk, H -> 68 lines
+    "miller_acc": 68 * 288 + 2,       # lines (+ statuses) -> per-request F_k
+}
+N_SETS = 65536
+
+
 def kernel_key(name):
     """'void lb::k_lines<1>(unsigned int, ...)' -> 'k_lines'"""
     n = name.split("(")[0].replace("void ", "").replace("lb::", "").strip()
@@ -37,7 +53,9 @@ def main():
                                                               "pmc_traffic.json")
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-launch values]
     full = {}
-    for f in glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), recursive=True):
+    files = glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), recursive=True)
+    files += glob.glob(os.path.join(d, "pass*_counter_collection.csv"))  # flattened copies under profiles/
+    for f in files:
         for row in csv.DictReader(open(f)):
             k = kernel_key(row["Kernel_Name"])
             full[k] = row["Kernel_Name"]
@@ -51,6 +69,10 @@ def main():
         ent = {"kernel": full[k].split("(")[0], "counters": {n: round(x, 3) for n, x in c.items()}}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             ent["hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+            if stage in ALG_BYTES_PER_SET:
+                alg = ALG_BYTES_PER_SET[stage] * N_SETS
+                ent["algorithmic_bytes_per_launch"] = alg
+                ent["traffic_over_algorithmic"] = round(ent["hbm_bytes_per_launch"] / alg, 2)
         if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c and c["SQ_WAVES"]:
             ent["valu_insts_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"])
         if c.get("SQ_LDS_IDX_ACTIVE"):
