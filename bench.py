@@ -157,7 +157,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")  # barrier, max-over-ranks and the 576-byte partials; no data-path collective
+        # barrier, max-over-ranks and the 576-byte partials; no data-path collective.  Gloo's
+        # C++ side prints "[Gloo] Rank r is connected ..." on stdout: route fd 1 to stderr
+        # meanwhile, so rank 0's stdout carries only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)  # one process per GPU; ranks > devices only when rehearsing
     torch.cuda.set_device(gpu)
@@ -298,7 +309,7 @@ def main():
     total_sets = n * world * a.steps
     value = total_sets / elapsed
     stage_ms = {k: v / max(n_acc[0], 1) for k, v in stage_acc.items()}
-    roof = roofline(iso_ms, stage_ms, n, value, a.iso_reps)
+    roof = roofline(iso_ms, stage_ms, n, value, a.iso_reps, n_req)
     cpu = None
     c1 = None
     if not a.no_cpu_baseline and world == 1:
@@ -356,7 +367,7 @@ def main():
         dist.barrier()
 
 
-def roofline(iso_ms, stage_ms, n, value, iso_reps):
+def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     """Dominant kernel's integer-MAD roofline (achieved = algorithmic mads of one
     launch / its HIP-event duration, one call at a time) + the pipeline's."""
     counts_path = os.path.join(ROOT, "profiles", "op_counts.json")
@@ -370,6 +381,12 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps):
     if not st:
         return None
     per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
+    # the iso launches are lone calls: k_miller_acc then splits requests in halves (one pair per
+    # lane, its own Fp12 squarings), so its work per set is that organisation's count
+    lone = oc.get("lone_call_stages", {}).get(dom) if iso_ms else None
+    per_set_pipe = per_set
+    if lone and n_req >= 64:  # bls_host.hip: a lone call splits from 64 requests up
+        per_set = lone["mads_per_set"]
     mads = per_set * n
     achieved = mads / (timing[dom] * 1e-3) / 1e12
     peak = PEAK_MAD_PER_S / 1e12
@@ -383,10 +400,16 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps):
             "launch_ms": round(timing[dom], 3),
             "timing": "median of %d one-at-a-time calls after the timed region (HIP events on the "
                       "kernel's stream)" % iso_reps if iso_ms else "timed region, calls overlapped"}
+    if per_set != per_set_pipe:
+        roof["organisation"] = ("lone call: requests split in halves, one pair per lane "
+                                "(profiles/op_counts.json lone_call_stages)")
+        roof["mads_per_set_launch"] = round(per_set)
+        roof["mads_per_set_two_pairs_per_lane"] = round(per_set_pipe)
+        roof["frac_at_two_pairs_per_lane_count"] = round(per_set_pipe * n / (timing[dom] * 1e-3) / 1e12 / peak, 5)
     if iso_ms and dom in stage_ms:
-        # the same kernel while other calls' kernels share the CUs (timed region)
+        # the same kernel while other calls' kernels share the CUs (timed region, two pairs per lane)
         roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
-        roof["in_pipeline_frac"] = round(mads / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
+        roof["in_pipeline_frac"] = round(per_set_pipe * n / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
     if "mads_per_set_total" in oc:
         # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
         pipe = value * oc["mads_per_set_total"] / 1e12

@@ -45,36 +45,49 @@ def main():
     native._lib = None
     lib = native.load_library()
     lib.lb_opcount_stages.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    dev = native.Device(0)
     n = a.sets
     r_order = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
     sks = [(int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % r_order).to_bytes(32, "big")
            for i in range(n)]
     msgs = [hashlib.sha256(b"opcount" + i.to_bytes(8, "little")).digest() for i in range(n)]
-    pks = dev.sk_to_pk(sks)
-    sigs = dev.sign(sks, msgs)
-    blob, offs = native.pack_blobs(sigs)
-    req = np.arange(0, n + 1, a.per_request, dtype=np.uint32)
-    res = dev.verify_requests(req, np.frombuffer(b"".join(pks), np.uint8), None, np.frombuffer(b"".join(msgs), np.uint8),
-                              blob, offs, bytes(32))
-    assert res.valid.all(), res.valid
-    names = [nm for nm, _ in dev.last_stage_times()]
-    buf = (ctypes.c_ulonglong * 24)()
-    k = lib.lb_opcount_stages(dev._h, buf, 24)
-    n_req = len(req) - 1
-    per = {}
-    tot_mul = tot_sqr = 0
-    for i in range(k):
-        # low half counts 144-mad halves (a Montgomery product is two)
-        muls, sqrs = (int(buf[i]) & 0xFFFFFFFF) / 2, int(buf[i]) >> 32
-        tot_mul += muls
-        tot_sqr += sqrs
-        per[names[i]] = {"fp_mul_total": muls, "fp_sqr_total": sqrs, "fp_mul_per_set": (muls + sqrs) / n,
-                         "mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n}
+
+    def count(split):
+        # LB_ACC_SPLIT=0: two pairs per lane in k_miller_acc (calls overlapped, the timed region);
+        # 1: requests split in halves, one pair per lane (a lone call: the roofline's iso launch)
+        os.environ["LB_ACC_SPLIT"] = str(split)
+        dev = native.Device(0)
+        pks = dev.sk_to_pk(sks)
+        sigs = dev.sign(sks, msgs)
+        blob, offs = native.pack_blobs(sigs)
+        req = np.arange(0, n + 1, a.per_request, dtype=np.uint32)
+        res = dev.verify_requests(req, np.frombuffer(b"".join(pks), np.uint8), None,
+                                  np.frombuffer(b"".join(msgs), np.uint8), blob, offs, bytes(32))
+        assert res.valid.all(), res.valid
+        names = [nm for nm, _ in dev.last_stage_times()]
+        buf = (ctypes.c_ulonglong * 24)()
+        k = lib.lb_opcount_stages(dev._h, buf, 24)
+        per = {}
+        tot_mul = tot_sqr = 0
+        for i in range(k):
+            # low half counts 144-mad halves (a Montgomery product is two)
+            muls, sqrs = (int(buf[i]) & 0xFFFFFFFF) / 2, int(buf[i]) >> 32
+            tot_mul += muls
+            tot_sqr += sqrs
+            per[names[i]] = {"fp_mul_total": muls, "fp_sqr_total": sqrs, "fp_mul_per_set": (muls + sqrs) / n,
+                             "mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n}
+        return per, tot_mul, tot_sqr
+
+    per, tot_mul, tot_sqr = count(0)
+    lone, _, _ = count(1)
+    n_req = n // a.per_request
     out = {"sets": n, "requests": n_req, "sets_per_request": a.per_request, "mads_per_fp_mul": MADS_PER_FPMUL,
-           "mads_per_fp_sqr": MADS_PER_FPSQR, "organisation": "LB_MILLER=lines, merged check",
+           "mads_per_fp_sqr": MADS_PER_FPSQR,
+           "organisation": "LB_MILLER=lines, merged check, two pairs per lane in k_miller_acc (LB_ACC_SPLIT=0)",
            "stages": per, "fp_mul_per_set_total": (tot_mul + tot_sqr) / n,
-           "mads_per_set_total": (tot_mul * MADS_PER_FPMUL + tot_sqr * MADS_PER_FPSQR) / n}
+           "mads_per_set_total": (tot_mul * MADS_PER_FPMUL + tot_sqr * MADS_PER_FPSQR) / n,
+           "lone_call_organisation": "LB_ACC_SPLIT=1: requests split in halves, one pair per lane (what a lone "
+                                     "call runs, e.g. bench.py's iso launches)",
+           "lone_call_stages": {k: {"mads_per_set": v["mads_per_set"]} for k, v in lone.items()}}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
