@@ -652,7 +652,11 @@ int lb_create(int device, lb_ctx** out_ctx) {
     if (ok) sl.h_stats[0] = sl.h_stats[1] = 0;
   }
   ctx->stream = ctx->slots[0].st[0];
-  ok = ok && hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) == hipSuccess;
+  // the host combine's one-wave final exponentiation must not queue behind the
+  // calls in flight (their 1-wave/SIMD kernels fill every SIMD): highest priority
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  ok = ok && hipStreamCreateWithPriority(&ctx->aux_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;
