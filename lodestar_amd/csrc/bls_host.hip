@@ -147,6 +147,9 @@ struct lb_ctx {
   // lb_gt_check runs on its own stream and buffers, so the host combine of the
   // shards' partials never drains the slots' calls in flight
   hipStream_t aux_stream = nullptr;
+  // the merged check's one-wave chain of every slot (highest priority) when
+  // LB_TAIL_PRIO=1; nullptr (default): the slot's own stream
+  hipStream_t tail_stream = nullptr;
   uint8_t* d_aux = nullptr;
   uint8_t* h_aux = nullptr;
   size_t aux_cap = 0;
@@ -229,23 +232,25 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
 #endif
 
 // Launch `kern` on stream `s` of slot `sl`, bracketed by timing events.
-#define LB_STAGE(name, s, kern, grid, block, ...)                                          \
+#define LB_STAGE_ON(name, strm, kern, grid, block, ...)                                    \
   do {                                                                                     \
     const int si_ = sl.n_stages < Slot::kMaxStages ? sl.n_stages++ : -1;                   \
+    hipStream_t strm_ = (strm);                                                            \
     LB_COUNT_SYNC();                                                                       \
     if (si_ >= 0) {                                                                        \
       LB_COUNT_TAKE(si_);                                                                  \
       sl.stage_name[si_] = name;                                                           \
-      LB_HIP(hipEventRecord(sl.ev0[si_], sl.st[s]));                                       \
+      LB_HIP(hipEventRecord(sl.ev0[si_], strm_));                                          \
     }                                                                                      \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, sl.st[s], __VA_ARGS__);          \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, strm_, __VA_ARGS__);             \
     LB_HIP(hipGetLastError());                                                             \
-    if (si_ >= 0) LB_HIP(hipEventRecord(sl.ev1[si_], sl.st[s]));                           \
+    if (si_ >= 0) LB_HIP(hipEventRecord(sl.ev1[si_], strm_));                              \
     LB_COUNT_SYNC();                                                                       \
     if (si_ >= 0) {                                                                        \
       LB_COUNT_TAKE(si_);                                                                  \
     }                                                                                      \
   } while (0)
+#define LB_STAGE(name, s, kern, grid, block, ...) LB_STAGE_ON(name, sl.st[s], kern, grid, block, __VA_ARGS__)
 
 #define LB_LAUNCH(kern, grid, block, ...)                                                  \
   do {                                                                                     \
@@ -439,24 +444,40 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   ps.d_mflag = d_mflag;
   ps.d_mstats = d_mstats;
   if (merged) {
-    // merged check: one tail for the whole call; per-request tails only if it fails
-    LB_HIP(hipMemsetAsync(d_mflag, 0, 2, sl.st[0]));
-    LB_STAGE("merge", 0, k_merge, 1u, TPB, n_req, (const g2a*)d_S, (const fp12*)d_F, (const uint8_t*)d_bad, d_Sall,
-             d_Fall);
-    LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
-             (const uint8_t*)nullptr);
+    // merged check: one tail for the whole call; per-request tails only if it fails.
+    // LB_TAIL_PRIO=1 runs its chain of one-wave kernels on a shared high-priority
+    // stream instead of the slot's own (measured slower, off by default).
+    hipStream_t ts = sl.st[0];
+    if (ctx->tail_stream) {
+      ts = ctx->tail_stream;
+      LB_HIP(hipEventRecord(sl.dep[3], sl.st[0]));
+      LB_HIP(hipStreamWaitEvent(ts, sl.dep[3], 0));
+    }
+    LB_HIP(hipMemsetAsync(d_mflag, 0, 2, ts));
+    LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, (const g2a*)d_S, (const fp12*)d_F, (const uint8_t*)d_bad,
+                d_Sall, d_Fall);
+    LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+                (const uint8_t*)nullptr);
     if (partial) {
       // two-phase call: the merged Miller product goes to the host, which
       // combines it with the other GPUs' partials; the tails wait for its verdict
-      LB_STAGE("partial", 0, k_partial, 1u, TPB, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
-               (const fp12*)d_Fall, d_partial);
-      LB_HIP(hipMemcpyAsync(sl.h_partial, d_partial, LB_GT_BYTES, hipMemcpyDeviceToHost, sl.st[0]));
-      LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
+      LB_STAGE_ON("partial", ts, k_partial, 1u, TPB, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+                  (const fp12*)d_Fall, d_partial);
+      LB_HIP(hipMemcpyAsync(sl.h_partial, d_partial, LB_GT_BYTES, hipMemcpyDeviceToHost, ts));
+      LB_HIP(hipEventRecord(sl.partial_ev, ts));
+      if (ts != sl.st[0]) {
+        LB_HIP(hipEventRecord(sl.dep[4], ts));
+        LB_HIP(hipStreamWaitEvent(sl.st[0], sl.dep[4], 0));
+      }
       sl.partial_pending = true;
       return LB_OK;
     }
-    LB_STAGE("tail_all", 0, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
-             (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
+    LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+                (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
+    if (ts != sl.st[0]) {
+      LB_HIP(hipEventRecord(sl.dep[4], ts));
+      LB_HIP(hipStreamWaitEvent(sl.st[0], sl.dep[4], 0));
+    }
   }
   return run_tails(ctx, sl);
 }
@@ -657,6 +678,13 @@ int lb_create(int device, lb_ctx** out_ctx) {
   int prio_least = 0, prio_greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
   ok = ok && hipStreamCreateWithPriority(&ctx->aux_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+  {
+    // off by default: one shared high-priority stream for every slot's merged check
+    // measured 2.40-2.43 vs 2.56-2.57 M sets/s (profiles/ab_r02s/r02s_d_*.json)
+    const char* e = getenv("LB_TAIL_PRIO");
+    if (e && atoi(e) == 1)
+      ok = ok && hipStreamCreateWithPriority(&ctx->tail_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+  }
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;
@@ -693,6 +721,10 @@ int lb_destroy(lb_ctx* ctx) {
   if (ctx->aux_stream) {
     (void)hipStreamSynchronize(ctx->aux_stream);
     (void)hipStreamDestroy(ctx->aux_stream);
+  }
+  if (ctx->tail_stream) {
+    (void)hipStreamSynchronize(ctx->tail_stream);
+    (void)hipStreamDestroy(ctx->tail_stream);
   }
   if (ctx->d_aux) (void)hipFree(ctx->d_aux);
   if (ctx->h_aux) (void)hipHostFree(ctx->h_aux);
