@@ -319,18 +319,19 @@ def test_mixed_workload_vs_c_oracle(device_modes, mixed_workload):
     assert 0 < int(valid.sum()) < len(valid)  # the injections hit some requests, not all
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
-def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split):
+@pytest.mark.parametrize("split,tail_prio", [("1", "0"), ("0", "0"), ("0", "1")])
+def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split, tail_prio):
     """The Miller accumulation with every request split in two halves (what a lone
     large call on an idle GPU runs: k_split_requests / k_join_halves, LB_ACC_SPLIT=1)
-    and never split, both forced onto the stored-lines organisation: verdicts and
+    and never split, both forced onto the stored-lines organisation, and the merged
+    check on the shared high-priority stream (LB_TAIL_PRIO=1): verdicts and
     rejection codes == the C oracle's (1-set requests have an empty half)."""
     import os
 
     from lodestar_amd.native import Device
     from oracle import c_oracle as C
-    old = {k: os.environ.get(k) for k in ("LB_MILLER", "LB_ACC_SPLIT")}
-    os.environ.update(LB_MILLER="lines", LB_ACC_SPLIT=split)
+    old = {k: os.environ.get(k) for k in ("LB_MILLER", "LB_ACC_SPLIT", "LB_TAIL_PRIO")}
+    os.environ.update(LB_MILLER="lines", LB_ACC_SPLIT=split, LB_TAIL_PRIO=tail_prio)
     try:
         dev = Device(0)
     finally:
