@@ -52,37 +52,15 @@ LB_DEV void wc_init_tables(wc_smem& S) {
   __syncthreads();
 }
 
-// ---- lazy accumulation: a lane sums up to 8 (|coef|-weighted) terms as a
-// plain 12-limb integer (every term is v or p - v, both <= p, so the sum stays
-// < 8p < 2^384), then reduces once with conditional subtractions of 4p, 2p, p.
+// ---- lazy accumulation: a lane sums up to 8 (|coef|-weighted) canonical terms
+// (the signed sum plus the negative weight times p stays in [0, 8p), 8p < 2^384),
+// then reduces once with conditional subtractions of 4p, 2p, p.
 static constexpr uint32_t WC_P2[12] = LB_P2_LIMBS;
 static constexpr uint32_t WC_P4[12] = LB_P4_LIMBS;
 
 struct lz {
   uint32_t l[12];
 };
-LB_DEV void lz_zero(lz& a) {
-#pragma unroll
-  for (int j = 0; j < 12; j++) a.l[j] = 0;
-}
-// a += c v  (c > 0)  or  a += |c| (p - v)  (c < 0)
-LB_DEV void lz_term(lz& a, const fp& v, int c) {
-  uint32_t t[12];
-  if (c < 0) {
-    uint32_t br = 0;
-#pragma unroll
-    for (int j = 0; j < 12; j++) t[j] = __builtin_subc(P_[j], v.l[j], br, &br);
-    c = -c;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 12; j++) t[j] = v.l[j];
-  }
-  for (int k = 0; k < c; k++) {
-    uint32_t cy = 0;
-#pragma unroll
-    for (int j = 0; j < 12; j++) a.l[j] = __builtin_addc(a.l[j], t[j], cy, &cy);
-  }
-}
 // a -= m if a >= m
 LB_DEV void lz_csub(lz& a, const uint32_t* m) {
   uint32_t s[12], br = 0;
@@ -92,17 +70,44 @@ LB_DEV void lz_csub(lz& a, const uint32_t* m) {
   for (int j = 0; j < 12; j++) a.l[j] = br ? a.l[j] : s[j];
 }
 // sum of the terms [t0, t1) (values val(code)) into r, reduced to < 2p
-// (operands of fp_mul: x y < 4p^2 < p R) or to < p (canonical outputs)
+// (operands of fp_mul: x y < 4p^2 < p R) or to < p (canonical outputs).
+// Limb-wise 64-bit accumulation: positive terms into P, negative ones into N,
+// no carry chain per term (a 12-limb carry chain pads every step with s_nop on
+// gfx950); one signed carry pass at the end forms P - N + kneg p, kneg = the
+// negative weight, which is >= 0 and < w p <= 8p < 2^384.
 template <class Val>
 LB_DEV void lz_sum(fp& r, const uint16_t* term, int t0, int t1, Val val, bool canonical) {
-  lz a;
-  lz_zero(a);
+  uint64_t P[12], N[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) P[j] = N[j] = 0;
   int w = 0;
+  uint32_t kneg = 0;
   for (int t = t0; t < t1; t++) {
     const uint16_t tm = term[t];
     const int c = (int8_t)(tm >> 8);
-    lz_term(a, val(tm & 255), c);
-    w += c < 0 ? -c : c;
+    const fp& v = val(tm & 255);
+    if (c > 0) {
+      for (int q = 0; q < c; q++) {
+#pragma unroll
+        for (int j = 0; j < 12; j++) P[j] += v.l[j];
+      }
+      w += c;
+    } else {
+      for (int q = 0; q < -c; q++) {
+#pragma unroll
+        for (int j = 0; j < 12; j++) N[j] += v.l[j];
+      }
+      w -= c;
+      kneg += (uint32_t)(-c);
+    }
+  }
+  lz a;
+  int64_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    const int64_t t = (int64_t)P[j] - (int64_t)N[j] + (int64_t)((uint64_t)P_[j] * kneg) + carry;
+    a.l[j] = (uint32_t)t;
+    carry = t >> 32;  // arithmetic: a limb's partial result may be negative
   }
   if (w > 4) lz_csub(a, WC_P4);
   if (w > 2) lz_csub(a, WC_P2);
