@@ -385,7 +385,9 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     # lane, its own Fp12 squarings), so its work per set is that organisation's count
     lone = oc.get("lone_call_stages", {}).get(dom) if iso_ms else None
     per_set_pipe = per_set
-    if lone and n_req >= 64:  # bls_host.hip: a lone call splits from 64 requests up
+    split_env = os.environ.get("LB_ACC_SPLIT")  # bls_host.hip: 1 always, 0 never,
+    split = split_env != "0" and (split_env == "1" or n_req >= 64)  # default: lone calls from 64 requests
+    if lone and split:
         per_set = lone["mads_per_set"]
     mads = per_set * n
     achieved = mads / (timing[dom] * 1e-3) / 1e12
