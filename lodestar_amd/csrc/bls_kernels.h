@@ -28,8 +28,11 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #ifndef LB_W_HASH
 #define LB_W_HASH 2
 #endif
-#ifndef LB_W_MAP  // k_hash_half (SHA-256 + SSWU + isogeny, small live state)
-#define LB_W_MAP 4
+// k_hash_half (SHA-256 + SSWU + isogeny): 2, not 4 -- the binary-GCD inversion
+// in its call graph takes 228 VGPRs, so 4 waves/SIMD is out of reach, and a
+// 128-register target for the kernel body only adds spills (1,328 vs 704 B/lane)
+#ifndef LB_W_MAP
+#define LB_W_MAP 2
 #endif
 #ifndef LB_W_DECODE
 #define LB_W_DECODE 2
