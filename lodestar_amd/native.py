@@ -180,12 +180,16 @@ def _u8(b) -> np.ndarray:
 def pack_blobs(items: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
     """Concatenate variable-length byte strings -> (blob, offsets[n+1])."""
     offs = np.zeros(len(items) + 1, dtype=np.uint32)
-    total = 0
-    for i, it in enumerate(items):
-        total += len(it)
-        offs[i + 1] = total
-    blob = np.frombuffer(b"".join(bytes(x) for x in items), dtype=np.uint8).copy() if total else np.zeros(1, np.uint8)
-    return blob, offs
+    if len(items):
+        offs[1:] = np.cumsum(np.fromiter((len(x) for x in items), dtype=np.uint64, count=len(items)))
+    total = int(offs[-1])
+    if not total:
+        return np.zeros(1, np.uint8), offs
+    try:
+        joined = b"".join(items)  # bytes-like items: no per-item copy
+    except TypeError:
+        joined = b"".join(bytes(x) for x in items)
+    return np.frombuffer(joined, dtype=np.uint8).copy(), offs
 
 
 @dataclass
@@ -350,11 +354,11 @@ class Device:
                 raise ValueError("signing root must be 32 bytes")
             job_off[j + 1] = job_off[j] + len(pks)
         ns = int(job_off[-1])
-        all_sigs = [bytes(s) for _, sigs, _ in jobs for s in sigs]
-        blob, offs = pack_blobs(all_sigs)
+        blob, offs = pack_blobs([s for _, sigs, _ in jobs for s in sigs])
         msgs = _u8(b"".join(bytes(m) for _, _, m in jobs))
         if by_index:
-            idx = np.ascontiguousarray([int(k) for pks, _, _ in jobs for k in pks] or [0], dtype=np.uint32)
+            idx = (np.concatenate([np.asarray(pks, dtype=np.uint32).reshape(-1) for pks, _, _ in jobs])
+                   if ns else np.zeros(1, np.uint32))
             pk = None
         else:
             pk = _u8(b"".join(bytes(k) for pks, _, _ in jobs for k in pks) or b"\0")
@@ -367,8 +371,10 @@ class Device:
         st = _Stats()
         rc = self.lib.lb_verify_same_message_batch(self._h, ctypes.byref(b), _ptr(out), _ptr(fast), ctypes.byref(st))
         self._check(rc, "lb_verify_same_message_batch")
-        res = [[bool(x) for x in out[job_off[j]:job_off[j + 1]]] for j in range(nj)]
-        return res, [bool(x) for x in fast], (int(st.batch_retries), int(st.batch_sigs_success))
+        flat = out[:ns].astype(bool).tolist()
+        bounds = job_off.tolist()
+        res = [flat[bounds[j]:bounds[j + 1]] for j in range(nj)]
+        return res, fast.astype(bool).tolist(), (int(st.batch_retries), int(st.batch_sigs_success))
 
     def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
                                d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,
