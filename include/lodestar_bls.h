@@ -3,8 +3,8 @@
  *
  * This is the drop-in boundary for Lodestar's BLS hot path
  * (packages/beacon-node/src/chain/bls).  Every entry point takes plain
- * pointers and sizes; no torch or HIP types cross the boundary.  The N-API
- * stub a maintainer would add on the Lodestar side is in INTEGRATION.md.
+ * pointers and sizes; no torch or HIP types cross the boundary.  Lodestar binds
+ * it through the N-API addon lodestar_amd/napi/addon.cc.
  *
  * Reference interfaces replaced (paths relative to packages/beacon-node/src/):
  *   lb_verify_requests      <- worker verifyManySignatureSets(BlsWorkReq[]) -> BlsWorkResult
@@ -120,9 +120,13 @@ typedef struct {
   /* Optional (NULL => use `pubkeys`): pk_offsets[n_sets] (or n_sets) u32 validator
    * indices into the context's device-resident pubkey table (lb_pubkey_table_append);
    * `pubkeys` is then ignored and may be NULL.  An index >= the table size makes
-   * its request LB_REQ_BAD_PUBKEY (the reference would index index2pubkey out of range). */
+   * its request LB_REQ_BAD_PUBKEY (the reference would index index2pubkey out of range).
+   * Mixed packages (e.g. a capella block: validator-index keys plus the BLS-change
+   * keys that are not in the table): with BOTH pubkey_indices and pubkeys given, an
+   * entry with LB_PK_ROW_FLAG set names row (entry & ~LB_PK_ROW_FLAG) of `pubkeys`. */
   const uint32_t* pubkey_indices;
 } lb_request_batch;
+#define LB_PK_ROW_FLAG 0x80000000u
 
 typedef struct {
   uint32_t batch_retries;      /* the DEVICE's merged check: 1 when it failed and requests were
@@ -255,6 +259,14 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys, uint8_
 int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* signatures, const uint32_t* sig_offsets,
                             uint8_t* out192, int32_t* out_bad_index);
 
+/* PublicKey.fromBytes(bytes, CoordType.affine, validate=true) for n keys of pk_len
+ * (48 compressed / 96 uncompressed) bytes: out96 = the uncompressed encoding,
+ * out_status[i] = LB_SET_OK, or LB_SET_BAD_ENCODING / NOT_ON_CURVE / NOT_IN_GROUP /
+ * PK_INFINITY for a key the reference's fromBytes would throw on (out96 then holds
+ * the infinity encoding).  Used for the fromBlsPubkey of BLS-to-execution changes
+ * (state-transition/src/signatureSets/blsToExecutionChange.ts:30). */
+int lb_pubkeys_from_bytes(lb_ctx* ctx, uint32_t n, const uint8_t* pubkeys, uint32_t pk_len, uint8_t* out96,
+                          uint8_t* out_status);
 /* ---- device-resident pubkey table ----------------------
  * Mirror of the beacon node's index2pubkey cache
  * (state-transition/src/cache/pubkeyCache.ts:56-77 syncPubkeys, held in

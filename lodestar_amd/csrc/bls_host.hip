@@ -823,12 +823,20 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   const uint32_t* pk_off = b->pk_offsets;
   const size_t n_pk = pk_off ? pk_off[ns] : ns;
   const bool by_index = b->pubkey_indices != nullptr;
+  // mixed package: rows of `pubkeys` named by flagged indices (every row < n_rows is staged)
+  size_t n_rows = 0;
+  if (by_index && b->pubkeys)
+    for (size_t k = 0; k < n_pk; k++) {
+      const uint32_t j = b->pubkey_indices[k];
+      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & ~LB_PK_ROW_FLAG) + 1 > n_rows) n_rows = (j & ~LB_PK_ROW_FLAG) + 1;
+    }
   const size_t sig_bytes = b->sig_offsets[ns];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t sz_req = sizeof(uint32_t) * (nr + 1), sz_pko = pk_off ? sizeof(uint32_t) * (ns + 1) : 0,
                sz_pk = n_pk * (by_index ? sizeof(uint32_t) : 96), sz_msg = (size_t)ns * 32,
-               sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = sig_bytes, sz_seed = 32;
-  const size_t in_bytes = al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed);
+               sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = sig_bytes, sz_seed = 32, sz_rows = n_rows * 96;
+  const size_t in_bytes =
+      al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed) + al(sz_rows);
   const size_t out_bytes = al(nr ? nr : 1) * 2 + al(ns ? ns : 1);
   LB_TRY(finish_slot(ctx, sl));
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
@@ -847,6 +855,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   stage(b->sig_offsets, sz_sigo);
   stage(b->signatures, sz_sig);
   stage(b->seed, sz_seed);
+  if (n_rows) stage(b->pubkeys, sz_rows);
   char* d_in = ws.take<char>(in_bytes);
   uint8_t* d_valid = ws.take<uint8_t>(nr ? nr : 1);
   uint8_t* d_err = ws.take<uint8_t>(nr ? nr : 1);
@@ -876,8 +885,9 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
   const uint8_t* d_sig = (const uint8_t*)dptr(sz_sig);
   const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
+  const uint8_t* d_rows = n_rows ? (const uint8_t*)dptr(sz_rows) : nullptr;
   if (nr) {
-    LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? nullptr : d_pks, d_pko,
+    LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? d_rows : d_pks, d_pko,
                         by_index ? (const uint32_t*)d_pks : nullptr, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst,
                         ws, d_partial));
   } else if (partial) {
@@ -904,10 +914,21 @@ static void fill_stats(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   }
 }
 
+// Round robin over the slots, passing over a slot whose two-phase call still
+// waits for the host's combined verdict (reusing it would retire that call with
+// merged_ok = 0: correct verdicts, but every request's tail re-run); only when
+// every slot holds a pending partial is the next one taken anyway.
 static Slot& next_async_slot(lb_ctx* ctx) {  // internal: not part of the C ABI
-  Slot& sl = ctx->slots[ctx->next_slot];
-  ctx->next_slot = (ctx->next_slot + 1) % ctx->n_slots;
-  return sl;
+  int s = ctx->next_slot;
+  for (int k = 0; k < ctx->n_slots; k++) {
+    const int c = (ctx->next_slot + k) % ctx->n_slots;
+    if (!ctx->slots[c].partial_pending) {
+      s = c;
+      break;
+    }
+  }
+  ctx->next_slot = (s + 1) % ctx->n_slots;
+  return ctx->slots[s];
 }
 
 int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
@@ -958,6 +979,9 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
   LB_HIP(hipSetDevice(ctx->device));
   Slot* sl = slot_of_ticket(ctx, ticket);
   if (!sl || !sl->partial_pending) {
+    // a two-phase call another call's slot reuse already resumed (with merged_ok
+    // = 0: every request re-verified alone, so its verdicts stand): nothing to do
+    if (ticket != 0 && ticket < ctx->next_ticket) return LB_OK;
     ctx->err = "ticket is not a pending two-phase call";
     return LB_ERR_INVALID_ARGUMENT;
   }
@@ -1117,6 +1141,25 @@ int lb_aggregate_pubkeys(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint8_t* o
   LB_HIP(hipStreamSynchronize(ctx->stream));
   if (st == LB_ST_PK_INFINITY) st = LB_ST_OK;  // an infinite aggregate is a valid encoding (0x40...)
   if (out_status) *out_status = st;
+  return LB_OK;
+}
+
+int lb_pubkeys_from_bytes(lb_ctx* ctx, uint32_t n, const uint8_t* pks, uint32_t pk_len, uint8_t* out96,
+                          uint8_t* out_status) {
+  if (!ctx || (n && (!pks || !out96 || !out_status)) || (pk_len != 48 && pk_len != 96)) return LB_ERR_INVALID_ARGUMENT;
+  if (n == 0) return LB_OK;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  LB_TRY(ensure_ws(ctx, (size_t)n * (pk_len + 96 + 1) + 8192));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  void* d_in;
+  LB_TRY(upload(ctx, ws, pks, (size_t)n * pk_len, &d_in));
+  uint8_t* d_out = ws.take<uint8_t>((size_t)n * 96);
+  uint8_t* d_st = ws.take<uint8_t>(n);
+  LB_LAUNCH(k_pubkey_validate, blocks_for(n), TPB, n, (const uint8_t*)d_in, pk_len, d_out, d_st);
+  LB_HIP(hipMemcpyAsync(out96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipMemcpyAsync(out_status, d_st, n, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
   return LB_OK;
 }
 

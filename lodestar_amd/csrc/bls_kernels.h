@@ -63,9 +63,12 @@ struct PkSource {
   uint32_t table_n;
 };
 // Pubkey k of the call; an index outside the table is a bad pubkey (LB_REQ_BAD_PUBKEY).
+// In a mixed package (index AND bytes given) an index with bit 31 set is row
+// (j & 0x7fffffff) of the call's 96-byte pubkeys (the host checked the rows exist).
 LB_DEV uint8_t pk_load(g1a& p, const PkSource& s, uint32_t k) {
   if (s.index) {
     const uint32_t j = s.index[k];
+    if ((j & LB_PK_ROW_FLAG) && s.bytes) return g1_deserialize(p, s.bytes + (size_t)(j & ~LB_PK_ROW_FLAG) * 96, 96);
     if (j >= s.table_n) {
       p.inf = true;
       return LB_ST_BAD_ENCODING;
@@ -91,6 +94,8 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource p
 __global__ void __launch_bounds__(TPB) k_table_decode(uint32_t n, const uint8_t* __restrict__ in, uint32_t len,
                                                       g1a* __restrict__ out, uint8_t* __restrict__ status);
 __global__ void k_g1a_serialize(uint32_t n, const g1a* __restrict__ in, uint8_t* __restrict__ out96);
+__global__ void __launch_bounds__(TPB) k_pubkey_validate(uint32_t n, const uint8_t* __restrict__ in, uint32_t len,
+                                                         uint8_t* __restrict__ out96, uint8_t* __restrict__ status);
 __global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
 __global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);

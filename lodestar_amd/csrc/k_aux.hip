@@ -55,6 +55,26 @@ __global__ void __launch_bounds__(TPB) k_table_decode(uint32_t n, const uint8_t*
   status[i] = g1_deserialize(p, in + (size_t)i * len, len);
   out[i] = p;
 }
+// PublicKey.fromBytes(bytes, affine, validate=true) (blst key_validate: a valid
+// encoding, not infinity, in G1), re-encoded uncompressed; the BLS-to-execution
+// change pubkeys of a capella+ block (signatureSets/blsToExecutionChange.ts:30)
+__global__ void __launch_bounds__(TPB) k_pubkey_validate(uint32_t n, const uint8_t* __restrict__ in, uint32_t len,
+                                                         uint8_t* __restrict__ out96, uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a p;
+  uint8_t st = g1_deserialize(p, in + (size_t)i * len, len);
+  if (st == LB_ST_OK && p.inf) st = LB_ST_PK_INFINITY;
+  if (st == LB_ST_OK) {
+    g1j j;
+    jac_from_aff(j, p);
+    if (!g1_in_subgroup(j)) st = LB_ST_NOT_IN_GROUP;
+  }
+  if (st != LB_ST_OK) p.inf = true;
+  g1_serialize(out96 + (size_t)i * 96, p);
+  status[i] = st;
+}
+
 __global__ void k_g1a_serialize(uint32_t n, const g1a* __restrict__ in, uint8_t* __restrict__ out96) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -37,6 +37,7 @@ const MAX_BUFFERED_SIGS = 32; // index.ts:66
 const MAX_BUFFER_WAIT_MS = 100; // index.ts:75
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // index.ts:80
 const BATCHABLE_MIN_PER_CHUNK = 16; // worker.ts:17
+const LB_PK_ROW_FLAG = 0x80000000;
 const LB_REQ_EMPTY_AGGREGATE = 1;
 const LB_REQ_BAD_PUBKEY = 2;
 const GT_BYTES = 576;
@@ -133,8 +134,19 @@ function packRequests(requests, seed) {
   };
   if (keys.length > 0 && keys.every((k) => k.index !== undefined)) {
     batch.pubkeyIndices = Uint32Array.from(keys.map((k) => k.index));
+  } else if (keys.some((k) => k.index !== undefined)) {
+    // mixed package (a capella block's BLS-change keys beside validator keys): table
+    // indices, plus flagged indices naming rows of the shipped 96-byte keys (LB_PK_ROW_FLAG)
+    const rows = [];
+    batch.pubkeyIndices = Uint32Array.from(
+      keys.map((k) => {
+        if (k.index !== undefined) return k.index;
+        rows.push(k.bytes);
+        return (LB_PK_ROW_FLAG | (rows.length - 1)) >>> 0;
+      })
+    );
+    batch.pubkeys = concat(rows, 96 * rows.length);
   } else {
-    if (keys.some((k) => !k.bytes)) throw new TypeError("mixed package: index-only pubkeys need their bytes");
     batch.pubkeys = concat(
       keys.map((k) => k.bytes),
       96 * keys.length
@@ -233,6 +245,13 @@ const M = {
   TOTAL_SIG_SETS: P + "sig_sets_total",
   PRIORITIZED_SIG_SETS: P + "prioritized_sig_sets_total",
   BATCHABLE_SIG_SETS: P + "batchable_sig_sets_total",
+  // lodestar.ts:486,491: the main thread's share of deserialization / aggregation.  Both run on
+  // the GPU here; what stays on the main thread is packing the keys and signature bytes
+  SIG_DESERIALIZATION_MAIN_THREAD: P + "signature_deserialization_main_thread_time_seconds",
+  PUBKEYS_AGGREGATION_MAIN_THREAD: P + "pubkeys_aggregation_main_thread_time_seconds",
+  // lodestar.ts:500,505 (single-thread mode)
+  SINGLE_THREAD_TIME: "lodestar_bls_single_thread_time_seconds",
+  SINGLE_THREAD_TIME_PER_SIGSET: "lodestar_bls_single_thread_time_per_sigset_seconds",
 };
 
 function hrNowNs() {
@@ -412,8 +431,25 @@ class BlsGpuVerifier {
     let outs;
     try {
       const waits = [];
-      if (def.length) waits.push(backend.verifyRequests(packRequests(def.map((j) => j.sets), this.seedSource())));
-      if (same.length) waits.push(backend.verifySameMessage(packSameMessage(same, this.seedSource())));
+      if (def.length) {
+        // the main thread's share of pubkey aggregation (jobItem.ts:55-63 / utils.ts:12):
+        // packing the keys; the sum itself runs on the GPU
+        const t0 = process.hrtime();
+        const batch = packRequests(def.map((j) => j.sets), this.seedSource());
+        const [s0, ns0] = process.hrtime(t0);
+        if (def.some((j) => j.sets.some((x) => x.type === "aggregate")))
+          m.observe(M.PUBKEYS_AGGREGATION_MAIN_THREAD, s0 + ns0 / 1e9);
+        waits.push(backend.verifyRequests(batch));
+      }
+      if (same.length) {
+        // jobItem.ts:72-74 times Signature.fromBytes on the main thread; here the bytes are
+        // only packed (every signature is decoded once, on the GPU)
+        const t0 = process.hrtime();
+        const batch = packSameMessage(same, this.seedSource());
+        const [s0, ns0] = process.hrtime(t0);
+        m.observe(M.SIG_DESERIALIZATION_MAIN_THREAD, s0 + ns0 / 1e9);
+        waits.push(backend.verifySameMessage(batch));
+      }
       outs = await Promise.all(waits);
     } catch (e) {
       // device failure rejects every job of the package (index.ts:503-512)
@@ -489,16 +525,30 @@ class BlsGpuSingleThreadVerifier {
   constructor(o = {}) {
     this.backend = o.backend || new (loadAddon().Context)(o.device || 0);
     this.seedSource = o.seedSource || (() => new Uint8Array(crypto.randomBytes(32)));
+    this.metrics = o.metrics || new PoolMetrics();
+  }
+  /** singleThread.ts:27-35 times the verification (mainThreadDurationInThreadPool); the
+   * single-thread histograms of lodestar.ts:498-508 get the same duration, and per set. */
+  observe(t0, nSets) {
+    const [s, ns] = process.hrtime(t0);
+    const sec = s + ns / 1e9;
+    this.metrics.observe(M.MAIN_THREAD_TIME, sec);
+    this.metrics.observe(M.SINGLE_THREAD_TIME, sec);
+    if (nSets > 0) this.metrics.observe(M.SINGLE_THREAD_TIME_PER_SIGSET, sec / nSets);
   }
   async verifySignatureSets(sets) {
+    const t0 = process.hrtime();
     const r = await this.backend.verifyRequests(packRequests([sets], this.seedSource()));
     if (r.errors[0] === LB_REQ_EMPTY_AGGREGATE) throw new Error("EMPTY_AGGREGATE_ARRAY");
     if (r.errors[0] === LB_REQ_BAD_PUBKEY) throw new Error("invalid pubkey encoding");
+    this.observe(t0, sets.length); // counted only for runs without an exception, as the reference
     return r.valid[0] === 1;
   }
   async verifySignatureSetsSameMessage(sets, message) {
     if (sets.length === 0) throw new Error("EMPTY_AGGREGATE_ARRAY"); // PublicKey.aggregate([]) throws (singleThread.ts:43)
+    const t0 = process.hrtime();
     const r = await this.backend.verifySameMessage(packSameMessage([{sets, message}], this.seedSource()));
+    this.observe(t0, sets.length);
     return Array.from(r.valid.subarray(0, sets.length), (v) => v === 1);
   }
   async close() {
@@ -530,22 +580,38 @@ function shardRequests(sizes, nShards) {
 }
 
 /** One call over several GPUs (SURVEY §8e): each shard runs to its 576-byte Fp12
- * partial, the host combines them with ONE final exponentiation (gtCheck on the first
- * GPU) and resumes every shard with the verdict.  Returns {valid, errors, mergedOk}. */
+ * partial, the host combines them with ONE final exponentiation (gtCheck on the GPU of
+ * the largest shard, not always the first) and resumes every shard with the verdict.
+ * A shard that fails in phase 1 fails the call after the others are resumed.
+ * Returns {valid, errors, mergedOk}. */
 async function verifyRequestsSharded(backends, requests, seedSource) {
   const shards = shardRequests(
     requests.map((r) => r.length),
     backends.length
-  ).filter(([lo, hi]) => hi > lo);
-  const calls = await Promise.all(
-    shards.map(([lo, hi], g) => backends[g].verifyRequestsPartial(packRequests(requests.slice(lo, hi), seedSource())))
+  )
+    .map(([lo, hi], g) => [lo, hi, g])
+    .filter(([lo, hi]) => hi > lo);
+  const settled = await Promise.allSettled(
+    shards.map(([lo, hi, g]) => backends[g].verifyRequestsPartial(packRequests(requests.slice(lo, hi), seedSource())))
   );
+  const failed = settled.find((x) => x.status === "rejected");
+  if (failed) {
+    await Promise.allSettled(
+      settled.map((x, i) => (x.status === "fulfilled" ? backends[shards[i][2]].finish(x.value.id, false) : null))
+    );
+    throw failed.reason;
+  }
+  const calls = settled.map((x) => x.value);
   const partials = concat(
     calls.map((c) => c.partial),
     GT_BYTES * calls.length
   );
-  const mergedOk = calls.length === 0 ? true : await backends[0].gtCheck(partials);
-  const res = await Promise.all(calls.map((c, g) => backends[g].finish(c.id, mergedOk)));
+  let big = 0;
+  shards.forEach(([lo, hi], i) => {
+    if (hi - lo > shards[big][1] - shards[big][0]) big = i;
+  });
+  const mergedOk = calls.length === 0 ? true : await backends[shards[big][2]].gtCheck(partials);
+  const res = await Promise.all(calls.map((c, i) => backends[shards[i][2]].finish(c.id, mergedOk)));
   const valid = new Uint8Array(requests.length);
   const errors = new Uint8Array(requests.length);
   shards.forEach(([lo], g) => {

@@ -122,7 +122,7 @@ struct Task {
   // inputs (copied on the JS thread)
   std::vector<uint32_t> req_off, pk_off, sig_off, pk_idx, job_off;
   std::vector<uint8_t> pubkeys, messages, signatures, seed, batchable;
-  bool has_pk_off = false, by_index = false, has_batchable = false;
+  bool has_pk_off = false, by_index = false, has_batchable = false, mixed = false;
   uint32_t n_req = 0, n_sets = 0, n_jobs = 0, pk_len = 0, n_keys = 0;
   int merged_ok = 0;
   uint64_t partial_id = 0;
@@ -160,6 +160,13 @@ void parse_requests(napi_env env, napi_value obj, Task& t) {
   t.by_index = opt_typed(env, obj, "pubkeyIndices", napi_uint32_array, t.pk_idx);
   if (t.by_index) {
     if (t.pk_idx.size() != n_pk) throw ArgError{"pubkeyIndices: one index per pubkey"};
+    // mixed package: rows of `pubkeys` named by indices with LB_PK_ROW_FLAG set
+    size_t rows = 0;
+    for (const uint32_t j : t.pk_idx)
+      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & ~LB_PK_ROW_FLAG) + 1 > rows) rows = (j & ~LB_PK_ROW_FLAG) + 1;
+    t.mixed = opt_typed(env, obj, "pubkeys", napi_uint8_array, t.pubkeys);
+    if (rows && (!t.mixed || t.pubkeys.size() < rows * LB_PUBKEY_BYTES))
+      throw ArgError{"pubkeyIndices name pubkey rows that `pubkeys` does not hold"};
   } else {
     if (!opt_typed(env, obj, "pubkeys", napi_uint8_array, t.pubkeys) && n_pk)
       throw ArgError{"missing pubkeys (or pubkeyIndices)"};
@@ -179,7 +186,7 @@ lb_request_batch batch_of(Task& t) {
   b.n_sets = t.n_sets;
   b.request_offsets = t.req_off.data();
   b.request_batchable = t.has_batchable ? t.batchable.data() : nullptr;
-  b.pubkeys = t.by_index ? nullptr : t.pubkeys.data();
+  b.pubkeys = (!t.by_index || t.mixed) ? t.pubkeys.data() : nullptr;
   b.pk_offsets = t.has_pk_off ? t.pk_off.data() : nullptr;
   b.messages = t.messages.data();
   b.signatures = t.signatures.data();

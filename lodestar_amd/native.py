@@ -39,10 +39,12 @@ EXPORTED_SYMBOLS = (
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
+    "lb_pubkeys_from_bytes",
 )
 
 LB_BATCH_DEVICE = 1
 LB_GT_BYTES = 576
+LB_PK_ROW_FLAG = 0x80000000  # mixed packages: an index naming a row of the call's 96-byte pubkeys
 
 
 class LodestarBlsError(RuntimeError):
@@ -152,6 +154,7 @@ def load_library() -> ctypes.CDLL:
                                                  ctypes.POINTER(_Stats)]
     lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
     lib.lb_pubkey_table_append.argtypes = [vp, u32, vp, u32, ctypes.POINTER(ctypes.c_int32)]
+    lib.lb_pubkeys_from_bytes.argtypes = [vp, u32, vp, u32, vp, vp]
     lib.lb_pubkey_table_size.argtypes = [vp, ctypes.POINTER(u32)]
     lib.lb_pubkey_table_read.argtypes = [vp, u32, u32, vp]
     lib.lb_pubkey_table_truncate.argtypes = [vp, u32]
@@ -461,6 +464,22 @@ class Device:
                                               ctypes.byref(bad))
         self._check(rc, "lb_aggregate_signatures")
         return out.tobytes(), int(bad.value)
+
+    def pubkeys_from_bytes(self, pubkeys: Sequence[bytes]) -> Tuple[List[bytes], List[int]]:
+        """PublicKey.fromBytes(b, affine, validate=true) on the GPU for keys of one length
+        (48 or 96): (96-byte uncompressed encodings, per-key status; 0 = valid)."""
+        n = len(pubkeys)
+        if n == 0:
+            return [], []
+        pk_len = len(pubkeys[0])
+        if pk_len not in (48, 96) or any(len(p) != pk_len for p in pubkeys):
+            raise ValueError("pubkeys_from_bytes expects keys of one encoding length (48 or 96)")
+        blob = _u8(b"".join(pubkeys))
+        out = np.zeros(n * 96, np.uint8)
+        st = np.zeros(n, np.uint8)
+        self._check(self.lib.lb_pubkeys_from_bytes(self._h, n, _ptr(blob), pk_len, _ptr(out), _ptr(st)),
+                    "lb_pubkeys_from_bytes")
+        return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)], [int(x) for x in st]
 
     # -- device-resident pubkey table (index2pubkey mirror) -------------------------
     def pubkey_table_append(self, pubkeys: Sequence[bytes]) -> int:

@@ -15,8 +15,8 @@ RCCL over xGMI is not used: per GPU the exchange is 576 bytes.
 * ``ShardedVerifier``: one process driving several local GPUs (one lb_ctx and
   one submission thread per GPU), with the Fp12-partial combine.
 * ``verify_distributed``: one process per GPU under torch.distributed (gloo,
-  host memory): the partials are all-gathered (576 B per rank), every rank runs
-  the same combined check on its own GPU, then the verdict bytes are gathered.
+  host memory): the partials are all-gathered (576 B per rank), rank 0 runs the
+  combined check and broadcasts it, then the verdict bytes are gathered.
 """
 from __future__ import annotations
 
@@ -104,10 +104,30 @@ class ShardedVerifier:
         # phase 1: every GPU runs its shard up to the merged Miller product
         futs = [(g, lo, hi, self.backends[g].submit_requests(list(requests[lo:hi]), partial=True))
                 for g, lo, hi in live]
-        calls = [(g, lo, hi, f.result()) for g, lo, hi, f in futs]
-        # host combine: prod of the <= 8 partials, one final exponentiation (on GPU 0)
+        calls, errors = [], []
+        for g, lo, hi, f in futs:
+            try:
+                calls.append((g, lo, hi, f.result()))
+            except BaseException as ex:  # noqa: BLE001 -- re-raised below, after the others are resumed
+                errors.append(ex)
+        if errors:
+            # never leave a shard's slot holding a partial: resume every call that got one
+            # (merged_ok = False: each runs its own per-request tails), then fail the call
+            for _, _, _, c in calls:
+                try:
+                    c.backend.finish(c, False).result()
+                except BaseException:  # noqa: BLE001
+                    pass
+            raise errors[0]
+        # host combine: prod of the <= 8 partials, one final exponentiation on the GPU of the
+        # largest shard (shards are balanced, so the check lands on a different GPU per call
+        # rather than always on GPU 0)
         partials = [c.partial for _, _, _, c in calls]
-        ok = bool(self.backends[calls[0][0]].gt_check(partials).result()) if calls else True
+        if calls:
+            gi = max(range(len(calls)), key=lambda i: (calls[i][2] - calls[i][1], -i))
+            ok = bool(self.backends[calls[gi][0]].gt_check(partials).result())
+        else:
+            ok = True
         self.last_combine = {"merged_ok": ok, "n_partials": len(partials)}
         # phase 2: resume every shard with the combined verdict
         fins = [(lo, hi, c.backend.finish(c, ok)) for _, lo, hi, c in calls]
@@ -124,36 +144,64 @@ def verify_distributed(requests: Sequence, verify_local: Optional[Callable[[list
                        rank: int, world: int, backend: Optional[object] = None) -> Tuple[List[bool], List[int]]:
     """torch.distributed version (one process per GPU): every rank holds the
     same request list and verifies its own shard.  With a two-phase ``backend``
-    the ranks all-gather their 576-byte partials (gloo, host memory), each runs
-    the same combined check on its own GPU (no broadcast needed) and resumes its
+    the ranks all-gather their 576-byte partials (gloo, host memory), rank 0 runs
+    the ONE combined check and broadcasts its verdict, and every rank resumes its
     shard; otherwise ``verify_local`` verifies the shard alone.  All ranks
-    receive every verdict (gloo all_gather of one int per request)."""
+    receive every verdict (gloo all_gather of one int per request).  A rank whose
+    shard raises still joins every collective (with an error flag), so all ranks
+    fail together instead of leaving the others blocked."""
     import torch
     import torch.distributed as dist
     shards = shard_requests([len(r) for r in requests], world)
     lo, hi = shards[rank]
+    err: Optional[BaseException] = None
+    v: List[bool] = []
+    e: List[int] = []
     if backend is not None and _two_phase(backend):
-        call = backend.submit_requests(list(requests[lo:hi]), partial=True).result() if hi > lo else None
-        part = torch.zeros(GT_BYTES + 1, dtype=torch.uint8)
+        call = None
+        try:
+            call = backend.submit_requests(list(requests[lo:hi]), partial=True).result() if hi > lo else None
+        except BaseException as ex:  # noqa: BLE001
+            err = ex
+        part = torch.zeros(GT_BYTES + 2, dtype=torch.uint8)
         if call is not None:
             part[:GT_BYTES] = torch.frombuffer(bytearray(call.partial), dtype=torch.uint8)
             part[GT_BYTES] = 1
-        parts = [torch.zeros(GT_BYTES + 1, dtype=torch.uint8) for _ in range(world)]
+        part[GT_BYTES + 1] = 1 if err is not None else 0
+        parts = [torch.zeros(GT_BYTES + 2, dtype=torch.uint8) for _ in range(world)]
         dist.all_gather(parts, part)
-        partials = [bytes(p[:GT_BYTES].tolist()) for p in parts if int(p[GT_BYTES]) == 1]
-        ok = bool(backend.gt_check(partials).result())
+        any_err = any(int(p[GT_BYTES + 1]) for p in parts)
+        verdict = torch.zeros(1, dtype=torch.int32)
+        if rank == 0 and not any_err:
+            partials = [bytes(p[:GT_BYTES].tolist()) for p in parts if int(p[GT_BYTES]) == 1]
+            try:
+                verdict[0] = 1 if bool(backend.gt_check(partials).result()) else 0
+            except BaseException as ex:  # noqa: BLE001
+                err, verdict[0] = ex, -1
+        dist.broadcast(verdict, 0)
+        any_err = any_err or int(verdict[0]) < 0
         if call is not None:
-            v, e, _ = backend.finish(call, ok).result()
-        else:
-            v, e = [], []
+            try:
+                v, e, _ = backend.finish(call, (not any_err) and int(verdict[0]) == 1).result()
+            except BaseException as ex:  # noqa: BLE001
+                err = err or ex
     else:
-        v, e = verify_local(list(requests[lo:hi])) if hi > lo else ([], [])
+        try:
+            v, e = verify_local(list(requests[lo:hi])) if hi > lo else ([], [])
+        except BaseException as ex:  # noqa: BLE001
+            err = ex
     n = len(requests)
-    mine = torch.zeros(n, dtype=torch.int32)
-    if hi > lo:
+    mine = torch.zeros(n + 1, dtype=torch.int32)
+    if hi > lo and err is None:
         mine[lo:hi] = torch.tensor([int(x) | (int(y) << 8) for x, y in zip(v, e)], dtype=torch.int32)
-    gathered = [torch.zeros(n, dtype=torch.int32) for _ in range(world)]
+    mine[n] = 1 if err is not None else 0
+    gathered = [torch.zeros(n + 1, dtype=torch.int32) for _ in range(world)]
     dist.all_gather(gathered, mine)
+    if err is not None:
+        raise err
+    bad = [r for r in range(world) if int(gathered[r][n])]
+    if bad:
+        raise RuntimeError(f"verify_distributed: rank(s) {bad} failed")
     combined = np.zeros(n, dtype=np.int32)
     for r, (a, b) in enumerate(shards):
         combined[a:b] = gathered[r].numpy()[a:b]

@@ -39,7 +39,7 @@ from typing import Callable, Deque, List, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from . import metrics as M
-from .native import (LB_REQ_BAD_PUBKEY, LB_REQ_EMPTY_AGGREGATE, BadPubkeyError, Device, EmptyAggregateError,
+from .native import (LB_PK_ROW_FLAG, LB_REQ_BAD_PUBKEY, LB_REQ_EMPTY_AGGREGATE, BadPubkeyError, Device, EmptyAggregateError,
                      pack_blobs)
 
 MAX_SIGNATURE_SETS_PER_JOB = 128      # index.ts:57
@@ -202,13 +202,23 @@ class DeviceBackend:
 
     def _loop(self) -> None:
         inflight: Deque[tuple] = deque()  # (PendingCall, future, post, CallStats)
+        # two-phase calls handed out and not yet finished hold a library slot too: they
+        # count against capacity, so no later call reuses (and silently resumes) their slot
+        self._partials = 0
         while True:
             with self._cv:
                 while not self._q and not inflight and not self._closing:
                     self._cv.wait()
-                item = self._q.popleft() if self._q and len(inflight) < self.capacity else None
+                # a finish never needs a free slot (it resumes its own)
+                head_is_finish = bool(self._q) and self._q[0][0] == "finish"
+                room = len(inflight) + self._partials < self.capacity
+                item = self._q.popleft() if self._q and (room or head_is_finish) else None
                 if item is None and not inflight and self._closing and not self._q:
                     break
+                if item is None and not inflight and self._q:
+                    # every slot holds a partial waiting for its host verdict: hand out the
+                    # next call anyway (the library then resumes the oldest with merged_ok = 0)
+                    item = self._q.popleft()
             if item is not None:
                 kind, payload, fut = item
                 if not fut.set_running_or_notify_cancel():
@@ -219,11 +229,19 @@ class DeviceBackend:
                         requests, partial = payload
                         pc, post = self._submit_requests(requests, partial)
                         if partial:
-                            fut.set_result(PartialCall(self, pc, post, cs, self.dev.partial_wait(pc)))
+                            self._partials += 1
+                            try:
+                                part = self.dev.partial_wait(pc)
+                            except BaseException:
+                                self._partials -= 1
+                                self.dev.verify_finish(pc, False)
+                                raise
+                            fut.set_result(PartialCall(self, pc, post, cs, part))
                         else:
                             inflight.append((pc, fut, post, cs))
                     elif kind == "finish":
                         call, ok = payload
+                        self._partials = max(0, self._partials - 1)
                         self.dev.verify_finish(call.pc, ok)
                         inflight.append((call.pc, fut, call.post, call.stats))
                     else:  # synchronous library calls (same-message batch, table sync, gt check, ...)
@@ -256,10 +274,26 @@ class DeviceBackend:
                 sigs.append(bytes(s.signature))
             req_off.append(len(msgs))
         blob, offs = pack_blobs(sigs)
-        # validator indices when every key has one (device table), else the encodings
-        by_index = bool(keys_all) and all(k.index is not None for k in keys_all)
-        idx = np.array([k.index for k in keys_all], np.uint32) if by_index else None
-        pks = None if by_index else np.frombuffer(b"".join(self._key_bytes(keys_all)) or b"\0", np.uint8)
+        # validator indices when every key has one (device table); a mixed package (e.g. a
+        # capella block's BLS-change keys beside validator keys) ships the byte keys as rows
+        # named by flagged indices (LB_PK_ROW_FLAG); with no index at all, the encodings
+        n_idx = sum(1 for k in keys_all if k.index is not None)
+        idx = pks = None
+        if keys_all and n_idx == len(keys_all):
+            idx = np.array([k.index for k in keys_all], np.uint32)
+        elif n_idx:
+            rows: List[bytes] = []
+            ix = []
+            for k in keys_all:
+                if k.index is not None:
+                    ix.append(k.index)
+                else:
+                    ix.append(LB_PK_ROW_FLAG | len(rows))
+                    rows.append(k.uncompressed)
+            idx = np.array(ix, np.uint32)
+            pks = np.frombuffer(b"".join(rows), np.uint8)
+        else:
+            pks = np.frombuffer(b"".join(self._key_bytes(keys_all)) or b"\0", np.uint8)
         pc = self.dev.verify_requests_async(np.array(req_off, np.uint32), pks, np.array(pk_off, np.uint32),
                                             np.frombuffer(b"".join(msgs) or b"\0", np.uint8), blob, offs,
                                             self.seed_source(), pk_indices=idx, partial=partial)

@@ -1,4 +1,4 @@
-"""Test helper (TEST INFRASTRUCTURE): SSZ encoding of phase0/altair SignedBeaconBlocks
+"""Test helper (TEST INFRASTRUCTURE): SSZ encoding of phase0 ... deneb SignedBeaconBlocks
 and an independent restatement of their hash_tree_root from the structured fields
 (oracle/ssz.py primitives), plus a synthetic signed-block generator for the
 getBlockSignatureSets tests.  The product parser (lodestar_amd/block_sets.py) reads
@@ -7,9 +7,10 @@ the bytes; this side never parses, it builds -- so the two meet only at the root
 Layouts: SignedBeaconBlock{message: BeaconBlock, signature}, BeaconBlock{slot,
 proposer_index, parent_root, state_root, body}, BeaconBlockBody phase0 {randao_reveal,
 eth1_data, graffiti, proposer_slashings, attester_slashings, attestations, deposits,
-voluntary_exits} (+ sync_aggregate in altair) -- the consensus-spec containers the
-reference's @lodestar/types ssz definitions follow (packages/types/src/phase0/sszTypes.ts,
-altair/sszTypes.ts).
+voluntary_exits} (+ sync_aggregate in altair, + execution_payload in bellatrix, +
+bls_to_execution_changes in capella, + blob_kzg_commitments in deneb) -- the
+consensus-spec containers the reference's @lodestar/types ssz definitions follow
+(packages/types/src/{phase0,altair,bellatrix,capella,deneb}/sszTypes.ts).
 """
 from __future__ import annotations
 
@@ -75,6 +76,69 @@ def header_root(h: bytes) -> bytes:
                         h[16:48], h[48:80], h[80:112]])
 
 
+FORK_NAMES = ("phase0", "altair", "bellatrix", "capella", "deneb")
+
+
+def seq(fork: str) -> int:
+    return FORK_NAMES.index(fork)
+
+
+@dataclass
+class Payload:
+    """ExecutionPayload (bellatrix/capella/deneb) from structured fields."""
+    fork: str
+    parent_hash: bytes
+    fee_recipient: bytes          # 20
+    state_root: bytes
+    receipts_root: bytes
+    logs_bloom: bytes             # 256
+    prev_randao: bytes
+    block_number: int
+    gas_limit: int
+    gas_used: int
+    timestamp: int
+    extra_data: bytes
+    base_fee_per_gas: int
+    block_hash: bytes
+    transactions: List[bytes] = field(default_factory=list)
+    withdrawals: List[Tuple[int, int, bytes, int]] = field(default_factory=list)  # index, validator, address, amount
+    blob_gas_used: int = 0
+    excess_blob_gas: int = 0
+
+    def ssz(self) -> bytes:
+        capella = seq(self.fork) >= seq("capella")
+        fixed = 508 + (4 if capella else 0) + (16 if self.fork == "deneb" else 0)
+        txs = var_list(self.transactions)
+        wds = b"".join(le64(i) + le64(v) + a + le64(am) for i, v, a, am in self.withdrawals)
+        head = (self.parent_hash + self.fee_recipient + self.state_root + self.receipts_root + self.logs_bloom +
+                self.prev_randao + le64(self.block_number) + le64(self.gas_limit) + le64(self.gas_used) +
+                le64(self.timestamp) + le32(fixed) + self.base_fee_per_gas.to_bytes(32, "little") + self.block_hash +
+                le32(fixed + len(self.extra_data)))
+        if capella:
+            head += le32(fixed + len(self.extra_data) + len(txs))
+        if self.fork == "deneb":
+            head += le64(self.blob_gas_used) + le64(self.excess_blob_gas)
+        assert len(head) == fixed
+        return head + self.extra_data + txs + (wds if capella else b"")
+
+    def root(self) -> bytes:
+        tx_roots = [S.mix_in_length(S.merkleize(S.pack_bytes(t) if t else [], 1 << 25), len(t))
+                    for t in self.transactions]
+        f = [self.parent_hash, S.bytes_vector_root(self.fee_recipient), self.state_root, self.receipts_root,
+             S.bytes_vector_root(self.logs_bloom), self.prev_randao, S.u64(self.block_number), S.u64(self.gas_limit),
+             S.u64(self.gas_used), S.u64(self.timestamp),
+             S.mix_in_length(S.merkleize(S.pack_bytes(self.extra_data) if self.extra_data else [], 1),
+                             len(self.extra_data)),
+             self.base_fee_per_gas.to_bytes(32, "little"), self.block_hash,
+             S.mix_in_length(S.merkleize(tx_roots, 1 << 20), len(tx_roots))]
+        if seq(self.fork) >= seq("capella"):
+            f.append(S.mix_in_length(S.merkleize([S.merkleize([S.u64(i), S.u64(v), S.bytes_vector_root(a), S.u64(am)])
+                                                  for i, v, a, am in self.withdrawals], 16), len(self.withdrawals)))
+        if self.fork == "deneb":
+            f += [S.u64(self.blob_gas_used), S.u64(self.excess_blob_gas)]
+        return S.merkleize(f)
+
+
 @dataclass
 class Body:
     randao: bytes
@@ -85,23 +149,40 @@ class Body:
     attestations: List[Att] = field(default_factory=list)
     deposits: List[bytes] = field(default_factory=list)  # 1240 bytes each
     exits: List[Tuple[int, int, bytes]] = field(default_factory=list)
-    sync: Optional[Tuple[bytes, bytes]] = None  # (64-byte bits, sig) altair
+    sync: Optional[Tuple[bytes, bytes]] = None  # (64-byte bits, sig) altair+
+    fork: Optional[str] = None                  # None: phase0, or altair when sync is set
+    payload: Optional[Payload] = None           # bellatrix+
+    bls_changes: List[Tuple[int, bytes, bytes, bytes]] = field(default_factory=list)  # vi, pk48, address, sig
+    blobs: List[bytes] = field(default_factory=list)  # deneb: 48-byte commitments
+
+    def _fork(self) -> str:
+        return self.fork or ("altair" if self.sync is not None else "phase0")
 
     def ssz(self) -> bytes:
-        fixed = 220 + (160 if self.sync is not None else 0)
+        fk = seq(self._fork())
+        fixed = 220 + (160 if fk >= 1 else 0) + 4 * max(0, fk - 1)
         parts = [b"".join(h1 + s1 + h2 + s2 for h1, s1, h2, s2 in self.proposer_slashings),
                  var_list([le32(8) + le32(8 + len(a.ssz())) + a.ssz() + b.ssz() for a, b in self.attester_slashings]),
                  var_list([a.ssz() for a in self.attestations]),
                  b"".join(self.deposits),
                  b"".join(le64(e) + le64(v) + s for e, v, s in self.exits)]
-        offs, o = b"", fixed
-        for p in parts:
-            offs += le32(o)
-            o += len(p)
-        tail = b"" if self.sync is None else self.sync[0] + self.sync[1]
-        return self.randao + self.eth1 + self.graffiti + offs + tail + b"".join(parts)
+        late = []
+        if fk >= 2:
+            late.append(self.payload.ssz())
+        if fk >= 3:
+            late.append(b"".join(le64(v) + pk + a + sg for v, pk, a, sg in self.bls_changes))
+        if fk >= 4:
+            late.append(b"".join(self.blobs))
+        offs, o = [], fixed
+        for q in parts + late:
+            offs.append(le32(o))
+            o += len(q)
+        tail = b"" if fk == 0 else self.sync[0] + self.sync[1]
+        return (self.randao + self.eth1 + self.graffiti + b"".join(offs[:5]) + tail + b"".join(offs[5:]) +
+                b"".join(parts) + b"".join(late))
 
     def root(self) -> bytes:
+        fk = seq(self._fork())
         ml = lambda xs, lim: S.mix_in_length(S.merkleize(xs, lim), len(xs))  # noqa: E731
         sh = lambda h, s: S.merkleize([header_root(h), S.bytes_vector_root(s)])  # noqa: E731
 
@@ -121,9 +202,20 @@ class Body:
                   ml([dep(d) for d in self.deposits], 16),
                   ml([S.merkleize([S.merkleize([S.u64(ep), S.u64(v)]), S.bytes_vector_root(s)])
                       for ep, v, s in self.exits], 16)]
-        if self.sync is not None:
+        if fk >= 1:
             fields.append(S.merkleize([S.merkleize(S.pack_bytes(self.sync[0])), S.bytes_vector_root(self.sync[1])]))
+        if fk >= 2:
+            fields.append(self.payload.root())
+        if fk >= 3:
+            fields.append(ml([S.merkleize([bls_change_root(v, pk, a), S.bytes_vector_root(sg)])
+                              for v, pk, a, sg in self.bls_changes], 16))
+        if fk >= 4:
+            fields.append(ml([S.bytes_vector_root(c) for c in self.blobs], 4096))
         return S.merkleize(fields)
+
+
+def bls_change_root(vi: int, pk48: bytes, addr: bytes) -> bytes:
+    return S.merkleize([S.u64(vi), S.bytes_vector_root(pk48), S.bytes_vector_root(addr)])
 
 
 def signed_block_ssz(slot, proposer, parent, state, body: Body, sig: bytes) -> bytes:
@@ -156,17 +248,27 @@ def json_block_to_ssz(b: dict) -> bytes:
 
 # ---- synthetic signed blocks -------------------------------------------------------------
 class Chain:
-    """Fork schedule + domains restated from the spec (compute_domain), independent of the product."""
+    """Fork schedule + domains restated from the spec (compute_domain), independent of the product.
+    forks: [(epoch, version)] in fork order phase0, altair, bellatrix, capella, deneb."""
 
     def __init__(self, gvr: bytes, forks: List[Tuple[int, bytes]]):
         self.gvr, self.forks = gvr, forks
 
+    def _index(self, slot: int) -> int:
+        return len([1 for ep, _ in self.forks if slot // 32 >= ep]) - 1
+
     def domain(self, dt: bytes, slot: int) -> bytes:
-        v = [ver for ep, ver in self.forks if slot // 32 >= ep][-1]
-        return S.compute_domain(dt, v, self.gvr)
+        """The message's own fork (every synthetic message sits in its block's fork)."""
+        return S.compute_domain(dt, self.forks[self._index(slot)][1], self.gvr)
+
+    def domain_at(self, dt: bytes, fork: str) -> bytes:
+        return S.compute_domain(dt, self.forks[seq(fork)][1], self.gvr)
+
+    def fork(self, slot: int) -> str:
+        return FORK_NAMES[self._index(slot)]
 
     def altair(self, slot: int) -> bool:
-        return len([1 for ep, _ in self.forks if slot // 32 >= ep]) >= 2
+        return self._index(slot) >= 1
 
 
 def committee_of(n_validators: int, size: int = 24) -> Callable[[int, int], List[int]]:
@@ -182,9 +284,12 @@ def sync_committee_of(n_validators: int) -> Callable[[int], List[int]]:
 
 
 def make_block(sign, sks: List[int], chain: Chain, slot: int, proposer: int, parent: bytes, committee, sync_committee,
-               n_atts=3, n_exits=1, n_prop_sl=1, n_att_sl=1, n_deposits=1, sync_participants=100, seed=0):
+               n_atts=3, n_exits=1, n_prop_sl=1, n_att_sl=1, n_deposits=1, sync_participants=100, seed=0,
+               pk48=None, n_changes=2, n_txs=3, n_withdrawals=2, n_blobs=2):
     """sign(list of int sks, list of 32-byte roots) -> signatures.  Returns (ssz, expected sets as
-    (validator indices, signing root), block root).  Every signature is valid."""
+    (validator indices, signing root), block root, body).  Every signature is valid.  A BLS-to-execution
+    change set (capella+, needs pk48(sk) -> 48-byte compressed pubkey) is expected as
+    (("pk48", key), root)."""
     rng = hashlib.sha256(b"blk" + le64(slot) + le64(seed)).digest()
     todo: List[Tuple[List[int], bytes]] = []   # expected sets in the reference's order
     dom = chain.domain
@@ -225,9 +330,13 @@ def make_block(sign, sks: List[int], chain: Chain, slot: int, proposer: int, par
         atts.append((bytes(raw), data, ix, r))
         todo.append((ix, r))
     exits = []
+    fork = chain.fork(slot)
     for k in range(n_exits):
         v = (proposer + 11 + k) % len(sks)
-        r = S.compute_signing_root(S.merkleize([S.u64(epoch), S.u64(v)]), dom(bytes([4, 0, 0, 0]), epoch * 32))
+        # EIP-7044: from deneb on, exits are signed with the capella fork version
+        exit_dom = chain.domain_at(bytes([4, 0, 0, 0]), "capella") if fork == "deneb" else \
+            dom(bytes([4, 0, 0, 0]), epoch * 32)
+        r = S.compute_signing_root(S.merkleize([S.u64(epoch), S.u64(v)]), exit_dom)
         exits.append((epoch, v, r))
         todo.append(([v], r))
     n_block_sets = len(todo)
@@ -244,7 +353,31 @@ def make_block(sign, sks: List[int], chain: Chain, slot: int, proposer: int, par
     ex_enc = [(ep, v, next(it)) for ep, v, _ in exits]
     deposits = [hashlib.sha256(rng + b"dep" + bytes([k])).digest() * 38 + bytes(24) for k in range(n_deposits)]
     body = Body(randao, hashlib.sha256(rng).digest() + le64(7) + bytes(32), b"graffiti".ljust(32, b"\0"),
-                ps_enc, as_enc, at_enc, deposits, ex_enc)
+                ps_enc, as_enc, at_enc, deposits, ex_enc, fork=fork)
+    if seq(fork) >= seq("bellatrix"):
+        hx = lambda t: hashlib.sha256(rng + t).digest()  # noqa: E731
+        body.payload = Payload(fork, hx(b"ph"), hx(b"fr")[:20], hx(b"sr"), hx(b"rr"), hx(b"lb") * 8, hx(b"pr"),
+                               1000 + slot, 30_000_000, 12_345_678, 1_700_000_000 + 12 * slot, b"lodestar-amd",
+                               7 * 10 ** 9, hx(b"bh"),
+                               [hx(b"tx" + bytes([k])) * (k + 1) + bytes([k]) for k in range(n_txs)],
+                               [(slot * 16 + k, (proposer + k) % len(sks), hx(b"wa" + bytes([k]))[:20], 32 * 10 ** 9 + k)
+                                for k in range(n_withdrawals)] if seq(fork) >= seq("capella") else [],
+                               131072 if fork == "deneb" else 0, 262144 if fork == "deneb" else 0)
+    change_sets = []
+    if seq(fork) >= seq("capella") and pk48 is not None:
+        csks = [(int.from_bytes(hashlib.sha256(rng + b"wsk" + bytes([k])).digest(), "big") % (R_ORDER - 1)) + 1
+                for k in range(n_changes)]
+        msgs = []
+        for k, csk in enumerate(csks):
+            vi, pk, addr = (proposer + 21 + k) % len(sks), pk48(csk), hashlib.sha256(rng + b"ea" + bytes([k])).digest()[:20]
+            r = S.compute_signing_root(bls_change_root(vi, pk, addr), chain.domain_at(bytes([10, 0, 0, 0]), "phase0"))
+            msgs.append((vi, pk, addr, r))
+        csigs = sign(csks, [m[3] for m in msgs])
+        body.bls_changes = [(vi, pk, addr, sg) for (vi, pk, addr, _), sg in zip(msgs, csigs)]
+        change_sets = [(("pk48", pk), r) for _, pk, _, r in msgs]
+    if fork == "deneb":
+        body.blobs = [bytes([0xC0 | k]) + hashlib.sha256(rng + b"kzg" + bytes([k])).digest() + bytes(15)
+                      for k in range(n_blobs)]
     sync_set = None
     if chain.altair(slot):
         members = sync_committee(slot)
@@ -264,12 +397,25 @@ def make_block(sign, sks: List[int], chain: Chain, slot: int, proposer: int, par
     broot = block_root(slot, proposer, parent, state, body)
     prop_root = S.compute_signing_root(broot, dom(bytes(4), slot))
     bsig = sign([sks[proposer]], [prop_root])[0]
-    expected = todo[:n_block_sets] + [([proposer], prop_root)] + ([sync_set] if sync_set else [])
+    expected = todo[:n_block_sets] + [([proposer], prop_root)] + ([sync_set] if sync_set else []) + change_sets
     return signed_block_ssz(slot, proposer, parent, state, body, bsig), expected, broot, body
 
 
 class OracleRoots:
     """The roots backend computed on the CPU with oracle/ssz.py (CPU tests)."""
+
+    def pubkeys_from_bytes(self, keys48):
+        from oracle import bls12_381 as O
+        out, st = [], []
+        for k in keys48:
+            try:
+                p = O.g1_from_bytes(k)
+                ok = p is not None and O.g1_in_subgroup(p)
+            except ValueError:
+                ok = False
+            out.append(O.g1_to_bytes(p, compressed=False) if ok else bytes([0x40]) + bytes(95))
+            st.append(0 if ok else 3)
+        return out, st
 
     def signing_roots_attestation(self, data, domains):
         doms = [domains] * len(data) if isinstance(domains, (bytes, bytearray)) else domains

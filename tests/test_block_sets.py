@@ -10,6 +10,7 @@ import struct
 import pytest
 
 import blocks_helper as BH
+import ssz_schema as SC
 from lodestar_amd import block_sets as B
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -114,6 +115,8 @@ def test_malformed_blocks_raise():
         builder.build([good])
     with pytest.raises(B.SszError):
         B.parse_signed_block(good, "bellatrix")
+    with pytest.raises(B.SszError):
+        B.parse_signed_block(good, "electra")
 
 
 def test_domains_follow_fork_schedule():
@@ -122,3 +125,148 @@ def test_domains_follow_fork_schedule():
     assert CONFIG.domain(B.DOMAIN_RANDAO, 64) == S.compute_domain(bytes([2, 0, 0, 0]), bytes([1, 0, 0, 0]),
                                                                   bytes(range(32)))
     assert B.MAINNET.domain(B.DOMAIN_BEACON_ATTESTER, 0).hex() == SSZ_GOLD["domain_attester"]
+
+
+# ---- bellatrix / capella / deneb ------------------------------------
+GVR5 = bytes(range(32, 64))
+VERS5 = [bytes([k, 0, 0, 9]) for k in range(5)]
+EPOCHS5 = [0, 2, 3, 4, 5]                                                   # fork k from epoch EPOCHS5[k]
+CHAIN5 = BH.Chain(GVR5, [(EPOCHS5[k], VERS5[k]) for k in range(5)])
+CONFIG5 = B.ChainConfig(GVR5, [(EPOCHS5[k], VERS5[k], B.FORKS[k]) for k in range(5)])
+BELLATRIX_SSZ = open(os.path.join(GOLD, "goerli_shadow_fork_block_13249.ssz"), "rb").read()
+
+
+def _pk48(sk):
+    from oracle import bls12_381 as O
+    return O.g1_to_bytes(O.sk_to_pk(sk), compressed=True)
+
+
+def _pk96(pk48):
+    from oracle import bls12_381 as O
+    return O.g1_to_bytes(O.g1_from_bytes(pk48), compressed=False)
+
+
+@pytest.mark.parametrize("fork_k", range(5))
+def test_synthetic_block_every_fork(fork_k):
+    """A block of each fork with every operation kind (execution payload with
+    transactions and withdrawals, BLS-to-execution changes, blob commitments): the
+    product parser's body / block roots equal the builder's restatement and the generic
+    schema decoder's, and the set list equals the expected one."""
+    slot = 32 * EPOCHS5[fork_k] + 9 if fork_k else 40
+    sks = list(range(1, 65))
+    committee, sync = BH.committee_of(64), BH.sync_committee_of(64)
+    ssz, expected, root, body = BH.make_block(_sign_stub, sks, CHAIN5, slot, 9, bytes([5]) * 32, committee, sync,
+                                              n_atts=3, n_exits=2, n_prop_sl=1, n_att_sl=1, n_deposits=1,
+                                              pk48=_pk48)
+    fork = B.FORKS[fork_k]
+    blk = B.parse_signed_block(ssz, fork)
+    assert blk.body_root == body.root() and blk.root() == root
+    typ = SC.signed_block_type(fork)
+    dec = typ.decode(ssz)
+    assert typ.encode(dec) == ssz
+    assert SC.BODY[fork].root(dec["message"]["body"]) == blk.body_root
+    assert len(blk.bls_to_execution_changes) == (2 if fork_k >= 3 else 0)
+    assert len(blk.blob_kzg_commitments) == (2 if fork_k >= 4 else 0)
+    (sets,) = B.BlockSignatureSetBuilder(BH.OracleRoots(), CONFIG5, committee, sync).build([ssz])
+    assert len(sets) == len(expected)
+    for st, (ix, r) in zip(sets, expected):
+        if isinstance(ix, tuple):  # BLS change: its own key, decompressed + validated
+            assert st.pubkey.index is None and st.pubkey.uncompressed == _pk96(ix[1])
+        else:
+            got = [st.pubkey.index] if st.pubkey is not None else [k.index for k in st.pubkeys]
+            assert got == ix
+        assert st.signing_root == r
+
+
+def test_bellatrix_reference_block_parses_and_rehashes():
+    """The reference's real bellatrix block (goerli shadow fork, slot 13249): the product
+    parser and the generic schema decoder agree on every root; re-encoding is byte-exact."""
+    blk = B.parse_signed_block(BELLATRIX_SSZ, "bellatrix")
+    assert (blk.slot, blk.proposer_index) == (13249, 18462)
+    typ = SC.signed_block_type("bellatrix")
+    dec = typ.decode(BELLATRIX_SSZ)
+    assert typ.encode(dec) == BELLATRIX_SSZ
+    body = dec["message"]["body"]
+    assert SC.PAYLOAD["bellatrix"].root(body["execution_payload"]) == blk.execution_payload_root
+    assert SC.BODY["bellatrix"].root(body) == blk.body_root
+    assert len(blk.attestations) == len(body["attestations"]) > 0
+    assert len(body["execution_payload"]["transactions"]) > 0
+    # the block root three ways
+    msg = dec["message"]
+    hdr = {"slot": msg["slot"], "proposer_index": msg["proposer_index"], "parent_root": msg["parent_root"],
+           "state_root": msg["state_root"], "body_root": SC.BODY["bellatrix"].root(body)}
+    assert SC.BeaconBlockHeader.root(hdr) == blk.root()
+    # a body byte flipped inside the payload changes the product's root
+    t = bytearray(BELLATRIX_SSZ)
+    t[100 + 84 + 3870 + 40] ^= 1  # fee_recipient (the payload starts at body offset 3870)
+    assert B.parse_signed_block(bytes(t), "bellatrix").body_root != blk.body_root
+
+
+def test_mainnet_blocks_match_schema_decoder():
+    typ = SC.signed_block_type("phase0")
+    for b in BLOCKS:
+        ssz = bytes.fromhex(b["ssz"])
+        dec = typ.decode(ssz)
+        assert typ.encode(dec) == ssz
+        assert SC.BODY["phase0"].root(dec["message"]["body"]) == B.parse_signed_block(ssz, "phase0").body_root
+
+
+def test_deneb_exit_domain_is_capella():
+    """getDomainForVoluntaryExit: from deneb on the exit domain is capella's (EIP-7044)."""
+    from oracle import ssz as S
+    d = CONFIG5.domain_voluntary_exit(32 * 5 + 3, 0)
+    assert d == S.compute_domain(bytes([4, 0, 0, 0]), VERS5[3], GVR5)
+    assert CONFIG5.domain_voluntary_exit(32 * 4 + 3, 32 * 4) == S.compute_domain(bytes([4, 0, 0, 0]), VERS5[3], GVR5)
+    assert CONFIG5.domain_voluntary_exit(32 * 3 + 3, 0) == S.compute_domain(bytes([4, 0, 0, 0]), VERS5[1], GVR5)
+
+
+def test_domain_uses_state_fork_or_previous():
+    """config.getDomain(stateSlot, type, messageSlot) (genesisConfig/index.ts:28-53): a
+    message from a later fork inside a phase0 block signs with phase0's version."""
+    from oracle import ssz as S
+    mainnet_altair = 74240 * 32
+    # a phase0 state slot, message slot in altair: still phase0
+    assert B.MAINNET.domain(B.DOMAIN_BEACON_PROPOSER, mainnet_altair - 5, mainnet_altair + 100) == \
+        S.compute_domain(bytes(4), bytes(4), B.MAINNET.genesis_validators_root)
+    # an altair state slot, message from phase0: previous fork
+    assert B.MAINNET.domain(B.DOMAIN_BEACON_PROPOSER, mainnet_altair + 5, mainnet_altair - 40) == \
+        S.compute_domain(bytes(4), bytes(4), B.MAINNET.genesis_validators_root)
+    # capella state, message from altair: only current (capella) or previous (bellatrix)
+    cap = 194048 * 32
+    assert B.MAINNET.domain(B.DOMAIN_RANDAO, cap + 1, 74240 * 32 + 1) == \
+        S.compute_domain(bytes([2, 0, 0, 0]), bytes([2, 0, 0, 0]), B.MAINNET.genesis_validators_root)
+    assert B.MAINNET.domain_at_fork("phase0", B.DOMAIN_BLS_TO_EXECUTION_CHANGE) == \
+        S.compute_domain(bytes([10, 0, 0, 0]), bytes(4), B.MAINNET.genesis_validators_root)
+
+
+def test_phase0_block_with_future_proposer_slashing_uses_phase0_domain():
+    """A proposer slashing whose headers carry a slot of the next fork, inside a block of
+    the earlier fork: the set's domain is the block's fork."""
+    from oracle import ssz as S
+    sks = list(range(1, 65))
+    committee, sync = BH.committee_of(64), BH.sync_committee_of(64)
+    ssz, _, _, body = BH.make_block(_sign_stub, sks, CHAIN, 40, 4, bytes(32), committee, sync, n_atts=0, n_exits=0,
+                                    n_prop_sl=1, n_att_sl=0, n_deposits=0)
+    # rewrite the slashing headers' slot to 70 (altair under CONFIG), re-encode the block
+    h1, s1, h2, s2 = body.proposer_slashings[0]
+    body.proposer_slashings = [(BH.le64(70) + h1[8:], s1, BH.le64(70) + h2[8:], s2)]
+    m = BH.signed_block_ssz(40, 4, bytes(32), ssz[100 + 48:100 + 80], body, bytes(96))
+    (sets,) = B.BlockSignatureSetBuilder(BH.OracleRoots(), CONFIG, committee, sync).build([m])
+    dom = S.compute_domain(bytes(4), bytes(4), bytes(range(32)))
+    assert sets[1].signing_root == S.compute_signing_root(BH.header_root(BH.le64(70) + h1[8:]), dom)
+
+
+def test_empty_sync_aggregate_requires_infinity_signature():
+    """processSyncCommittee.ts:94-101: no participants and a non-infinity signature throws."""
+    sks = list(range(1, 65))
+    committee, sync = BH.committee_of(64), BH.sync_committee_of(64)
+    ssz, _, _, _ = BH.make_block(_sign_stub, sks, CHAIN, 80, 4, bytes(32), committee, sync, n_atts=1,
+                                 n_exits=0, n_prop_sl=0, n_att_sl=0, n_deposits=0, sync_participants=0)
+    builder = B.BlockSignatureSetBuilder(BH.OracleRoots(), CONFIG, committee, sync)
+    assert len(builder.build([ssz])[0]) == 3
+    # the same block with a non-infinity sync signature (the last 96 bytes of the sync aggregate)
+    body0 = 100 + 84
+    t = bytearray(ssz)
+    t[body0 + 284] = 0xA0
+    with pytest.raises(ValueError, match="not infinity"):
+        builder.build([bytes(t)])

@@ -45,6 +45,7 @@ class TwoPhaseBackend(TableBackend):
 
     def gt_check(self, partials):
         import concurrent.futures
+        self.gt_checks = getattr(self, "gt_checks", 0) + 1
         f = concurrent.futures.Future()
         f.set_result(all(p[0] == 1 for p in partials))
         return f
@@ -112,16 +113,56 @@ def test_sharded_verifier_combines_partials(bad):
     assert all(b.finished == [not bad] for b in backs)
 
 
-def _worker(rank, world, port, reqs, out_q, two_phase=False):
+class FailingBackend(TwoPhaseBackend):
+    """Phase 1 raises (a device error on this GPU)."""
+
+    def submit_requests(self, requests, partial=False, priority=False):
+        import concurrent.futures
+        f = concurrent.futures.Future()
+        f.set_exception(RuntimeError("device lost"))
+        return f
+
+
+def test_sharded_verifier_resumes_the_other_shards_when_one_fails():
+    """a failing shard must not leave the others' partials pending."""
+    reqs = make_requests(5)
+    backs = [TwoPhaseBackend(), FailingBackend(), TwoPhaseBackend()]
+    with pytest.raises(RuntimeError, match="device lost"):
+        ShardedVerifier(backs).verify_requests(reqs)
+    assert backs[0].finished == [False] and backs[2].finished == [False]
+
+
+def _worker(rank, world, port, reqs, out_q, two_phase=False, fail_rank=-1):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b = TwoPhaseBackend() if two_phase else TableBackend()
-    v, e = verify_distributed(reqs, b.verify_requests, rank, world, backend=b if two_phase else None)
-    out_q.put((rank, v, e, b.seen))
+    b = (FailingBackend() if rank == fail_rank else TwoPhaseBackend()) if two_phase else TableBackend()
+    try:
+        v, e = verify_distributed(reqs, b.verify_requests, rank, world, backend=b if two_phase else None)
+        out_q.put((rank, v, e, b.seen, getattr(b, "gt_checks", None)))
+    except Exception as ex:  # noqa: BLE001
+        out_q.put((rank, "error", str(ex), None, None))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_verify_distributed_fails_on_every_rank_together():
+    """A rank whose shard raises joins the collectives with an error flag: every rank
+    raises instead of the others blocking in all_gather."""
+    reqs = make_requests(6)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + random.Random(os.getpid()).randrange(2000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, reqs, q, True, 1)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == ["error", "error"]
+    assert "device lost" in res[1][2] and "rank(s) [1]" in res[0][2]
 
 
 @pytest.mark.parametrize("two_phase", [False, True])
@@ -140,7 +181,9 @@ def test_verify_distributed_gloo_world2(two_phase):
         p.join(timeout=60)
         assert p.exitcode == 0
     shards = shard_requests([len(r) for r in reqs], 2)
-    for rank, v, e, seen in res:
+    for rank, v, e, seen, checks in res:
         assert (v, e) == want
+        if two_phase:  # the combined check runs once, on rank 0
+            assert checks == (1 if rank == 0 else None)
         lo, hi = shards[rank]
         assert len(seen[0]) == hi - lo  # each rank verified only its own shard

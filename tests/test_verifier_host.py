@@ -261,11 +261,16 @@ def test_device_backend_ships_indices_when_every_key_has_one():
     assert b.verify_requests([[s1, s2]]) == ([True], [0])
     pks, idx, pk_off = b.dev.calls[-1]
     assert pks is None and idx == [4, 1, 2] and pk_off == [0, 1, 3]
-    # mixed: index-only keys are materialised from the table, bytes shipped
+    # mixed (a capella block's BLS-change key beside validator keys): indices for the table
+    # keys, flagged row indices (LB_PK_ROW_FLAG) for the keys shipped as bytes
     s3 = single_set(PublicKey(bytes([7]) * 96), bytes(32), bytes(96))
-    b.verify_requests([[s1, s3]])
+    b.verify_requests([[s1, s3, s2]])
     pks, idx, _ = b.dev.calls[-1]
-    assert idx is None and pks.tobytes() == bytes([4]) * 96 + bytes([7]) * 96
+    assert idx == [4, 0x80000000, 1, 2] and pks.tobytes() == bytes([7]) * 96
+    # no index at all: the encodings
+    b.verify_requests([[s3]])
+    pks, idx, _ = b.dev.calls[-1]
+    assert idx is None and pks.tobytes() == bytes([7]) * 96
     b.close()
 
 
@@ -353,3 +358,52 @@ def test_pool_metrics_reference_names():
         assert 'lodestar_bls_thread_pool_jobs_started_total{type="default"}' in names
         await v.close()
     run(main())
+
+
+class SlotDev(FakeDev):
+    """FakeDev with the library's slot accounting: a two-phase call holds its slot from
+    submission until verify_finish; more than `slots` calls holding slots at once would
+    make the library reuse (and silently resume) a pending partial."""
+
+    def __init__(self, slots=2, slow=0.02):
+        super().__init__(slow=slow)
+        self.slots, self.pending, self.max_used = slots, 0, 0
+
+    def verify_requests_async(self, *a, partial=False, **k):
+        assert self.active + self.pending < self.slots, "a slot holding a pending partial was reused"
+        pc = super().verify_requests_async(*a, partial=partial, **k)
+        if partial:
+            self.active -= 1
+            self.pending += 1
+        self.max_used = max(self.max_used, self.active + self.pending)
+        return pc
+
+    def partial_wait(self, pc):
+        return bytes(576)
+
+    def verify_finish(self, pc, ok):
+        self.pending -= 1
+        self.active += 1
+
+    def verify_same_message_batch(self, jobs, seed, by_index=False):
+        return [[True] * len(s) for _, s, _ in jobs], [True] * len(jobs), (0, sum(len(s) for _, s, _ in jobs))
+
+
+def test_partial_call_holds_its_slot_until_finished():
+    """pending two-phase calls count against the backend's capacity, so
+    neither a later package nor an interleaved same-message call resumes them early."""
+    from lodestar_amd.verifier import DeviceBackend, PublicKey, single_set
+
+    dev = SlotDev(slots=2)
+    b = DeviceBackend(seed_source=lambda: bytes(32), dev=dev, capacity=2)
+    req = [[single_set(PublicKey(index=1), bytes(32), bytes(96))]]
+    pc = b.submit_requests(req, partial=True).result()
+    later = [b.submit_requests(req) for _ in range(3)]
+    sm = b.submit_same_message([([PublicKey(index=2)], [bytes(96)], bytes(32))])
+    assert sm.result()[0] == [[True]]
+    for f in later:
+        assert f.result()[0] == [True]
+    assert dev.pending == 1  # still waiting for its host verdict
+    assert b.finish(pc, True).result()[0] == [True]
+    assert dev.max_used <= 2 and dev.pending == 0
+    b.close()
