@@ -330,6 +330,11 @@ int lb_batch_scalars(lb_ctx* ctx, const uint8_t* seed, uint32_t first, uint32_t 
 /* [k_i] P_i on G1 and G2 (uncompressed in/out) */
 int lb_g1_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g1_96, const uint64_t* k, uint8_t* out96);
 int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* k, uint8_t* out192);
+/* sum_i (a_i + b_i lambda) P_i, a_i / b_i = low / high 32 bits of raw[i], lambda = -x^2: the
+ * merged check's bucket MSM alone (uncompressed in/out; an undecodable point gives infinity).
+ * Replaces nothing in the reference: the sum blst's mul_n_aggregate accumulates inside
+ * verifyMultipleSignatures (BN/chain/bls/maybeBatch.ts:19-26), exposed for tests. */
+int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* raw, uint8_t* out192);
 
 /* ---- synthetic data generation (bench / tests) ---------------------------- */
 /* SecretKey.fromBytes(sk).toPublicKey().toBytes(uncompressed) and

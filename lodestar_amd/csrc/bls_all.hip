@@ -10,4 +10,5 @@
 #include "k_aux.hip"
 #include "k_tail.hip"
 #include "k_ssz.hip"
+#include "k_msm.hip"
 #include "bls_host.hip"

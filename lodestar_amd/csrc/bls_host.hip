@@ -12,8 +12,11 @@
 //   k_decode_sigs     per set     : Signature.fromBytes(validate=true)
 //   k_pubkeys_*       per set     : PublicKey.fromBytes + PublicKey.aggregate
 //   k_hash_half/finish per message: hash_to_G2(signing root), two lanes per message
-//   k_scalar_pk/sig   per set     : r_i pk_i, r_i sig_i (GLV, 2 x 32-bit)
-//   k_sum_tree        per request : S_k = sum r_i sig_i
+//   k_scalar_pk       per set     : r_i pk_i (GLV, 2 x 32-bit)
+//   k_msm_*           per call    : S_all = sum r_i sig_i over the good requests, one
+//                                   bucket MSM (k_msm.hip) for the merged check; or
+//   k_scalar_sig + k_sum_tree     : r_i sig_i, S_k per request (small calls, and the
+//                                   per-request tails after a failed merged check)
 //   k_lines + k_miller_acc        : Miller(r_i pk_i, H_i) from stored lines, several
 //     (or k_miller_sets + k_prod_tree) pairs per lane, product per request
 //   k_lines_S + k_tail per request: Miller(-g1, S_k), final exponentiation, == 1,
@@ -50,6 +53,13 @@ static unsigned long long opcount_read_reset() {
 struct PipeState {
   uint32_t n_req = 0, n_sets = 0, n_pairs = 0;
   bool merged = false, tail_wave = true;
+  // merged check's S_all from the bucket MSM: the per-request S_k (per-set
+  // ladders + sums) are computed only when the tails run
+  bool msm = false;
+  const uint8_t* d_seed = nullptr;
+  const g2j* d_sig = nullptr;
+  const uint8_t* d_sig_st = nullptr;
+  g2j* d_rsig = nullptr;
   const uint32_t* d_req_off = nullptr;
   uint32_t* d_lines = nullptr;
   g2a* d_S = nullptr;
@@ -69,7 +79,7 @@ struct Slot {
   size_t ws_cap = 0;
   char* h_pin = nullptr;
   size_t pin_cap = 0;
-  static constexpr int kMaxStages = 24;
+  static constexpr int kMaxStages = 32;
   hipEvent_t ev0[kMaxStages] = {}, ev1[kMaxStages] = {};
   const char* stage_name[kMaxStages] = {};
   int n_stages = 0;
@@ -132,6 +142,9 @@ struct lb_ctx {
   // merged check of the whole call first (one tail), per-request tails only
   // when it fails; used from merge_min_req requests up (LB_MERGE_MIN, 0 = off)
   uint32_t merge_min_req = 8;
+  // merged calls of at least msm_min_sets sets take S_all from the bucket MSM
+  // (k_msm.hip) instead of per-set ladders (LB_MSM_MIN, 0 = never)
+  uint32_t msm_min_sets = 4096;
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -280,6 +293,12 @@ int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
 int run_tails(lb_ctx* ctx, Slot& sl) {
   const PipeState& p = sl.ps;
   if (p.merged) {
+    if (p.msm) {  // the S_k of the per-request tails (skipped when the merged check passed)
+      LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(p.n_sets), TPB, p.n_sets, p.d_seed, p.d_sig, p.d_sig_st,
+               p.d_rsig, (const uint8_t*)p.d_mflag);
+      LB_STAGE("sum_tree", 0, k_sum_tree, p.n_req, TPB, p.n_req, p.d_req_off, (const g2j*)p.d_rsig, p.d_S,
+               (const uint8_t*)p.d_mflag);
+    }
     LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
              p.d_lines, (const uint8_t*)p.d_mflag);
     LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
@@ -319,6 +338,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
   const bool merged = partial || (tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req);
   const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
+  const bool use_msm = merged && n_sets && ctx->msm_min_sets && n_sets >= ctx->msm_min_sets;
   uint32_t* d_lines =
       (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
@@ -332,6 +352,16 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   fp12* d_Fall = ws.take<fp12>(1);
   uint8_t* d_mflag = ws.take<uint8_t>(2);  // [0] merged check passed, [1] constant 0 (req_bad of the merged pair)
   uint32_t* d_mstats = ws.take<uint32_t>(2);
+  // bucket MSM workspace: keys + sorted entries (2 half-points x W windows per
+  // set), histogram / cursors / offsets, chunk partials, bucket sums, G_p
+  const size_t n_ent = use_msm ? 2 * (size_t)n_sets * LB_MSM_W : 0;
+  const size_t max_chunks = use_msm ? n_ent / LB_MSM_T + LB_MSM_BUCKETS : 0;
+  uint32_t* d_mkeys = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
+  uint32_t* d_msorted = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
+  uint32_t* d_mhist = use_msm ? ws.take<uint32_t>(4 * (LB_MSM_BUCKETS + 1)) : nullptr;
+  g2j* d_mcsum = use_msm ? ws.take<g2j>(max_chunks) : nullptr;
+  g2j* d_mbsum = use_msm ? ws.take<g2j>(LB_MSM_BUCKETS) : nullptr;
+  g2j* d_mG = use_msm ? ws.take<g2j>(LB_MSM_POS) : nullptr;
   sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
@@ -371,10 +401,32 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   if (n_sets) {
     LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
              (const uint8_t*)d_single, d_sig, d_sig_st);
-    LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
-             (const uint8_t*)d_sig_st, d_rsig);
+    if (!use_msm)
+      LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
+               (const uint8_t*)d_sig_st, d_rsig, (const uint8_t*)nullptr);
   }
-  LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S);
+  if (use_msm) {
+    // S_all = sum r_i sig_i over the good requests' sets: one bucket MSM (k_msm.hip)
+    uint32_t* d_off = d_mhist + (LB_MSM_BUCKETS + 1);
+    uint32_t* d_coff = d_off + (LB_MSM_BUCKETS + 1);
+    uint32_t* d_cur = d_coff + (LB_MSM_BUCKETS + 1);
+    LB_HIP(hipMemsetAsync(d_mhist, 0, (LB_MSM_BUCKETS + 1) * sizeof(uint32_t), sl.st[0]));
+    LB_STAGE("msm_digits", 0, k_msm_scalars, n_req, TPB, n_req, d_req_off, d_seed, (const uint64_t*)nullptr,
+             (const g2j*)d_sig, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_mkeys, d_mhist);
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, sl.st[0], (const uint32_t*)d_mhist, d_off, d_coff, d_cur);
+    LB_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_msm_scatter, dim3(blocks_for((uint32_t)n_ent, 256)), dim3(256), 0, sl.st[0], (uint32_t)n_ent,
+                       (const uint32_t*)d_mkeys, (const uint32_t*)d_off, d_cur, d_msorted);
+    LB_HIP(hipGetLastError());
+    LB_STAGE("msm_chunks", 0, k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks,
+             (const uint32_t*)d_off, (const uint32_t*)d_coff, (const uint32_t*)d_msorted, (const g2j*)d_sig, d_mcsum);
+    LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS), TPB, (const uint32_t*)d_coff,
+             (const g2j*)d_mcsum, d_mbsum);
+    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_mbsum, d_mG);
+    LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
+  } else {
+    LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S, (const uint8_t*)nullptr);
+  }
   if (tail_wave && !merged)
     LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines,
              (const uint8_t*)nullptr);
@@ -435,6 +487,11 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   ps.n_pairs = n_pairs;
   ps.merged = merged;
   ps.tail_wave = tail_wave;
+  ps.msm = use_msm;
+  ps.d_seed = d_seed;
+  ps.d_sig = d_sig;
+  ps.d_sig_st = d_sig_st;
+  ps.d_rsig = d_rsig;
   ps.d_req_off = d_req_off;
   ps.d_lines = d_lines;
   ps.d_S = d_S;
@@ -454,7 +511,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_HIP(hipStreamWaitEvent(ts, sl.dep[3], 0));
     }
     LB_HIP(hipMemsetAsync(d_mflag, 0, 2, ts));
-    LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, (const g2a*)d_S, (const fp12*)d_F, (const uint8_t*)d_bad,
+    LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, use_msm ? (const g2a*)nullptr : (const g2a*)d_S,
+                (const fp12*)d_F, (const uint8_t*)d_bad,
                 d_Sall, d_Fall);
     LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
                 (const uint8_t*)nullptr);
@@ -484,11 +542,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
 
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
+  // (+ the bucket MSM: 2 W keys + 2 W sorted entries and 2 W / T chunk partials per set)
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
-                   (size_t)LB_MILLER_LINES * 72 * 4;
+                   (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 + (2 * LB_MSM_W * sizeof(g2j)) / LB_MSM_T + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
   size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
-  return ns * per_set + (size_t)(n_req + 1) * per_req + 64 * 256 + 4096;
+  const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
+                           8 * 256;
+  return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * 256 + 4096;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -647,6 +708,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
     ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : strcmp(e, "wave") == 0 ? 3 : 0;
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
@@ -1626,6 +1688,66 @@ int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* k, 
   uint8_t* d_out = ws.take<uint8_t>((size_t)n * 192);
   LB_LAUNCH(k_g2_mul, blocks_for(n), TPB, n, (const uint8_t*)d_in, (const uint64_t*)d_k, d_out);
   LB_HIP(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  return LB_OK;
+}
+
+// sum_i (a_i + b_i lambda) P_i through the merged check's bucket MSM (k_msm.hip),
+// a_i / b_i = the low / high 32 bits of raw[i]: the MSM alone, for tests.
+int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw, uint8_t* out192) {
+  if (!ctx || !out192 || (n && (!in192 || !raw))) return LB_ERR_INVALID_ARGUMENT;
+  if (n > (1u << 28)) {
+    ctx->err = "lb_g2_msm: too many points";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  const uint32_t ns = n ? n : 1;
+  const size_t n_ent = 2 * (size_t)ns * LB_MSM_W, max_chunks = n_ent / LB_MSM_T + LB_MSM_BUCKETS;
+  LB_TRY(ensure_ws(ctx, (size_t)ns * (192 + 8 + sizeof(g2j) + 1) + 2 * n_ent * 4 + max_chunks * sizeof(g2j) +
+                            (LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 + 64 * 256));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  void *d_in = nullptr, *d_raw = nullptr;
+  if (n) {
+    LB_TRY(upload(ctx, ws, in192, (size_t)n * 192, &d_in));
+    LB_TRY(upload(ctx, ws, raw, (size_t)n * 8, &d_raw));
+  }
+  g2j* d_pts = ws.take<g2j>(ns);
+  uint8_t* d_st = ws.take<uint8_t>(ns);
+  uint32_t* d_req = ws.take<uint32_t>(2);
+  uint32_t* d_keys = ws.take<uint32_t>(n_ent);
+  uint32_t* d_sorted = ws.take<uint32_t>(n_ent);
+  uint32_t* d_hist = ws.take<uint32_t>(4 * (LB_MSM_BUCKETS + 1));
+  g2j* d_csum = ws.take<g2j>(max_chunks);
+  g2j* d_bsum = ws.take<g2j>(LB_MSM_BUCKETS);
+  g2j* d_G = ws.take<g2j>(LB_MSM_POS);
+  g2a* d_S = ws.take<g2a>(1);
+  uint8_t* d_out = ws.take<uint8_t>(192);
+  if (ws.off > ws.cap) {
+    ctx->err = "workspace overflow";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  uint32_t* d_off = d_hist + (LB_MSM_BUCKETS + 1);
+  uint32_t* d_coff = d_off + (LB_MSM_BUCKETS + 1);
+  uint32_t* d_cur = d_coff + (LB_MSM_BUCKETS + 1);
+  const uint32_t req[2] = {0, n};
+  LB_HIP(hipMemcpyAsync(d_req, req, sizeof(req), hipMemcpyHostToDevice, ctx->stream));
+  LB_HIP(hipMemsetAsync(d_hist, 0, (LB_MSM_BUCKETS + 1) * sizeof(uint32_t), ctx->stream));
+  if (n) {
+    LB_LAUNCH(k_msm_load, blocks_for(n), TPB, n, (const uint8_t*)d_in, d_pts, d_st);
+    LB_LAUNCH(k_msm_scalars, 1u, TPB, 1u, (const uint32_t*)d_req, (const uint8_t*)nullptr, (const uint64_t*)d_raw,
+              (const g2j*)d_pts, (const uint8_t*)d_st, (const uint8_t*)nullptr, d_keys, d_hist);
+  }
+  LB_LAUNCH(k_msm_scan, 1u, 1024u, (const uint32_t*)d_hist, d_off, d_coff, d_cur);
+  if (n) LB_LAUNCH(k_msm_scatter, blocks_for((uint32_t)n_ent, 256), 256u, (uint32_t)n_ent, (const uint32_t*)d_keys,
+                   (const uint32_t*)d_off, d_cur, d_sorted);
+  LB_LAUNCH(k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks, (const uint32_t*)d_off,
+            (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum);
+  LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS), TPB, (const uint32_t*)d_coff, (const g2j*)d_csum, d_bsum);
+  LB_LAUNCH(k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_bsum, d_G);
+  LB_LAUNCH(k_msm_final, 1u, TPB, (const g2j*)d_G, d_S);
+  LB_LAUNCH(k_g2a_serialize, 1u, TPB, 1u, (const g2a*)d_S, d_out);
+  LB_HIP(hipMemcpyAsync(out192, d_out, 192, hipMemcpyDeviceToHost, ctx->stream));
   LB_HIP(hipStreamSynchronize(ctx->stream));
   return LB_OK;
 }

@@ -51,6 +51,17 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #endif
 
 
+// Bucket MSM of the merged check (k_msm.hip): signed digits of LB_MSM_C bits in
+// LB_MSM_W windows of the 32-bit GLV half-scalars, LB_MSM_NB buckets per window,
+// chunks of <= LB_MSM_T entries, bit positions 0 .. LB_MSM_POS - 1.
+#define LB_MSM_C 11
+#define LB_MSM_W 3
+#define LB_MSM_NB 1024u
+#define LB_MSM_BUCKETS (LB_MSM_W * LB_MSM_NB)
+#define LB_MSM_T 16u
+#define LB_MSM_POS 33u
+#define LB_MSM_NONE 0xffffffffu
+
 namespace lb {
 // Where a set's pubkeys come from: the call's 96-byte uncompressed encodings
 // (the worker wire format, chain/bls/multithread/worker.ts:110-116) or the
@@ -102,12 +113,13 @@ __global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, cons
 __global__ void __launch_bounds__(TPB, LB_W_SSIG) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
-                                                    g2j* __restrict__ rsig);
+                                                    g2j* __restrict__ rsig, const uint8_t* __restrict__ skip);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, const uint8_t* __restrict__ seed,
                                                    const g1j* __restrict__ pk, const uint8_t* __restrict__ single_flag,
                                                    uint8_t* __restrict__ pk_status, g1j* __restrict__ rpk);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S);
+                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S,
+                                                  const uint8_t* __restrict__ skip);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_miller_S(uint32_t n_req, const g2a* __restrict__ S, fp12* __restrict__ fS);
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_miller_sets(uint32_t n, const g1j* __restrict__ rpk, const g2j* __restrict__ h,
                                                      fp12* __restrict__ f);
@@ -189,4 +201,24 @@ __global__ void __launch_bounds__(TPB) k_signing_root_att(uint32_t n, const uint
 __global__ void __launch_bounds__(TPB) k_signing_root_chunks(uint32_t n, uint32_t m, const uint8_t* __restrict__ chunks,
                                                              const uint8_t* __restrict__ domains, uint32_t dstride,
                                                              uint8_t* __restrict__ out);
+__global__ void __launch_bounds__(TPB) k_msm_scalars(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                     const uint8_t* __restrict__ seed, const uint64_t* __restrict__ raw,
+                                                     const g2j* __restrict__ sig, const uint8_t* __restrict__ sig_status,
+                                                     const uint8_t* __restrict__ pk_status, uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ hist);
+__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ off,
+                                                   uint32_t* __restrict__ coff, uint32_t* __restrict__ cursor);
+__global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n_ent, const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                     uint32_t* __restrict__ sorted);
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_chunks, const uint32_t* __restrict__ off,
+                                                                 const uint32_t* __restrict__ coff,
+                                                                 const uint32_t* __restrict__ sorted,
+                                                                 const g2j* __restrict__ sig, g2j* __restrict__ csum);
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t* __restrict__ coff,
+                                                                  const g2j* __restrict__ csum, g2j* __restrict__ bsum);
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G);
+__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_final(const g2j* __restrict__ G, g2a* __restrict__ S);
+__global__ void __launch_bounds__(TPB) k_msm_load(uint32_t n, const uint8_t* __restrict__ in192, g2j* __restrict__ out,
+                                                  uint8_t* __restrict__ status);
 }  // namespace lb

@@ -8,9 +8,9 @@ namespace lb {
 __global__ void __launch_bounds__(TPB, LB_W_SSIG) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
-                                                    g2j* __restrict__ rsig) {
+                                                    g2j* __restrict__ rsig, const uint8_t* __restrict__ skip) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (skip && *skip)) return;
   g2j rs;
   jac_set_inf(rs);
   if (sig_status[i] == LB_ST_OK) {
@@ -47,11 +47,14 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, cons
 }
 
 // S_k = sum_{i in request k} r_i sig_i : one wave per request, strided + LDS tree
+// skip (k_scalar_sig too): optional flag, nonzero -> nothing to do (the merged
+// check, whose sum came from the bucket MSM, passed: no per-request tails)
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
-                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S) {
+                                                  const g2j* __restrict__ rsig, g2a* __restrict__ S,
+                                                  const uint8_t* __restrict__ skip) {
   __shared__ g2j sh[TPB];
   const uint32_t k = blockIdx.x;
-  if (k >= n_req) return;
+  if (k >= n_req || (skip && *skip)) return;
   const uint32_t a = req_off[k], b = req_off[k + 1];
   g2j acc;
   jac_set_inf(acc);

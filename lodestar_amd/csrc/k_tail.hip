@@ -63,6 +63,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t
 
 // Merged check of a whole call (the worker's merged batch, worker.ts:41-96):
 // S_all = sum S_k and F_all = prod F_k over the requests not already false.
+// S == nullptr: S_all already came from the bucket MSM (k_msm_final); only F_all.
 // One wave; the tail kernel then verifies (F_all, S_all) once, and the
 // per-request tails only run if that merged check fails.
 // The worker's bookkeeping of its merged batch (worker.ts:66-85): batchRetries
@@ -145,8 +146,10 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
   fp12_one(f);
   for (uint32_t k = threadIdx.x; k < n_req; k += TPB) {
     if (req_bad[k]) continue;
-    const g2a s = S[k];
-    if (!s.inf) jac_add_aff(acc, acc, s);
+    if (S) {
+      const g2a s = S[k];
+      if (!s.inf) jac_add_aff(acc, acc, s);
+    }
     fp12 t = F[k];
     fp12_mul(f, f, t);
   }
@@ -155,9 +158,11 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
   __syncthreads();
   for (int st = TPB / 2; st > 0; st >>= 1) {
     if ((int)threadIdx.x < st) {
-      g2j m = shs[threadIdx.x], o = shs[threadIdx.x + st];
-      jac_add(m, m, o);
-      shs[threadIdx.x] = m;
+      if (S) {
+        g2j m = shs[threadIdx.x], o = shs[threadIdx.x + st];
+        jac_add(m, m, o);
+        shs[threadIdx.x] = m;
+      }
       fp12 a = shf[threadIdx.x], b = shf[threadIdx.x + st];
       fp12_mul(a, a, b);
       shf[threadIdx.x] = a;
@@ -165,10 +170,12 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    g2j tot = shs[0];
-    g2a sa;
-    jac_to_aff(sa, tot);
-    S_all[0] = sa;
+    if (S) {
+      g2j tot = shs[0];
+      g2a sa;
+      jac_to_aff(sa, tot);
+      S_all[0] = sa;
+    }
     F_all[0] = shf[0];
   }
 }

@@ -33,7 +33,7 @@ SET_STATUS_NAMES = {0: "OK", 1: "BAD_ENCODING", 2: "NOT_ON_CURVE", 3: "NOT_IN_GR
 EXPORTED_SYMBOLS = (
     "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
-    "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul",
+    "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul", "lb_g2_msm",
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
     "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
@@ -140,6 +140,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_batch_scalars.argtypes = [vp, vp, u32, u32, vp]
     lib.lb_g1_mul.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_g2_mul.argtypes = [vp, u32, vp, vp, vp]
+    lib.lb_g2_msm.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_verify_requests_device_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_Stats)]
@@ -608,6 +609,16 @@ class Device:
         self._check(self.lib.lb_g2_mul(self._h, n, _ptr(a), _ptr(k), _ptr(out)), "lb_g2_mul")
         return [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
 
+    def g2_msm(self, pts: Sequence[bytes], raw: Sequence[int]) -> bytes:
+        """sum_i (a_i + b_i lambda) P_i (a_i / b_i = low / high 32 bits of raw[i]) through
+        the merged check's bucket MSM; 192-byte uncompressed points in and out."""
+        n = len(pts)
+        a = _u8(b"".join(pts)) if n else np.zeros(1, np.uint8)
+        k = np.array(list(raw) or [0], dtype=np.uint64)
+        out = np.zeros(192, np.uint8)
+        self._check(self.lib.lb_g2_msm(self._h, n, _ptr(a), _ptr(k), _ptr(out)), "lb_g2_msm")
+        return out.tobytes()
+
     def sk_to_pk(self, sks_be32: Sequence[bytes]) -> List[bytes]:
         n = len(sks_be32)
         k = _u8(b"".join(sks_be32))
@@ -624,10 +635,10 @@ class Device:
         return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
 
     def last_stage_times(self) -> List[Tuple[str, float]]:
-        ms = (ctypes.c_float * 24)()
-        names = (ctypes.c_char_p * 24)()
-        n = self.lib.lb_last_stage_times(self._h, ms, names, 24)
-        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 24))]
+        ms = (ctypes.c_float * 32)()
+        names = (ctypes.c_char_p * 32)()
+        n = self.lib.lb_last_stage_times(self._h, ms, names, 32)
+        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 32))]
 
 
 def device_count() -> int:

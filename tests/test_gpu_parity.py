@@ -251,7 +251,7 @@ def test_c3_sync_aggregate_512(device):
 
 
 # ---- mixed block-import / gossip workloads vs the C oracle (configs C4 / C5 shapes) ----------
-def _mixed_workload(device, n_keys=512, n_sets=1500, seed=5):
+def _mixed_workload(device, n_keys=512, n_sets=1500, seed=5, inject=True):
     """Single sets, committee aggregates (2..64 pubkeys, same message, 192-byte
     aggregated signature), and injected failures: wrong message, malformed
     signatures (Buffer.alloc(96, 10), 32 zero bytes), infinite signature,
@@ -276,7 +276,7 @@ def _mixed_workload(device, n_keys=512, n_sets=1500, seed=5):
             msig, bad = device.aggregate_signatures(part)
             assert bad == -1
             sigs.append(msig)
-    for j in rnd.sample(range(n_sets), 40):
+    for j in rnd.sample(range(n_sets), 40 if inject else 0):
         kind = rnd.randrange(6)
         if kind == 0:
             msgs[j] = bytes(32)
@@ -350,3 +350,54 @@ def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split, tail_pri
             assert "join_halves" in dict(dev.last_stage_times())
     finally:
         dev.close()
+
+
+def _device_with_env(**env):
+    import os
+
+    from lodestar_amd.native import Device
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Device(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("inject", [True, False])
+def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject):
+    """The merged check's sum of r_i sig_i from the bucket MSM (k_msm.hip), forced
+    onto this 1,500-set call (LB_MSM_MIN=1; by default calls of >= 4096 sets):
+    with injected failures the merged check fails and the per-request tails take
+    their S_k from the per-set ladders; without, the merged check passes on the
+    MSM's sum alone.  Verdicts and rejection codes == the C oracle's."""
+    from oracle import c_oracle as C
+    args = mixed_workload_cache(device, inject)
+    seed = hashlib.sha256(b"msm-seed").digest()
+    dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines")
+    try:
+        res = dev.verify_requests(*args, seed)
+        stages = dict(dev.last_stage_times())
+        valid, err = C.verify_requests(*args, seed, threads=16)
+        assert list(res.errors) == list(err)
+        assert list(res.valid) == list(valid)
+        assert "msm_final" in stages and "msm_chunks" in stages
+        if inject:
+            assert res.batch_retries == 1 and "scalar_sig" in stages
+        else:
+            assert all(valid) and res.batch_retries == 0
+    finally:
+        dev.close()
+
+
+_MIXED = {}
+
+
+def mixed_workload_cache(device, inject):
+    if inject not in _MIXED:
+        _MIXED[inject] = _mixed_workload(device, inject=inject)
+    return _MIXED[inject]

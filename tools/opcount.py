@@ -64,8 +64,8 @@ def main():
                                   np.frombuffer(b"".join(msgs), np.uint8), blob, offs, bytes(32))
         assert res.valid.all(), res.valid
         names = [nm for nm, _ in dev.last_stage_times()]
-        buf = (ctypes.c_ulonglong * 24)()
-        k = lib.lb_opcount_stages(dev._h, buf, 24)
+        buf = (ctypes.c_ulonglong * 32)()
+        k = lib.lb_opcount_stages(dev._h, buf, 32)
         per = {}
         tot_mul = tot_sqr = 0
         for i in range(k):
