@@ -490,6 +490,24 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
                             "sets_per_job": per_job,
                             "api": "lb_verify_same_message_batch (host buffers, validator indices, one call)",
                             "stage_ms": sm_stage}
+    # (4) the same packages kept in flight (lb_verify_same_message_batch_async, what the pool's
+    # submission thread does): packed once, nbuf packages in flight, PCIe included
+    prep = dev.prepare_same_message(jobs, seed, by_index=True)
+    for pc in [dev.verify_same_message_prepared_async(prep) for _ in range(nbuf)]:
+        assert all(dev.wait_same_message(pc)[1])
+    t1 = time.perf_counter()
+    pend, allv = [], True
+    for _ in range(reps):
+        pend.append(dev.verify_same_message_prepared_async(prep))
+        if len(pend) >= nbuf:
+            allv &= all(dev.wait_same_message(pend.pop(0))[1])
+    for pc in pend:
+        allv &= all(dev.wait_same_message(pc)[1])
+    el = time.perf_counter() - t1
+    legs["same_message_inflight"] = {"sets_per_s": round(n_jobs * per_job * reps / el, 1), "packages": reps,
+                                     "all_fast": bool(allv), "jobs": n_jobs, "sets_per_job": per_job,
+                                     "api": f"lb_verify_same_message_batch_async, {nbuf} packages in flight "
+                                            "(host buffers, validator indices)"}
     return legs
 
 

@@ -249,6 +249,14 @@ typedef struct {
 } lb_same_message_batch;
 int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* batch, uint8_t* out_valid,
                                  uint8_t* out_job_fast, lb_verify_stats* stats);
+/* The same, asynchronous, on the ring of calls in flight (like lb_verify_requests_async):
+ * the inputs are staged before it returns; out_valid / out_job_fast are written when the
+ * call retires (lb_wait(ticket, stats), or when its slot is reused).  The per-set retry of
+ * failed jobs runs on the same slot from the device-resident decoded signatures (no second
+ * request batch, no re-upload); the pool's packages in flight across workers
+ * (BN/chain/bls/multithread/index.ts:362-519). */
+int lb_verify_same_message_batch_async(lb_ctx* ctx, const lb_same_message_batch* batch, uint8_t* out_valid,
+                                       uint8_t* out_job_fast, uint64_t* out_ticket);
 
 /* Sum of n uncompressed pubkeys -> 96-byte uncompressed encoding.  n == 0 ->
  * LB_ERR_INVALID_ARGUMENT (EMPTY_AGGREGATE_ARRAY). *out_status = LB_SET_*. */

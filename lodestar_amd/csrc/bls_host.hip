@@ -70,6 +70,29 @@ struct PipeState {
   uint32_t* d_mstats = nullptr;
 };
 
+// A same-message package in flight (lb_verify_same_message_batch[_async]):
+// what its completion needs after phase 1 (the jobs' aggregated sets) to
+// publish verdicts and, for failed jobs, to run phase 2 (every set of those
+// jobs alone) on the same slot from the device-resident decoded signatures.
+struct SmState {
+  bool active = false;
+  bool by_index = false;
+  uint32_t nj = 0, ns = 0;
+  uint8_t* out_valid = nullptr;     // caller: n_sets verdicts
+  uint8_t* out_job_fast = nullptr;  // caller (optional): n_jobs flags
+  const uint32_t* h_joff = nullptr;  // pinned copy of job_offsets
+  const uint8_t* h_res = nullptr;    // pinned phase-1 results: valid, err, job_bad, pk status (al(nj) each)
+  uint32_t* h_rset = nullptr;        // pinned: phase-2 set indices, then job indices (ns each)
+  uint8_t* h_rout = nullptr;         // pinned: phase-2 verdicts, errors (al(ns) each)
+  // device-resident phase-1 data
+  const uint8_t* d_pks = nullptr;    // 96-byte keys or u32 indices (by_index)
+  const g2j* d_sig = nullptr;        // decoded signatures (validate=true done once)
+  const uint8_t* d_sst = nullptr;
+  const uint8_t* d_msgs = nullptr;
+  const uint8_t* d_seed = nullptr;
+  size_t ws_off = 0;                 // bump offset after phase 1 (phase 2 allocates from here)
+};
+
 // One in-flight call: two streams (DAG), own workspace, staging and events.
 struct Slot {
   hipStream_t st[2] = {};
@@ -99,6 +122,7 @@ struct Slot {
   char* h_out = nullptr;
   uint8_t *out_valid = nullptr, *out_err = nullptr, *out_sst = nullptr;
   uint32_t out_nr = 0, out_ns = 0;
+  SmState sm;
 };
 
 // Stats of a retired call, kept per ticket (lb_wait reports the stats of ITS
@@ -320,10 +344,13 @@ int run_tails(lb_ctx* ctx, Slot& sl) {
 int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
                  const uint8_t* d_pks, const uint32_t* d_pk_off, const uint32_t* d_pk_idx, const uint8_t* d_msgs, const uint8_t* d_sigs,
                  const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
-                 uint8_t* d_set_status, Bump& ws, uint8_t* d_partial = nullptr) {
+                 uint8_t* d_set_status, Bump& ws, uint8_t* d_partial = nullptr, const g2j* d_sig_pre = nullptr,
+                 const uint8_t* d_sst_pre = nullptr) {
+  // d_sig_pre / d_sst_pre: signatures already decoded and validated (same-message
+  // phase 2): no k_decode_sigs, d_sigs / d_sig_off unused
   const bool partial = d_partial != nullptr;
   const uint32_t ns = n_sets ? n_sets : 1;
-  g2j* d_sig = ws.take<g2j>(ns);
+  g2j* d_sig = d_sig_pre ? const_cast<g2j*>(d_sig_pre) : ws.take<g2j>(ns);
   g2j* d_rsig = ws.take<g2j>(ns);
   g2j* d_q = ws.take<g2j>(2 * (size_t)ns);
   g2j* d_h = ws.take<g2j>(ns);
@@ -339,11 +366,25 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   const bool merged = partial || (tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req);
   const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
   const bool use_msm = merged && n_sets && ctx->msm_min_sets && n_sets >= ctx->msm_min_sets;
+  // a lone call on an otherwise idle GPU splits every request of the Miller
+  // accumulation in two halves: twice the waves (one per SIMD for a 65,536-set
+  // call instead of one per two SIMDs) at the price of the halves' separate
+  // Fp12 squarings; with other calls in flight the idle SIMDs run their stages
+  // instead and the work-efficient form is kept (LB_ACC_SPLIT=0|1 forces one)
+  bool lone = true;
+  for (int s = 0; s < ctx->n_slots; s++)
+    if (&ctx->slots[s] != &sl && ctx->slots[s].busy) lone = false;
+  const bool split = by_lines && (ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64));
+  // merged pair (-g1, S_all) with S_all from the MSM: without a split its Miller
+  // value is one extra workgroup of k_miller_acc (fold; its 512 request waves
+  // leave SIMDs free), otherwise its lines are stored right after the MSM, on
+  // stream 0 beside stream 1's hash/lines (lines_all), and k_tail multiplies it in
+  const bool fold = use_msm && by_lines && !split;
   uint32_t* d_lines =
       (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
   uint8_t* d_pk_st = ws.take<uint8_t>(ns);
-  uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
+  uint8_t* d_sig_st = d_sst_pre ? const_cast<uint8_t*>(d_sst_pre) : d_set_status ? d_set_status : ws.take<uint8_t>(ns);
   g2a* d_S = ws.take<g2a>(n_req);
   fp12* d_fS = ws.take<fp12>(n_req);
   fp12* d_F = ws.take<fp12>(n_req);
@@ -399,8 +440,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1j*)d_rpk, (const g2j*)d_h,
              d_f);
   if (n_sets) {
-    LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
-             (const uint8_t*)d_single, d_sig, d_sig_st);
+    if (!d_sig_pre)
+      LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
+               (const uint8_t*)d_single, d_sig, d_sig_st);
     if (!use_msm)
       LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
                (const uint8_t*)d_sig_st, d_rsig, (const uint8_t*)nullptr);
@@ -424,6 +466,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const g2j*)d_mcsum, d_mbsum);
     LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_mbsum, d_mG);
     LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
+    if (!fold)
+      LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+               (const uint8_t*)nullptr);
   } else {
     LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S, (const uint8_t*)nullptr);
   }
@@ -434,16 +479,12 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("miller_S", 0, k_miller_S, blocks_for(n_req), TPB, n_req, (const g2a*)d_S, d_fS);
   const fp12* fS_in = tail_wave ? nullptr : (const fp12*)d_fS;
   LB_TRY(stream_wait(ctx, sl, 1, 0, 2));
+  fp12* d_Fx = fold ? ws.take<fp12>(1) : nullptr;
+  if (ws.off > ws.cap) {
+    ctx->err = "workspace overflow";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
   if (by_lines) {
-    // a lone call on an otherwise idle GPU splits every request in two halves:
-    // twice the waves (one per SIMD for a 65,536-set call instead of one per
-    // two SIMDs) at the price of the halves' separate Fp12 squarings; with
-    // other calls in flight the idle SIMDs run their stages instead and the
-    // work-efficient form is kept (LB_ACC_SPLIT=0|1 forces one)
-    bool lone = true;
-    for (int s = 0; s < ctx->n_slots; s++)
-      if (&ctx->slots[s] != &sl && ctx->slots[s].busy) lone = false;
-    const bool split = ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64);
     const uint32_t nr = split ? 2 * n_req : n_req;
     const uint32_t* acc_off = d_req_off;
     fp12* acc_F = d_F;
@@ -462,12 +503,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_HIP(hipGetLastError());
       acc_off = off2;
     }
-    const uint32_t rpw = TPB / ctx->acc_lpr, grid = (nr + rpw - 1) / rpw;
+    const uint32_t rpw = TPB / ctx->acc_lpr, grid = (nr + rpw - 1) / rpw + (fold ? 1u : 0u);
     const fp12* acc_fS = split ? nullptr : fS_in;
     const uint32_t halves = split ? 1u : 0u;
 #define LB_ACC_STAGE(L)                                                                                       \
   LB_STAGE("miller_acc", 0, k_miller_acc<L>, grid, TPB, nr, acc_off, n_pairs, (const uint32_t*)d_lines, acc_fS, \
-           (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, acc_F, acc_bad, acc_err, halves)
+           (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, acc_F, acc_bad, acc_err, halves,               \
+           fold ? (const g2a*)d_Sall : (const g2a*)nullptr, d_Fx)
     if (ctx->acc_lpr == 16)
       LB_ACC_STAGE(16);
     else if (ctx->acc_lpr == 32)
@@ -513,13 +555,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_HIP(hipMemsetAsync(d_mflag, 0, 2, ts));
     LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, use_msm ? (const g2a*)nullptr : (const g2a*)d_S,
                 (const fp12*)d_F, (const uint8_t*)d_bad,
-                d_Sall, d_Fall);
-    LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
-                (const uint8_t*)nullptr);
+                d_Sall, d_Fall, (const fp12*)d_Fx);
+    if (!use_msm)  // (with the MSM: folded into k_miller_acc, or stored right after the MSM)
+      LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+                  (const uint8_t*)nullptr);
+    const uint32_t* merged_lines = fold ? nullptr : (const uint32_t*)d_lines;
     if (partial) {
       // two-phase call: the merged Miller product goes to the host, which
       // combines it with the other GPUs' partials; the tails wait for its verdict
-      LB_STAGE_ON("partial", ts, k_partial, 1u, TPB, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+      LB_STAGE_ON("partial", ts, k_partial, 1u, TPB, n_pairs, n_sets + n_req, merged_lines,
                   (const fp12*)d_Fall, d_partial);
       LB_HIP(hipMemcpyAsync(sl.h_partial, d_partial, LB_GT_BYTES, hipMemcpyDeviceToHost, ts));
       LB_HIP(hipEventRecord(sl.partial_ev, ts));
@@ -530,7 +574,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       sl.partial_pending = true;
       return LB_OK;
     }
-    LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const uint32_t*)d_lines,
+    LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, merged_lines,
                 (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
     if (ts != sl.st[0]) {
       LB_HIP(hipEventRecord(sl.dep[4], ts));
@@ -595,10 +639,13 @@ int finish_partial(lb_ctx* ctx, Slot& sl, bool merged_ok) {
 // Wait for a slot's outstanding call and publish its stage times, stats and
 // (host-buffer calls) verdicts.  A two-phase call whose host verdict never came
 // runs its per-request tails (merged_ok = 0: every verdict computed alone).
+int sm_complete(lb_ctx* ctx, Slot& sl);
+
 int finish_slot(lb_ctx* ctx, Slot& sl) {
   if (!sl.busy) return LB_OK;
   LB_TRY(finish_partial(ctx, sl, false));
   LB_HIP(hipEventSynchronize(sl.done));
+  if (sl.sm.active) LB_TRY(sm_complete(ctx, sl));
   ctx->n_stages = sl.n_stages;
   for (int i = 0; i < sl.n_stages; i++) {
     float ms = 0.f;
@@ -1430,16 +1477,43 @@ int lb_aggregate_signatures(lb_ctx* ctx, uint32_t n, const uint8_t* sigs, const 
 // jobs: jobItemWorkReq sameMessage, jobItem.ts:64-86, the worker's verify of
 // the aggregated set, index.ts:455-489, and the per-set retry of failed jobs,
 // index.ts:473-484,557-568 / jobItemSameMessageToMultiSet, jobItem.ts:93-125).
-// One device pass for all jobs: every signature decoded + validated ONCE,
-// pubkeys and signatures summed per job, and every job's aggregated set verified
-// as a 1-set request of ONE merged call; only the sets of failed jobs are then
-// re-verified, each alone, in one more call.
-int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* b, uint8_t* out_valid,
-                                 uint8_t* out_job_fast, lb_verify_stats* stats) {
-  if (!ctx || !b || (b->n_sets && !out_valid)) return LB_ERR_INVALID_ARGUMENT;
+// Phase 1 (sm_submit): every signature decoded + validated ONCE, pubkeys and
+// signatures summed per job, every job's aggregated set verified as a 1-set
+// request of ONE merged call.  Phase 2 (sm_complete, when the call retires and
+// only if a job failed): the sets of the failed jobs, each its own 1-set
+// request, through the same pipeline on the same slot -- signatures from the
+// phase-1 decode (k_sm_retry_gather), pubkeys / messages from the phase-1
+// uploads: nothing re-packed or re-uploaded but the retry index list.
+}  // extern "C"
+
+// phase-2 inputs: retry r = set rset[r] of job rjob[r] as a 1-set request
+__global__ void __launch_bounds__(TPB) k_sm_retry_gather(uint32_t n, const uint32_t* __restrict__ rset,
+                                                         const uint32_t* __restrict__ rjob,
+                                                         const g2j* __restrict__ sig, const uint8_t* __restrict__ sst,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint32_t* __restrict__ pk_index, g2j* __restrict__ out_sig,
+                                                         uint8_t* __restrict__ out_st, uint8_t* __restrict__ out_msg,
+                                                         uint32_t* __restrict__ out_idx, uint32_t* __restrict__ out_req) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t i = rset[r], j = rjob[r];
+  const g2j g = sig[i];
+  uint8_t st = sst[i];
+  // a 1-set request: core verify rejects the infinite signature (k_decode_sigs' single-set rule)
+  if (st == LB_ST_OK && jac_is_inf(g)) st = LB_ST_ZERO_SIGNATURE;
+  out_sig[r] = g;
+  out_st[r] = st;
+  for (int k = 0; k < 32; k++) out_msg[(size_t)r * 32 + k] = msgs[(size_t)j * 32 + k];
+  // the set's key: its validator index, or row i of the package's 96-byte keys
+  out_idx[r] = pk_index ? pk_index[i] : (i | LB_PK_ROW_FLAG);
+  out_req[r] = r;
+  if (r == n - 1) out_req[n] = n;
+}
+
+namespace {
+
+int sm_validate(lb_ctx* ctx, const lb_same_message_batch* b) {
   const uint32_t nj = b->n_jobs, ns = b->n_sets;
-  if (stats) *stats = lb_verify_stats{0, 0, 0.0};
-  if (nj == 0) return LB_OK;
   if (!b->job_offsets || !b->sig_offsets || !b->messages || !b->seed || (ns && !b->signatures) ||
       (ns && !b->pubkeys && !b->pubkey_indices)) {
     ctx->err = "null pointer in lb_same_message_batch";
@@ -1459,147 +1533,215 @@ int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* b, ui
       ctx->err = "sig_offsets not monotone";
       return LB_ERR_INVALID_ARGUMENT;
     }
-  LB_HIP(hipSetDevice(ctx->device));
+  return LB_OK;
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// phase-2 device reserve: the retry pipeline over at most every set, its gathered inputs
+size_t sm_phase2_bytes(uint32_t ns) {
+  const size_t n = ns ? ns : 1;
+  return pipeline_ws_bytes(ns, ns) + n * (2 * 4 + sizeof(g2j) + 1 + 32 + 4 + 4 + 2) + 16 * 256;
+}
+
+// Phase 1 on slot `sl` (already retired by the caller); the call stays busy
+// until finish_slot, which runs sm_complete.
+int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* out_valid, uint8_t* out_job_fast) {
+  const uint32_t nj = b->n_jobs, ns = b->n_sets;
   const bool by_index = b->pubkey_indices != nullptr;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t sz_joff = sizeof(uint32_t) * (nj + 1), sz_pk = (size_t)ns * (by_index ? 4 : 96),
                sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = b->sig_offsets[ns], sz_msg = (size_t)nj * 32,
                sz_seed = 32, sz_areq = sizeof(uint32_t) * (nj + 1), sz_asig = sizeof(uint32_t) * (nj + 1);
-  const size_t in_bytes =
-      al(sz_joff) + al(sz_pk) + al(sz_sigo) + al(sz_sig) + al(sz_msg) + al(sz_seed) + al(sz_areq) + al(sz_asig);
-  const size_t out_bytes = 4 * al(nj);
+  const size_t in_bytes = al256(sz_joff) + al256(sz_pk) + al256(sz_sigo) + al256(sz_sig) + al256(sz_msg) +
+                          al256(sz_seed) + al256(sz_areq) + al256(sz_asig);
   const size_t ns1 = ns ? ns : 1;
+  const size_t res_bytes = 4 * al256(nj), retry_bytes = 2 * al256(4 * ns1) + 2 * al256(ns1);
   const size_t extra = ns1 * (sizeof(g2j) + 1) + (size_t)nj * (sizeof(g1j) + 1 + 96 + 192 + 1 + 2) + 16 * 256;
-  std::vector<uint8_t> fast(nj);
-  {
-    BorrowGuard g{ctx};  // slot 0, two-stream DAG
-    LB_TRY(borrow_second_stream(ctx, g));
-    Slot& sl = ctx->slots[0];
-    LB_TRY(finish_slot(ctx, sl));
-    LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
-    LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj)));
-    Bump ws{sl.d_ws, 0, sl.ws_cap};
-    char* h = sl.h_pin;
-    size_t ho = 0;
-    auto stage = [&](const void* src, size_t n) {
-      char* p = h + ho;
-      if (n && src) memcpy(p, src, n);
-      ho += al(n);
-      return p;
-    };
-    stage(b->job_offsets, sz_joff);
-    stage(by_index ? (const void*)b->pubkey_indices : (const void*)b->pubkeys, sz_pk);
-    stage(b->sig_offsets, sz_sigo);
-    stage(b->signatures, sz_sig);
-    stage(b->messages, sz_msg);
-    stage(b->seed, sz_seed);
-    uint32_t* areq = (uint32_t*)stage(nullptr, sz_areq);
-    uint32_t* asig = (uint32_t*)stage(nullptr, sz_asig);
-    for (uint32_t j = 0; j <= nj; j++) {
-      areq[j] = j;        // every job one request of one (aggregated) set
-      asig[j] = 192 * j;  // Signature.aggregate(...).toBytes(uncompressed)
-    }
-    char* d_in = ws.take<char>(in_bytes);
-    size_t o = 0;
-    auto dptr = [&](size_t n) {
-      char* p = d_in + o;
-      o += al(n);
-      return p;
-    };
-    const uint32_t* d_joff = (const uint32_t*)dptr(sz_joff);
-    const uint8_t* d_pks = (const uint8_t*)dptr(sz_pk);
-    const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
-    const uint8_t* d_sigs = (const uint8_t*)dptr(sz_sig);
-    const uint8_t* d_msgs = (const uint8_t*)dptr(sz_msg);
-    const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
-    const uint32_t* d_areq = (const uint32_t*)dptr(sz_areq);
-    const uint32_t* d_asig = (const uint32_t*)dptr(sz_asig);
-    g2j* d_sig = ws.take<g2j>(ns1);
-    uint8_t* d_sst = ws.take<uint8_t>(ns1);
-    g1j* d_jpk = ws.take<g1j>(nj);
-    uint8_t* d_jpkst = ws.take<uint8_t>(nj);
-    uint8_t* d_pk96 = ws.take<uint8_t>((size_t)nj * 96);
-    uint8_t* d_sig192 = ws.take<uint8_t>((size_t)nj * 192);
-    uint8_t* d_jbad = ws.take<uint8_t>(nj);
-    uint8_t* d_valid = ws.take<uint8_t>(nj);
-    uint8_t* d_err = ws.take<uint8_t>(nj);
-    LB_TRY(begin_call(ctx, sl));
-    LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
-    if (ns)
-      LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
-               d_sst);
-    const PkSource src{by_index ? nullptr : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
-                       ctx->table_n};
-    const uint32_t agg_grid = nj < 16384u ? nj : 16384u;
-    LB_STAGE("sm_pubkeys", 0, k_pubkeys_single, blocks_for(nj), TPB, nj, src, d_joff, d_jpk, d_jpkst);
-    LB_STAGE("sm_pubkeys_agg", 0, k_pubkeys_agg, agg_grid, TPB, nj, src, d_joff, d_jpk, d_jpkst);
-    LB_STAGE("sm_aggregate", 0, k_same_message_agg, agg_grid, TPB, nj, d_joff, (const g2j*)d_sig,
-             (const uint8_t*)d_sst, (const g1j*)d_jpk, d_pk96, d_sig192, d_jbad);
-    LB_TRY(run_pipeline(ctx, sl, nj, nj, d_areq, d_pk96, nullptr, nullptr, d_msgs, d_sig192, d_asig, d_seed, d_valid,
-                        d_err, nullptr, ws));
-    char* h_out = h + in_bytes;
-    LB_HIP(hipMemcpyAsync(h_out, d_valid, nj, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_HIP(hipMemcpyAsync(h_out + al(nj), d_err, nj, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_HIP(hipMemcpyAsync(h_out + 2 * al(nj), d_jbad, nj, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_HIP(hipMemcpyAsync(h_out + 3 * al(nj), d_jpkst, nj, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_TRY(end_call_async(ctx, sl));
-    LB_TRY(finish_slot(ctx, sl));
-    if (stats) stats->device_ms = ctx->wall_ms;
-    // fast path per job: aggregated set valid, every signature validated, pubkeys aggregated
-    const uint8_t *v = (const uint8_t*)h_out, *e = v + al(nj), *jb = v + 2 * al(nj), *pst = v + 3 * al(nj);
-    for (uint32_t j = 0; j < nj; j++) fast[j] = v[j] && e[j] == LB_REQ_OK && !jb[j] && pst[j] == LB_ST_OK;
-    for (uint32_t j = 0; j < nj; j++) {
-      if (out_job_fast) out_job_fast[j] = fast[j];
-      if (fast[j])
-        for (uint32_t i = b->job_offsets[j]; i < b->job_offsets[j + 1]; i++) out_valid[i] = 1;
-    }
-    uint32_t fast_sets = 0, retried_jobs = 0;
-    for (uint32_t j = 0; j < nj; j++) {
-      const uint32_t n_j = b->job_offsets[j + 1] - b->job_offsets[j];
-      if (fast[j])
-        fast_sets += n_j;
-      else if (n_j)
-        retried_jobs++;
-    }
-    if (stats) {
-      stats->batch_retries = retried_jobs;
-      stats->batch_sigs_success = fast_sets;
-    }
-    if (retried_jobs == 0) return LB_OK;
+  LB_TRY(ensure_pin(ctx, sl, in_bytes + res_bytes + retry_bytes));
+  LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj) + sm_phase2_bytes(ns)));
+  Bump ws{sl.d_ws, 0, sl.ws_cap};
+  char* h = sl.h_pin;
+  size_t ho = 0;
+  auto stage = [&](const void* src, size_t n) {
+    char* p = h + ho;
+    if (n && src) memcpy(p, src, n);
+    ho += al256(n);
+    return p;
+  };
+  const uint32_t* h_joff = (const uint32_t*)stage(b->job_offsets, sz_joff);
+  stage(by_index ? (const void*)b->pubkey_indices : (const void*)b->pubkeys, sz_pk);
+  stage(b->sig_offsets, sz_sigo);
+  stage(b->signatures, sz_sig);
+  stage(b->messages, sz_msg);
+  stage(b->seed, sz_seed);
+  uint32_t* areq = (uint32_t*)stage(nullptr, sz_areq);
+  uint32_t* asig = (uint32_t*)stage(nullptr, sz_asig);
+  for (uint32_t j = 0; j <= nj; j++) {
+    areq[j] = j;        // every job one request of one (aggregated) set
+    asig[j] = 192 * j;  // Signature.aggregate(...).toBytes(uncompressed)
   }
-  // per-set retry of the failed jobs: every set its own (non-batchable) 1-set request
-  std::vector<uint32_t> fs;
-  std::vector<uint32_t> req_off{0}, sig_off{0}, idx;
-  std::vector<uint8_t> pks, sigs, msgs;
+  char* d_in = ws.take<char>(in_bytes);
+  size_t o = 0;
+  auto dptr = [&](size_t n) {
+    char* p = d_in + o;
+    o += al256(n);
+    return p;
+  };
+  const uint32_t* d_joff = (const uint32_t*)dptr(sz_joff);
+  const uint8_t* d_pks = (const uint8_t*)dptr(sz_pk);
+  const uint32_t* d_sigo = (const uint32_t*)dptr(sz_sigo);
+  const uint8_t* d_sigs = (const uint8_t*)dptr(sz_sig);
+  const uint8_t* d_msgs = (const uint8_t*)dptr(sz_msg);
+  const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
+  const uint32_t* d_areq = (const uint32_t*)dptr(sz_areq);
+  const uint32_t* d_asig = (const uint32_t*)dptr(sz_asig);
+  g2j* d_sig = ws.take<g2j>(ns1);
+  uint8_t* d_sst = ws.take<uint8_t>(ns1);
+  g1j* d_jpk = ws.take<g1j>(nj);
+  uint8_t* d_jpkst = ws.take<uint8_t>(nj);
+  uint8_t* d_pk96 = ws.take<uint8_t>((size_t)nj * 96);
+  uint8_t* d_sig192 = ws.take<uint8_t>((size_t)nj * 192);
+  uint8_t* d_jbad = ws.take<uint8_t>(nj);
+  uint8_t* d_valid = ws.take<uint8_t>(nj);
+  uint8_t* d_err = ws.take<uint8_t>(nj);
+  LB_TRY(begin_call(ctx, sl));
+  LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
+  if (ns)
+    LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
+             d_sst);
+  const PkSource src{by_index ? nullptr : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
+                     ctx->table_n};
+  const uint32_t agg_grid = nj < 16384u ? nj : 16384u;
+  LB_STAGE("sm_pubkeys", 0, k_pubkeys_single, blocks_for(nj), TPB, nj, src, d_joff, d_jpk, d_jpkst);
+  LB_STAGE("sm_pubkeys_agg", 0, k_pubkeys_agg, agg_grid, TPB, nj, src, d_joff, d_jpk, d_jpkst);
+  LB_STAGE("sm_aggregate", 0, k_same_message_agg, agg_grid, TPB, nj, d_joff, (const g2j*)d_sig, (const uint8_t*)d_sst,
+           (const g1j*)d_jpk, d_pk96, d_sig192, d_jbad);
+  LB_TRY(run_pipeline(ctx, sl, nj, nj, d_areq, d_pk96, nullptr, nullptr, d_msgs, d_sig192, d_asig, d_seed, d_valid,
+                      d_err, nullptr, ws));
+  char* h_res = h + in_bytes;
+  LB_HIP(hipMemcpyAsync(h_res, d_valid, nj, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_HIP(hipMemcpyAsync(h_res + al256(nj), d_err, nj, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_HIP(hipMemcpyAsync(h_res + 2 * al256(nj), d_jbad, nj, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_HIP(hipMemcpyAsync(h_res + 3 * al256(nj), d_jpkst, nj, hipMemcpyDeviceToHost, sl.st[0]));
+  SmState& m = sl.sm;
+  m.active = true;
+  m.by_index = by_index;
+  m.nj = nj;
+  m.ns = ns;
+  m.out_valid = out_valid;
+  m.out_job_fast = out_job_fast;
+  m.h_joff = h_joff;
+  m.h_res = (const uint8_t*)h_res;
+  m.h_rset = (uint32_t*)(h_res + res_bytes);
+  m.h_rout = (uint8_t*)(h_res + res_bytes + 2 * al256(4 * ns1));
+  m.d_pks = d_pks;
+  m.d_sig = d_sig;
+  m.d_sst = d_sst;
+  m.d_msgs = d_msgs;
+  m.d_seed = d_seed;
+  m.ws_off = ws.off;
+  return end_call_async(ctx, sl);
+}
+
+// Completion of a same-message call after its phase 1: verdicts of the jobs
+// whose aggregate passed, and phase 2 for the sets of the others.
+int sm_complete(lb_ctx* ctx, Slot& sl) {
+  SmState& m = sl.sm;
+  m.active = false;
+  const uint32_t nj = m.nj, ns = m.ns;
+  const uint8_t *v = m.h_res, *e = v + al256(nj), *jb = v + 2 * al256(nj), *pst = v + 3 * al256(nj);
+  uint32_t fast_sets = 0, retried_jobs = 0, nr = 0;
   for (uint32_t j = 0; j < nj; j++) {
-    if (fast[j]) continue;
-    for (uint32_t i = b->job_offsets[j]; i < b->job_offsets[j + 1]; i++) {
-      fs.push_back(i);
-      req_off.push_back((uint32_t)fs.size());
-      if (by_index)
-        idx.push_back(b->pubkey_indices[i]);
-      else
-        pks.insert(pks.end(), b->pubkeys + (size_t)i * 96, b->pubkeys + (size_t)i * 96 + 96);
-      sigs.insert(sigs.end(), b->signatures + b->sig_offsets[i], b->signatures + b->sig_offsets[i + 1]);
-      sig_off.push_back((uint32_t)sigs.size());
-      msgs.insert(msgs.end(), b->messages + (size_t)j * 32, b->messages + (size_t)j * 32 + 32);
+    // fast path: aggregated set valid, every signature validated, pubkeys aggregated
+    const bool fast = v[j] && e[j] == LB_REQ_OK && !jb[j] && pst[j] == LB_ST_OK;
+    if (m.out_job_fast) m.out_job_fast[j] = fast ? 1 : 0;
+    const uint32_t a = m.h_joff[j], b = m.h_joff[j + 1];
+    if (fast) {
+      for (uint32_t i = a; i < b; i++) m.out_valid[i] = 1;
+      fast_sets += b - a;
+    } else if (b > a) {
+      retried_jobs++;
+      for (uint32_t i = a; i < b; i++) {
+        m.h_rset[nr] = i;
+        m.h_rset[(size_t)ns + nr] = j;
+        nr++;
+      }
     }
   }
-  if (fs.empty()) return LB_OK;
-  if (sigs.empty()) sigs.push_back(0);
-  lb_request_batch rb{};
-  rb.n_requests = (uint32_t)fs.size();
-  rb.n_sets = (uint32_t)fs.size();
-  rb.request_offsets = req_off.data();
-  rb.pubkeys = by_index ? nullptr : pks.data();
-  rb.pubkey_indices = by_index ? idx.data() : nullptr;
-  rb.messages = msgs.data();
-  rb.signatures = sigs.data();
-  rb.sig_offsets = sig_off.data();
-  rb.seed = b->seed;
-  std::vector<uint8_t> rv(fs.size()), re(fs.size());
-  LB_TRY(lb_verify_requests(ctx, &rb, rv.data(), re.data(), nullptr, nullptr));
-  for (size_t k = 0; k < fs.size(); k++) out_valid[fs[k]] = (rv[k] && re[k] == LB_REQ_OK) ? 1 : 0;
+  if (nr) {
+    Bump ws{sl.d_ws, m.ws_off, sl.ws_cap};
+    uint32_t* d_rset = ws.take<uint32_t>(2 * (size_t)ns);
+    g2j* d_rsig = ws.take<g2j>(nr);
+    uint8_t* d_rst = ws.take<uint8_t>(nr);
+    uint8_t* d_rmsg = ws.take<uint8_t>((size_t)nr * 32);
+    uint32_t* d_ridx = ws.take<uint32_t>(nr);
+    uint32_t* d_rreq = ws.take<uint32_t>((size_t)nr + 1);
+    uint8_t* d_rvalid = ws.take<uint8_t>(nr);
+    uint8_t* d_rerr = ws.take<uint8_t>(nr);
+    if (ws.off > ws.cap) {
+      ctx->err = "workspace overflow";
+      return LB_ERR_OUT_OF_MEMORY;
+    }
+    LB_HIP(hipMemcpyAsync(d_rset, m.h_rset, sizeof(uint32_t) * 2 * (size_t)ns, hipMemcpyHostToDevice, sl.st[0]));
+    hipLaunchKernelGGL(k_sm_retry_gather, dim3(blocks_for(nr)), dim3(TPB), 0, sl.st[0], nr, (const uint32_t*)d_rset,
+                       (const uint32_t*)(d_rset + ns), m.d_sig, m.d_sst, m.d_msgs,
+                       m.by_index ? (const uint32_t*)m.d_pks : (const uint32_t*)nullptr, d_rsig, d_rst, d_rmsg, d_ridx,
+                       d_rreq);
+    LB_HIP(hipGetLastError());
+    LB_TRY(run_pipeline(ctx, sl, nr, nr, d_rreq, m.by_index ? nullptr : m.d_pks, nullptr, d_ridx, d_rmsg, nullptr,
+                        nullptr, m.d_seed, d_rvalid, d_rerr, nullptr, ws, nullptr, d_rsig, d_rst));
+    LB_HIP(hipMemcpyAsync(m.h_rout, d_rvalid, nr, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_HIP(hipMemcpyAsync(m.h_rout + al256(ns), d_rerr, nr, hipMemcpyDeviceToHost, sl.st[0]));
+    LB_TRY(end_call(ctx, sl));
+    LB_HIP(hipEventSynchronize(sl.done));
+    for (uint32_t r = 0; r < nr; r++)
+      m.out_valid[m.h_rset[r]] = (m.h_rout[r] && m.h_rout[al256(ns) + r] == LB_REQ_OK) ? 1 : 0;
+  }
+  // the package's worker bookkeeping (index.ts:557-568): jobs retried set by set,
+  // sets verified by a passing aggregate (after phase 2's own merged-check stats)
+  sl.h_stats[0] = retried_jobs;
+  sl.h_stats[1] = fast_sets;
+  return LB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lb_verify_same_message_batch_async(lb_ctx* ctx, const lb_same_message_batch* b, uint8_t* out_valid,
+                                       uint8_t* out_job_fast, uint64_t* out_ticket) {
+  if (!ctx || !b || !out_ticket || (b->n_sets && !out_valid)) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(sm_validate(ctx, b));
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot& sl = next_async_slot(ctx);
+  LB_TRY(finish_slot(ctx, sl));
+  if (b->n_jobs == 0) {  // nothing to verify: a call that completes at once
+    LB_TRY(begin_call(ctx, sl));
+    LB_TRY(end_call_async(ctx, sl));
+    *out_ticket = sl.ticket;
+    return LB_OK;
+  }
+  LB_TRY(sm_submit(ctx, sl, b, out_valid, out_job_fast));
+  *out_ticket = sl.ticket;
+  return LB_OK;
+}
+
+// Synchronous form: slot 0 as the two-stream DAG (lowest latency).
+int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* b, uint8_t* out_valid,
+                                 uint8_t* out_job_fast, lb_verify_stats* stats) {
+  if (!ctx || !b || (b->n_sets && !out_valid)) return LB_ERR_INVALID_ARGUMENT;
+  if (stats) *stats = lb_verify_stats{0, 0, 0.0};
+  if (b->n_jobs == 0) return LB_OK;
+  LB_TRY(sm_validate(ctx, b));
+  LB_HIP(hipSetDevice(ctx->device));
+  BorrowGuard g{ctx};
+  LB_TRY(borrow_second_stream(ctx, g));
+  Slot& sl = ctx->slots[0];
+  LB_TRY(finish_slot(ctx, sl));
+  LB_TRY(sm_submit(ctx, sl, b, out_valid, out_job_fast));
+  const uint64_t t = sl.ticket;
+  LB_TRY(finish_slot(ctx, sl));
+  fill_stats(ctx, t, stats);
   return LB_OK;
 }
 

@@ -16,7 +16,7 @@
 #include <stdint.h>
 
 #ifndef LB_HD
-#if defined(__HIPCC__) || defined(__CUDACC__)
+#if defined(__HIPCC__)
 #define LB_HD __host__ __device__ __forceinline__
 #else
 #define LB_HD inline

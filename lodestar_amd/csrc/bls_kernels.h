@@ -158,7 +158,8 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
                                                                     const uint8_t* __restrict__ sig_status,
                                                                     const uint8_t* __restrict__ pk_status,
                                                                     fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
-                                                                    uint8_t* __restrict__ req_err, uint32_t halves);
+                                                                    uint8_t* __restrict__ req_err, uint32_t halves,
+                                                                    const g2a* __restrict__ Sx, fp12* __restrict__ Fx);
 __global__ void __launch_bounds__(TPB) k_split_requests(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                         uint32_t* __restrict__ off2);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_join_halves(uint32_t n_req, const uint32_t* __restrict__ req_off,
@@ -180,7 +181,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,
-                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all);
+                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all,
+                                                        const fp12* __restrict__ Fx);
 __global__ void __launch_bounds__(TPB) k_merge_stats(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                      const uint8_t* __restrict__ req_bad,
                                                      const uint8_t* __restrict__ mflag, uint32_t* __restrict__ out);

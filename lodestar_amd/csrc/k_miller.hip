@@ -74,6 +74,22 @@ LB_DEV void acc_lines(fp12& f, const uint32_t* __restrict__ lines, uint32_t n_pa
   }
 }
 
+// Miller(-g1, S) with its lines computed on the fly (one lane); out of line so
+// the accumulation loop of k_miller_acc keeps its own register allocation
+__device__ __noinline__ void miller_neg_g1(fp12* __restrict__ out, const g2a* __restrict__ S) {
+  fp12 r;
+  fp12_one(r);
+  const g2a q = *S;
+  if (!q.inf) {
+    g1a g;
+    fp_set(g.x, LB_G1_X);
+    fp_set(g.y, LB_G1_NEG_Y);
+    g.inf = false;
+    miller_loop(r, g, q);
+  }
+  *out = r;
+}
+
 // Per request k: F_k = f_S[k] * prod_{i in request} Miller(r_i pk_i, H_i), from
 // the stored lines.  LB_ACC_LPR lanes per request (64 / LB_ACC_LPR requests per
 // wave); lane l accumulates the set pairs a + l, a + l + LPR, ... into ONE f,
@@ -83,6 +99,10 @@ LB_DEV void acc_lines(fp12& f, const uint32_t* __restrict__ lines, uint32_t n_pa
 // halves != 0: the "requests" are the halves of the call's requests (a lone call
 // on an idle GPU runs twice as many waves, k_split_requests / k_join_halves); an
 // empty half is then not a false verdict.
+// Sx != nullptr: one extra (last) workgroup computes Fx = Miller(-g1, Sx) for
+// the merged check, alongside the per-request waves (its sum S_all came from
+// the bucket MSM before this launch), so neither the lines of that pair nor
+// their wave-cooperative Miller value sit on the call's serial tail.
 template <int LPR>
 __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                                     uint32_t n_pairs, const uint32_t* __restrict__ lines,
@@ -90,8 +110,13 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
                                                                     const uint8_t* __restrict__ sig_status,
                                                                     const uint8_t* __restrict__ pk_status,
                                                                     fp12* __restrict__ F, uint8_t* __restrict__ req_bad,
-                                                                    uint8_t* __restrict__ req_err, uint32_t halves) {
+                                                                    uint8_t* __restrict__ req_err, uint32_t halves,
+                                                                    const g2a* __restrict__ Sx, fp12* __restrict__ Fx) {
   constexpr uint32_t RPW = TPB / LPR;  // requests per workgroup
+  if (Sx && blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x == 0) miller_neg_g1(Fx, Sx);
+    return;
+  }
   __shared__ fp12 sh[TPB];
   __shared__ uint32_t bad[RPW], err_empty[RPW], err_pk[RPW];
   const uint32_t sub = threadIdx.x / LPR, lane = threadIdx.x % LPR;
@@ -191,7 +216,8 @@ LB_INST_LINES(2)
   template __global__ void k_miller_acc<L>(uint32_t, const uint32_t* __restrict__, uint32_t,                    \
                                            const uint32_t* __restrict__, const fp12* __restrict__,              \
                                            const uint8_t* __restrict__, const uint8_t* __restrict__,            \
-                                           fp12* __restrict__, uint8_t* __restrict__, uint8_t* __restrict__, uint32_t);
+                                           fp12* __restrict__, uint8_t* __restrict__, uint8_t* __restrict__, uint32_t, \
+                                           const g2a* __restrict__, fp12* __restrict__);
 LB_INST_ACC(64)
 LB_INST_ACC(32)
 LB_INST_ACC(16)

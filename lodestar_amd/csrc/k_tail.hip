@@ -24,6 +24,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_lines_S(uint32_t n_req, uint
 }
 
 // one workgroup (one wave) per request: valid[k] = final_exp(F_k * Miller(-g1, S_k)) == 1.
+// lines == nullptr: F_k already holds the Miller(-g1, S) factor (the merged
+// check folded into k_miller_acc): valid[k] = final_exp(F_k) == 1.
 // skip (optional): nonzero when the merged check of the whole call passed ->
 // valid[k] = !req_bad[k] without any arithmetic.
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_t n_pairs, uint32_t base,
@@ -41,9 +43,9 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_tail(uint32_t n_req, uint32_
   }
   wc_init_tables(S);
   wc_init_gammas(S);
-  wc_miller_from_lines(S, WC_FS, lines, n_pairs, (size_t)base + k);
+  if (lines) wc_miller_from_lines(S, WC_FS, lines, n_pairs, (size_t)base + k);
   wc_load12(S, WC_F, F[k]);
-  wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
+  if (lines) wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
   wc_final_exp(S, WC_F, WC_F);
   if (threadIdx.x == 0) valid[k] = wc_is_one(S, WC_F) ? 1 : 0;
 }
@@ -64,6 +66,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t
 // Merged check of a whole call (the worker's merged batch, worker.ts:41-96):
 // S_all = sum S_k and F_all = prod F_k over the requests not already false.
 // S == nullptr: S_all already came from the bucket MSM (k_msm_final); only F_all.
+// Fx != nullptr: Miller(-g1, S_all) computed by k_miller_acc, multiplied in.
 // One wave; the tail kernel then verifies (F_all, S_all) once, and the
 // per-request tails only run if that merged check fails.
 // The worker's bookkeeping of its merged batch (worker.ts:66-85): batchRetries
@@ -97,9 +100,9 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_partial(uint32_t n_pairs, ui
                                                           const fp12* __restrict__ F_all, uint8_t* __restrict__ out576) {
   __shared__ wc_smem S;
   wc_init_tables(S);
-  wc_miller_from_lines(S, WC_FS, lines, n_pairs, base);
+  if (lines) wc_miller_from_lines(S, WC_FS, lines, n_pairs, base);  // (nullptr: F_all holds the factor)
   wc_load12(S, WC_F, F_all[0]);
-  wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
+  if (lines) wc_apply(S, LB_WC_MUL, WC_F, WC_F, WC_FS);
   if (threadIdx.x < 12) fp_write_be(out576 + 48 * threadIdx.x, S.slot[WC_F][threadIdx.x]);
 }
 
@@ -137,13 +140,15 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_check(uint32_t n, const u
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,
-                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all) {
+                                                        g2a* __restrict__ S_all, fp12* __restrict__ F_all,
+                                                        const fp12* __restrict__ Fx) {
   __shared__ g2j shs[TPB];
   __shared__ fp12 shf[TPB];
   g2j acc;
   jac_set_inf(acc);
   fp12 f;
   fp12_one(f);
+  if (Fx && threadIdx.x == 0) f = Fx[0];
   for (uint32_t k = threadIdx.x; k < n_req; k += TPB) {
     if (req_bad[k]) continue;
     if (S) {

@@ -332,10 +332,16 @@ void worker_loop(Context* c) {
         b.seed = t->seed.data();
         t->valid.assign(t->n_sets ? t->n_sets : 1, 0);
         t->job_fast.assign(t->n_jobs ? t->n_jobs : 1, 0);
-        const int rc = lb_verify_same_message_batch(c->ctx, &b, t->valid.data(), t->job_fast.data(), &t->stats);
-        if (rc != LB_OK) fail(t, rc, c->ctx);
-        t->t_end = now_ns();
-        complete(c, t);
+        // in flight like a verify call (the package's per-set retries run when it retires)
+        const int rc =
+            lb_verify_same_message_batch_async(c->ctx, &b, t->valid.data(), t->job_fast.data(), &t->ticket);
+        if (rc != LB_OK) {
+          fail(t, rc, c->ctx);
+          t->t_end = now_ns();
+          complete(c, t);
+        } else {
+          inflight.push_back(t);
+        }
         break;
       }
       case Kind::SyncPubkeys: {

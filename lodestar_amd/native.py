@@ -33,7 +33,7 @@ SET_STATUS_NAMES = {0: "OK", 1: "BAD_ENCODING", 2: "NOT_ON_CURVE", 3: "NOT_IN_GR
 EXPORTED_SYMBOLS = (
     "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
-    "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul", "lb_g2_msm",
+    "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul", "lb_g2_msm", "lb_verify_same_message_batch_async",
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
     "lb_pubkey_table_append", "lb_pubkey_table_size", "lb_pubkey_table_read", "lb_pubkey_table_truncate",
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
@@ -153,6 +153,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_verify_requests_finish.argtypes = [vp, ctypes.c_uint64, i32]
     lib.lb_verify_same_message_batch.argtypes = [vp, ctypes.POINTER(_SameMessageBatch), vp, vp,
                                                  ctypes.POINTER(_Stats)]
+    lib.lb_verify_same_message_batch_async.argtypes = [vp, ctypes.POINTER(_SameMessageBatch), vp, vp,
+                                                       ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_sk_to_pk.argtypes = [vp, u32, vp, vp]
     lib.lb_pubkey_table_append.argtypes = [vp, u32, vp, u32, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_pubkeys_from_bytes.argtypes = [vp, u32, vp, u32, vp, vp]
@@ -218,6 +220,18 @@ class PendingCall:
     sst: np.ndarray
     keep: object
     partial: bool = False
+
+
+@dataclass
+class PendingSameMessage:
+    """An enqueued same-message package: its ticket, the verdict / fast-path arrays
+    the library fills when it retires, and the inputs it reads until then."""
+    ticket: int
+    n_jobs: int
+    out: np.ndarray
+    fast: np.ndarray
+    job_off: np.ndarray
+    keep: object
 
 
 class Device:
@@ -341,15 +355,10 @@ class Device:
         self._check(self.lib.lb_gt_check(self._h, len(partials), _ptr(blob), ctypes.byref(out)), "lb_gt_check")
         return bool(out.value)
 
-    def verify_same_message_batch(self, jobs: Sequence[Tuple[Sequence, Sequence[bytes], bytes]], seed: bytes,
-                                  by_index: bool = False) -> Tuple[List[List[bool]], List[bool], Tuple[int, int]]:
-        """jobs: (pubkeys, signatures, message) per same-message job; pubkeys are
-        96-byte encodings, or validator indices when by_index.  Returns per-set
-        verdicts per job, the per-job fast-path flags and (retried jobs, sets
-        verified by a passing aggregate)."""
+    def _same_message_batch(self, jobs, seed: bytes, by_index: bool):
+        """The lb_same_message_batch of a package, its output arrays and the
+        input arrays the library reads (kept alive until the call retires)."""
         nj = len(jobs)
-        if nj == 0:
-            return [], [], (0, 0)
         job_off = np.zeros(nj + 1, np.uint32)
         for j, (pks, sigs, msg) in enumerate(jobs):
             if len(pks) != len(sigs):
@@ -371,14 +380,68 @@ class Device:
         b = _SameMessageBatch(nj, ns, _ptr(job_off), _ptr(pk), _ptr(idx), _ptr(blob), _ptr(offs), _ptr(msgs),
                               _ptr(sd))
         out = np.zeros(max(ns, 1), np.uint8)
-        fast = np.zeros(nj, np.uint8)
-        st = _Stats()
-        rc = self.lib.lb_verify_same_message_batch(self._h, ctypes.byref(b), _ptr(out), _ptr(fast), ctypes.byref(st))
-        self._check(rc, "lb_verify_same_message_batch")
+        fast = np.zeros(max(nj, 1), np.uint8)
+        return b, out, fast, job_off, (job_off, pk, idx, blob, offs, msgs, sd)
+
+    @staticmethod
+    def _same_message_result(out, fast, job_off, nj, st):
+        ns = int(job_off[-1])
         flat = out[:ns].astype(bool).tolist()
         bounds = job_off.tolist()
         res = [flat[bounds[j]:bounds[j + 1]] for j in range(nj)]
-        return res, fast.astype(bool).tolist(), (int(st.batch_retries), int(st.batch_sigs_success))
+        return res, fast[:nj].astype(bool).tolist(), (int(st.batch_retries), int(st.batch_sigs_success))
+
+    def verify_same_message_batch(self, jobs: Sequence[Tuple[Sequence, Sequence[bytes], bytes]], seed: bytes,
+                                  by_index: bool = False) -> Tuple[List[List[bool]], List[bool], Tuple[int, int]]:
+        """jobs: (pubkeys, signatures, message) per same-message job; pubkeys are
+        96-byte encodings, or validator indices when by_index.  Returns per-set
+        verdicts per job, the per-job fast-path flags and (retried jobs, sets
+        verified by a passing aggregate)."""
+        nj = len(jobs)
+        if nj == 0:
+            return [], [], (0, 0)
+        b, out, fast, job_off, keep = self._same_message_batch(jobs, seed, by_index)
+        st = _Stats()
+        rc = self.lib.lb_verify_same_message_batch(self._h, ctypes.byref(b), _ptr(out), _ptr(fast), ctypes.byref(st))
+        self._check(rc, "lb_verify_same_message_batch")
+        del keep
+        return self._same_message_result(out, fast, job_off, nj, st)
+
+    def verify_same_message_batch_async(self, jobs: Sequence[Tuple[Sequence, Sequence[bytes], bytes]], seed: bytes,
+                                        by_index: bool = False) -> "PendingSameMessage":
+        """lb_verify_same_message_batch_async: enqueue the package on the next slot of
+        the ring of calls in flight and return at once; wait_same_message() gives
+        what verify_same_message_batch returns."""
+        nj = len(jobs)
+        b, out, fast, job_off, keep = self._same_message_batch(jobs, seed, by_index) if nj else (
+            _SameMessageBatch(0, 0, None, None, None, None, None, None, None), np.zeros(1, np.uint8),
+            np.zeros(1, np.uint8), np.zeros(1, np.uint32), None)
+        t = ctypes.c_uint64(0)
+        rc = self.lib.lb_verify_same_message_batch_async(self._h, ctypes.byref(b), _ptr(out), _ptr(fast),
+                                                         ctypes.byref(t))
+        self._check(rc, "lb_verify_same_message_batch_async")
+        return PendingSameMessage(int(t.value), nj, out, fast, job_off, keep)
+
+    def prepare_same_message(self, jobs, seed: bytes, by_index: bool = False):
+        """A package packed once (bench: the same package resubmitted without re-packing)."""
+        return (len(jobs),) + self._same_message_batch(jobs, seed, by_index)
+
+    def verify_same_message_prepared_async(self, prep) -> "PendingSameMessage":
+        nj, b, _, _, job_off, keep = prep
+        out = np.zeros(max(int(job_off[-1]), 1), np.uint8)
+        fast = np.zeros(max(nj, 1), np.uint8)
+        t = ctypes.c_uint64(0)
+        rc = self.lib.lb_verify_same_message_batch_async(self._h, ctypes.byref(b), _ptr(out), _ptr(fast),
+                                                         ctypes.byref(t))
+        self._check(rc, "lb_verify_same_message_batch_async")
+        return PendingSameMessage(int(t.value), nj, out, fast, job_off, keep)
+
+    def wait_same_message(self, pc: "PendingSameMessage"):
+        st = _Stats()
+        self._check(self.lib.lb_wait(self._h, pc.ticket, ctypes.byref(st)), "lb_wait")
+        pc.keep = None
+        res = self._same_message_result(pc.out, pc.fast, pc.job_off, pc.n_jobs, st)
+        return res + (float(st.device_ms),)
 
     def verify_requests_device(self, n_req: int, n_sets: int, d_req_off: int, d_pubkeys: int, d_pk_off: Optional[int],
                                d_msgs: int, d_sigs: int, d_sig_off: int, d_seed: int, d_valid: int, d_err: int,

@@ -39,7 +39,7 @@ from typing import Callable, Deque, List, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from . import metrics as M
-from .native import (LB_PK_ROW_FLAG, LB_REQ_BAD_PUBKEY, LB_REQ_EMPTY_AGGREGATE, BadPubkeyError, Device, EmptyAggregateError,
+from .native import (LB_PK_ROW_FLAG, PendingSameMessage, LB_REQ_BAD_PUBKEY, LB_REQ_EMPTY_AGGREGATE, BadPubkeyError, Device, EmptyAggregateError,
                      pack_blobs)
 
 MAX_SIGNATURE_SETS_PER_JOB = 128      # index.ts:57
@@ -244,6 +244,11 @@ class DeviceBackend:
                         self._partials = max(0, self._partials - 1)
                         self.dev.verify_finish(call.pc, ok)
                         inflight.append((call.pc, fut, call.post, call.stats))
+                    elif kind == "same_message":
+                        # one package of same-message jobs, in flight like any call: its
+                        # per-set retries run when it retires, on its own slot
+                        pc, post = self._submit_same_message(payload)
+                        inflight.append((pc, fut, post, cs))
                     else:  # synchronous library calls (same-message batch, table sync, gt check, ...)
                         fut.set_result(payload(cs))
                 except BaseException as e:  # noqa: BLE001 -- surfaced through the future
@@ -251,6 +256,13 @@ class DeviceBackend:
                 continue
             pc, fut, post, cs = inflight.popleft()
             try:
+                if isinstance(pc, PendingSameMessage):
+                    res, fast, (retried, ok_sets), dev_ms = self.dev.wait_same_message(pc)
+                    cs.batch_retries, cs.batch_sigs_success, cs.device_ms = retried, ok_sets, dev_ms
+                    cs.stage_ms = dict(self.dev.last_stage_times())
+                    cs.t_end = time.monotonic()
+                    fut.set_result((res, fast, cs))
+                    continue
                 res = self.dev.wait_call(pc)
                 cs.batch_retries, cs.batch_sigs_success, cs.device_ms = (res.batch_retries, res.batch_sigs_success,
                                                                          res.device_ms)
@@ -329,21 +341,18 @@ class DeviceBackend:
     def gt_check(self, partials: Sequence[bytes]) -> concurrent.futures.Future:
         return self._put("call", lambda cs: self.dev.gt_check(list(partials)), front=True)
 
+    def _submit_same_message(self, jobs):
+        by_index = all(k.index is not None for pks, _, _ in jobs for k in pks)
+        dj = [([k.index for k in pks] if by_index else self._key_bytes(pks), list(sigs), bytes(msg))
+              for pks, sigs, msg in jobs]
+        return self.dev.verify_same_message_batch_async(dj, self.seed_source(), by_index=by_index), None
+
     def submit_same_message(self, jobs: Sequence[Tuple[Sequence[PublicKey], Sequence[bytes], bytes]],
                             priority: bool = False) -> concurrent.futures.Future:
         """Future of (per-job verdict lists, per-job fast flags, CallStats): all
-        same-message jobs of a package in one device call."""
-        def run(cs: CallStats):
-            by_index = all(k.index is not None for pks, _, _ in jobs for k in pks)
-            dj = [([k.index for k in pks] if by_index else self._key_bytes(pks), list(sigs), bytes(msg))
-                  for pks, sigs, msg in jobs]
-            res, fast, (retried, ok_sets) = self.dev.verify_same_message_batch(dj, self.seed_source(),
-                                                                                by_index=by_index)
-            cs.batch_retries, cs.batch_sigs_success = retried, ok_sets
-            cs.stage_ms = dict(self.dev.last_stage_times())
-            cs.t_end = time.monotonic()
-            return res, fast, cs
-        return self._put("call", run, front=priority)
+        same-message jobs of a package in one device call, kept in flight beside
+        the other packages (lb_verify_same_message_batch_async)."""
+        return self._put("same_message", list(jobs), front=priority)
 
     def verify_requests(self, requests: List[List[SignatureSet]]) -> Tuple[List[bool], List[int]]:
         """Blocking convenience (tests, ShardedVerifier without the combine)."""

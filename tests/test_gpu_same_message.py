@@ -156,3 +156,66 @@ def test_pool_same_message_jobs_share_one_device_call(keyed):
     outs, calls = asyncio.run(main())
     assert outs == expect
     assert calls == [6]
+
+
+def test_same_message_async_packages_in_flight(keyed):
+    """lb_verify_same_message_batch_async: four packages (two with corrupted sets, whose
+    failed jobs are re-verified set by set when the package retires, on its own slot)
+    in flight beside a default-request call, retired out of order; verdicts, fast-path
+    flags and retry counts as by construction, and one package's sets re-verified alone
+    by the C oracle."""
+    from lodestar_amd.native import pack_blobs
+    from oracle import c_oracle as C
+    dev, keys = keyed
+    pkgs = [W.same_message_jobs(dev, keys, n_jobs=64, per_job=32, seed=20 + k, n_invalid=(0, 7, 0, 3)[k])
+            for k in range(4)]
+    pend = [dev.verify_same_message_batch_async(jobs, bytes([k]) * 32, by_index=True)
+            for k, (jobs, _) in enumerate(pkgs)]
+    # a default-request call in flight between them
+    jobs0 = pkgs[0][0]
+    flat = [(keys.pks[i], s, m) for ix, sigs, m in jobs0[:8] for i, s in zip(ix, sigs)]
+    blob, offs = pack_blobs([s for _, s, _ in flat])
+    n = len(flat)
+    pc = dev.verify_requests_async(np.arange(0, n + 1, 32, dtype=np.uint32),
+                                   np.frombuffer(b"".join(p for p, _, _ in flat), np.uint8), None,
+                                   np.frombuffer(b"".join(m for _, _, m in flat), np.uint8), blob, offs, bytes(32))
+    for k in (2, 0, 3, 1):
+        res, fast, (retried, ok_sets), _ = dev.wait_same_message(pend[k])
+        jobs, expect = pkgs[k]
+        assert res == expect, k
+        bad = {j for j, e in enumerate(expect) if not all(e)}
+        assert [not f for f in fast] == [j in bad for j in range(len(jobs))]
+        assert retried == len(bad) and ok_sets == sum(len(e) for j, e in enumerate(expect) if j not in bad)
+    assert list(dev.wait_call(pc).valid) == [1] * 8
+    # package 1 (7 corrupted sets) set by set against the C oracle
+    jobs, expect = pkgs[1]
+    flat = [(keys.pks[i], s, m) for ix, sigs, m in jobs for i, s in zip(ix, sigs)]
+    blob, offs = pack_blobs([s for _, s, _ in flat])
+    n = len(flat)
+    valid, _ = C.verify_requests(np.arange(n + 1, dtype=np.uint32), np.frombuffer(b"".join(p for p, _, _ in flat),
+                                                                                 np.uint8),
+                                 None, np.frombuffer(b"".join(m for _, _, m in flat), np.uint8), blob, offs,
+                                 bytes(32), threads=16)
+    assert [bool(x) for x in valid] == [v for e in expect for v in e]
+
+
+def test_same_message_async_edge_jobs_bytes(keyed):
+    """The edge jobs of test_same_message_edge_jobs through the async entry with 96-byte
+    pubkeys (phase-2 keys are rows of the package's own key bytes), plus an
+    infinite signature in a 1-set job (core verify rejects it in phase 2)."""
+    dev, keys = keyed
+    root = hashlib.sha256(b"edge-async").digest()
+    s = W.sign_many(dev, keys.sks[:4], [root] * 4)
+    d = O.g2_mul(O.G2, 7919)
+    s0 = O.g2_to_bytes(O.E2.add(O.signature_from_bytes(s[0]), d))
+    s1 = O.g2_to_bytes(O.E2.add(O.signature_from_bytes(s[1]), O.E2.neg(d)))
+    inf = bytes([0xC0]) + bytes(95)
+    pk = keys.pks
+    jobs = [([pk[0], pk[1]], [s[0], s[1]], root), ([], [], root), ([pk[2]], [s[2]], root),
+            ([pk[3]], [bytes([10]) * 96], root), ([pk[0], pk[1]], [s0, s1], root), ([pk[2]], [inf], root),
+            ([pk[3], pk[2]], [s[3], s0], root)]
+    p = dev.verify_same_message_batch_async(jobs, bytes(32))
+    res, fast, (retried, ok_sets), _ = dev.wait_same_message(p)
+    assert res == [[True, True], [], [True], [False], [True, True], [False], [True, False]]
+    assert fast == [True, False, True, False, True, False, False]
+    assert retried == 3 and ok_sets == 5

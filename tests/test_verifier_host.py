@@ -238,6 +238,20 @@ class FakeDev:
         self.active -= 1
         return VerifyResult(pc.valid[:pc.n_req], pc.err[:pc.n_req], np.zeros(0, np.uint8), 0.0)
 
+    def verify_same_message_batch_async(self, jobs, seed, by_index=False):
+        import numpy as np
+        from lodestar_amd.native import PendingSameMessage
+        assert not self.closed, "call on a destroyed context"
+        self.active += 1
+        return PendingSameMessage(0, len(jobs), None, None, np.zeros(1, np.uint32), list(jobs))
+
+    def wait_same_message(self, pc):
+        assert not self.closed, "wait on a destroyed context"
+        self.active -= 1
+        jobs = pc.keep
+        return ([[True] * len(s) for _, s, _ in jobs], [True] * len(jobs), (0, sum(len(s) for _, s, _ in jobs)),
+                0.0)
+
     def last_stage_times(self):
         return [("pubkeys_agg", 0.5)]
 
@@ -385,8 +399,11 @@ class SlotDev(FakeDev):
         self.pending -= 1
         self.active += 1
 
-    def verify_same_message_batch(self, jobs, seed, by_index=False):
-        return [[True] * len(s) for _, s, _ in jobs], [True] * len(jobs), (0, sum(len(s) for _, s, _ in jobs))
+    def verify_same_message_batch_async(self, jobs, seed, by_index=False):
+        assert self.active + self.pending < self.slots, "a slot holding a pending partial was reused"
+        pc = super().verify_same_message_batch_async(jobs, seed, by_index)
+        self.max_used = max(self.max_used, self.active + self.pending)
+        return pc
 
 
 def test_partial_call_holds_its_slot_until_finished():
