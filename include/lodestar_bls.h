@@ -81,6 +81,10 @@ int lb_create(int device, lb_ctx** out_ctx);
 int lb_destroy(lb_ctx* ctx);
 /* Human-readable message for the last error on this context (never NULL). */
 const char* lb_last_error(const lb_ctx* ctx);
+/* Calls the context keeps in flight on the async entry points (one per HIP hardware
+ * queue of the process: GPU_MAX_HW_QUEUES, 4 by default, up to 16; LB_SLOTS overrides):
+ * the capacity a host keeps busy (the pool's worker count, multithread/index.ts:47). */
+int lb_slots(const lb_ctx* ctx);
 /* Number of visible HIP devices (0 when none). */
 int lb_device_count(void);
 

@@ -142,9 +142,9 @@ struct lb_ctx {
   // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
   // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
   // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
-  static constexpr int kMaxSlots = 8;
+  static constexpr int kMaxSlots = 16;
   int n_slots = 4;
-  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1, 1, 1, 1, 1};
+  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
   Slot slots[kMaxSlots];
   int next_slot = 0;
   uint64_t next_ticket = 1;
@@ -744,9 +744,13 @@ int lb_create(int device, lb_ctx** out_ctx) {
   ctx->device = device;
   bool ok = hipSetDevice(device) == hipSuccess;
   // one single-stream slot per hardware queue HIP gives this process (4 by
-  // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8
-  // calls in flight -- within run-to-run noise of 4 on MI355X, profiles/ab_r01i.txt)
-  if (const char* e = getenv("GPU_MAX_HW_QUEUES")) ctx->n_slots = atoi(e) >= 8 ? 8 : 4;
+  // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8 calls
+  // in flight: 2.94 vs 2.74 M sets/s once the merged check's one-wave kernels
+  // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 16)
+  if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
+    const int v = atoi(e);
+    ctx->n_slots = v < 4 ? 4 : v > lb_ctx::kMaxSlots ? lb_ctx::kMaxSlots : v;
+  }
   if (const char* e = getenv("LB_SLOTS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
@@ -842,6 +846,8 @@ int lb_destroy(lb_ctx* ctx) {
 }
 
 const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int lb_slots(const lb_ctx* ctx) { return ctx ? ctx->n_slots : 0; }
 
 #ifdef LB_COUNT_OPS
 // Fp products executed per stage of the last completed verify call (count build only)

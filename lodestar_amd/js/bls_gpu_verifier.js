@@ -272,7 +272,8 @@ class BlsGpuVerifier {
     if (o.backends) this.backends = o.backends;
     else {
       const addon = loadAddon();
-      this.backends = (o.devices || [0]).map((d) => new addon.Context(d, {capacity: o.capacity || 4}));
+      // capacity: the library's calls in flight per GPU (lb_slots) unless given
+      this.backends = (o.devices || [0]).map((d) => new addon.Context(d, o.capacity ? {capacity: o.capacity} : {}));
     }
     if (this.backends.length === 0) throw new Error("at least one GPU backend is required");
     this.blsVerifyAllMultiThread = Boolean(o.blsVerifyAllMultiThread);
@@ -585,14 +586,52 @@ function shardRequests(sizes, nShards) {
  * A shard that fails in phase 1 fails the call after the others are resumed.
  * Returns {valid, errors, mergedOk}. */
 async function verifyRequestsSharded(backends, requests, seedSource) {
-  const shards = shardRequests(
+  return combineShards(
+    backends,
     requests.map((r) => r.length),
-    backends.length
-  )
+    (lo, hi) => packRequests(requests.slice(lo, hi), seedSource())
+  );
+}
+
+/** Requests [lo, hi) of a packed call ({requestOffsets, pkOffsets, pubkeyIndices |
+ * pubkeys, messages, signatures, sigOffsets}) as a call of their own, offsets rebased. */
+function slicePacked(p, lo, hi, seed) {
+  const a = p.requestOffsets[lo];
+  const b = p.requestOffsets[hi];
+  const ka = p.pkOffsets[a];
+  const kb = p.pkOffsets[b];
+  const sa = p.sigOffsets[a];
+  const sb = p.sigOffsets[b];
+  const rebase = (arr, x, y, base) => Uint32Array.from(arr.subarray(x, y), (v) => v - base);
+  const out = {
+    requestOffsets: rebase(p.requestOffsets, lo, hi + 1, a),
+    pkOffsets: rebase(p.pkOffsets, a, b + 1, ka),
+    messages: p.messages.subarray(32 * a, 32 * b),
+    signatures: p.signatures.subarray(sa, sb),
+    sigOffsets: rebase(p.sigOffsets, a, b + 1, sa),
+    seed,
+  };
+  if (p.pubkeyIndices) out.pubkeyIndices = p.pubkeyIndices.subarray(ka, kb);
+  else out.pubkeys = p.pubkeys.subarray(96 * ka, 96 * kb);
+  return out;
+}
+
+/** verifyRequestsSharded for a call already packed (a gossip replay of ~1M sets
+ * without one JS object per set or key). */
+async function verifyPackedSharded(backends, packed, seedSource) {
+  const nReq = packed.requestOffsets.length - 1;
+  const sizes = [];
+  for (let k = 0; k < nReq; k++) sizes.push(packed.requestOffsets[k + 1] - packed.requestOffsets[k]);
+  return combineShards(backends, sizes, (lo, hi) => slicePacked(packed, lo, hi, seedSource()));
+}
+
+async function combineShards(backends, sizes, packShard) {
+  const nReq = sizes.length;
+  const shards = shardRequests(sizes, backends.length)
     .map(([lo, hi], g) => [lo, hi, g])
     .filter(([lo, hi]) => hi > lo);
   const settled = await Promise.allSettled(
-    shards.map(([lo, hi, g]) => backends[g].verifyRequestsPartial(packRequests(requests.slice(lo, hi), seedSource())))
+    shards.map(([lo, hi, g]) => backends[g].verifyRequestsPartial(packShard(lo, hi)))
   );
   const failed = settled.find((x) => x.status === "rejected");
   if (failed) {
@@ -612,8 +651,8 @@ async function verifyRequestsSharded(backends, requests, seedSource) {
   });
   const mergedOk = calls.length === 0 ? true : await backends[shards[big][2]].gtCheck(partials);
   const res = await Promise.all(calls.map((c, i) => backends[shards[i][2]].finish(c.id, mergedOk)));
-  const valid = new Uint8Array(requests.length);
-  const errors = new Uint8Array(requests.length);
+  const valid = new Uint8Array(nReq);
+  const errors = new Uint8Array(nReq);
   shards.forEach(([lo], g) => {
     valid.set(res[g].valid, lo);
     errors.set(res[g].errors, lo);
@@ -633,7 +672,9 @@ module.exports = {
   packRequests,
   packSameMessage,
   shardRequests,
+  slicePacked,
   verifyRequestsSharded,
+  verifyPackedSharded,
   loadAddon,
   MAX_SIGNATURE_SETS_PER_JOB,
   MAX_BUFFERED_SIGS,

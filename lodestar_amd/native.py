@@ -31,7 +31,7 @@ SET_STATUS_NAMES = {0: "OK", 1: "BAD_ENCODING", 2: "NOT_ON_CURVE", 3: "NOT_IN_GR
 
 # Every symbol include/lodestar_bls.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = (
-    "lb_create", "lb_destroy", "lb_last_error", "lb_device_count", "lb_verify_requests",
+    "lb_create", "lb_destroy", "lb_last_error", "lb_slots", "lb_device_count", "lb_verify_requests",
     "lb_verify_requests_device", "lb_verify_same_message", "lb_aggregate_pubkeys", "lb_aggregate_signatures",
     "lb_hash_to_g2", "lb_decode_signatures", "lb_pairing", "lb_batch_scalars", "lb_g1_mul", "lb_g2_mul", "lb_g2_msm", "lb_verify_same_message_batch_async",
     "lb_last_stage_times", "lb_sk_to_pk", "lb_sign", "lb_verify_requests_device_async", "lb_wait",
@@ -128,6 +128,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_destroy.argtypes = [vp]
     lib.lb_last_error.argtypes = [vp]
     lib.lb_last_error.restype = ctypes.c_char_p
+    lib.lb_slots.argtypes = [vp]
     lib.lb_device_count.argtypes = []
     lib.lb_verify_requests.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
     lib.lb_verify_requests_device.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
@@ -247,6 +248,10 @@ class Device:
         self.device = device
 
     # -- lifecycle ---------------------------------------------------------
+    def slots(self) -> int:
+        """Calls the library keeps in flight (lb_slots: one per HIP hardware queue)."""
+        return int(self.lib.lb_slots(self._h))
+
     def close(self) -> None:
         if self._h:
             self.lib.lb_destroy(self._h)

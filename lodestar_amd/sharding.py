@@ -21,6 +21,7 @@ RCCL over xGMI is not used: per GPU the exchange is 576 bytes.
 from __future__ import annotations
 
 import threading
+from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -53,6 +54,40 @@ def slice_requests(requests: Sequence, lo: int, hi: int) -> list:
     return list(requests[lo:hi])
 
 
+@dataclass
+class PackedRequests:
+    """Requests already in the C-ABI layout (lb_request_batch): the shape a gossip
+    replay of ~1 M sets takes without one Python object per set or per key.
+    ``idx`` holds validator indices (device pubkey table) when not None, else
+    ``pks`` the 96-byte keys; ``msgs`` is n_sets x 32 bytes."""
+    req_off: np.ndarray
+    pk_off: np.ndarray
+    msgs: np.ndarray
+    sig_blob: np.ndarray
+    sig_off: np.ndarray
+    idx: Optional[np.ndarray] = None
+    pks: Optional[np.ndarray] = None
+
+    @property
+    def n_req(self) -> int:
+        return len(self.req_off) - 1
+
+    def request_sizes(self) -> np.ndarray:
+        return np.diff(self.req_off.astype(np.int64))
+
+    def slice(self, lo: int, hi: int) -> "PackedRequests":
+        """Requests [lo, hi) as a call of their own (offsets rebased)."""
+        a, b = int(self.req_off[lo]), int(self.req_off[hi])
+        ka, kb = int(self.pk_off[a]), int(self.pk_off[b])
+        sa, sb = int(self.sig_off[a]), int(self.sig_off[b])
+        return PackedRequests(
+            (self.req_off[lo:hi + 1] - a).astype(np.uint32), (self.pk_off[a:b + 1] - ka).astype(np.uint32),
+            self.msgs[32 * a:32 * b], self.sig_blob[sa:sb] if sb > sa else np.zeros(1, np.uint8),
+            (self.sig_off[a:b + 1] - sa).astype(np.uint32),
+            None if self.idx is None else self.idx[ka:kb],
+            None if self.pks is None else self.pks[96 * ka:96 * kb])
+
+
 def _two_phase(backend) -> bool:
     return all(hasattr(backend, a) for a in ("submit_requests", "finish", "gt_check"))
 
@@ -72,6 +107,14 @@ class ShardedVerifier:
         self.backends = list(backends)
         self.combine = combine and all(_two_phase(b) for b in self.backends)
         self.last_combine: Optional[dict] = None
+
+    def verify_packed(self, p: PackedRequests) -> Tuple[List[bool], List[int]]:
+        """verify_requests for requests already packed (PackedRequests): each shard's
+        slice goes to its backend's submit_packed; the same two-phase combine."""
+        shards = shard_requests(p.request_sizes().tolist(), len(self.backends))
+        if not self.combine:
+            raise ValueError("verify_packed needs two-phase backends (DeviceBackend)")
+        return self._verify_combined(p, shards, packed=True)
 
     def verify_requests(self, requests: Sequence) -> Tuple[List[bool], List[int]]:
         shards = shard_requests([len(r) for r in requests], len(self.backends))
@@ -99,10 +142,11 @@ class ShardedVerifier:
             raise errors[0]
         return out_valid, out_err
 
-    def _verify_combined(self, requests, shards):
+    def _verify_combined(self, requests, shards, packed: bool = False):
         live = [(g, lo, hi) for g, (lo, hi) in enumerate(shards) if hi > lo]
         # phase 1: every GPU runs its shard up to the merged Miller product
-        futs = [(g, lo, hi, self.backends[g].submit_requests(list(requests[lo:hi]), partial=True))
+        futs = [(g, lo, hi, self.backends[g].submit_packed(requests.slice(lo, hi), partial=True) if packed else
+                 self.backends[g].submit_requests(list(requests[lo:hi]), partial=True))
                 for g, lo, hi in live]
         calls, errors = [], []
         for g, lo, hi, f in futs:
@@ -131,8 +175,9 @@ class ShardedVerifier:
         self.last_combine = {"merged_ok": ok, "n_partials": len(partials)}
         # phase 2: resume every shard with the combined verdict
         fins = [(lo, hi, c.backend.finish(c, ok)) for _, lo, hi, c in calls]
-        out_valid: List[bool] = [False] * len(requests)
-        out_err: List[int] = [0] * len(requests)
+        n = requests.n_req if packed else len(requests)
+        out_valid: List[bool] = [False] * n
+        out_err: List[int] = [0] * n
         for lo, hi, f in fins:
             v, e, _ = f.result()
             out_valid[lo:hi] = v

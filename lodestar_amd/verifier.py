@@ -183,7 +183,9 @@ class DeviceBackend:
         self.dev = dev if dev is not None else Device(device)  # dev: an injected stand-in (host tests)
         self.device = device
         self.seed_source = seed_source
-        self.capacity = capacity or max(1, int(os.environ.get("LB_SLOTS", "4")))
+        # the library's calls in flight (lb_slots: one per HIP hardware queue of the process)
+        self.capacity = capacity or (self.dev.slots() if hasattr(self.dev, "slots") else
+                                     max(1, int(os.environ.get("LB_SLOTS", "4"))))
         self._q: Deque[tuple] = deque()
         self._cv = threading.Condition()
         self._closing = False
@@ -225,9 +227,10 @@ class DeviceBackend:
                     continue
                 cs = CallStats(t_start=time.monotonic())
                 try:
-                    if kind == "requests":
+                    if kind in ("requests", "packed"):
                         requests, partial = payload
-                        pc, post = self._submit_requests(requests, partial)
+                        pc, post = (self._submit_requests(requests, partial) if kind == "requests" else
+                                    self._submit_packed(requests, partial))
                         if partial:
                             self._partials += 1
                             try:
@@ -314,6 +317,15 @@ class DeviceBackend:
             return [bool(v) for v in res.valid], [int(e) for e in res.errors], cs
         return pc, post
 
+    def _submit_packed(self, p, partial: bool):
+        pc = self.dev.verify_requests_async(p.req_off, p.pks if p.idx is None else None, p.pk_off, p.msgs,
+                                            p.sig_blob, p.sig_off, self.seed_source(), pk_indices=p.idx,
+                                            partial=partial)
+
+        def post(res, cs):
+            return [bool(v) for v in res.valid], [int(e) for e in res.errors], cs
+        return pc, post
+
     def _key_bytes(self, keys: Sequence[PublicKey]) -> List[bytes]:
         """96-byte encodings; index-only keys are read back from the device table
         (mixed packages only).  An index outside the table -> an all-zero
@@ -334,6 +346,11 @@ class DeviceBackend:
         """Future of (valid, errors, CallStats); with partial=True a PartialCall
         (the shard's 576-byte Fp12 partial, to be finished with finish())."""
         return self._put("requests", (list(requests), partial), front=priority)
+
+    def submit_packed(self, p, partial: bool = False, priority: bool = False) -> concurrent.futures.Future:
+        """submit_requests for requests already in the C-ABI layout
+        (sharding.PackedRequests): no per-set packing on the host."""
+        return self._put("packed", (p, partial), front=priority)
 
     def finish(self, call: "PartialCall", merged_ok: bool) -> concurrent.futures.Future:
         return self._put("finish", (call, merged_ok), front=True)

@@ -187,3 +187,30 @@ def test_verify_distributed_gloo_world2(two_phase):
             assert checks == (1 if rank == 0 else None)
         lo, hi = shards[rank]
         assert len(seen[0]) == hi - lo  # each rank verified only its own shard
+
+
+def test_packed_requests_slice_rebases_offsets():
+    """PackedRequests.slice(lo, hi): requests [lo, hi) as a call of their own."""
+    import numpy as np
+    from lodestar_amd.sharding import PackedRequests, shard_requests
+    rng = np.random.default_rng(1)
+    sizes = rng.integers(1, 6, 40)
+    req_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    n = int(req_off[-1])
+    keys_per_set = rng.integers(1, 4, n)
+    pk_off = np.concatenate([[0], np.cumsum(keys_per_set)]).astype(np.uint32)
+    idx = np.arange(int(pk_off[-1]), dtype=np.uint32) * 7
+    sig_len = rng.choice([96, 192], n)
+    sig_off = np.concatenate([[0], np.cumsum(sig_len)]).astype(np.uint32)
+    blob = (np.arange(int(sig_off[-1])) % 251).astype(np.uint8)
+    msgs = (np.arange(32 * n) % 253).astype(np.uint8)
+    p = PackedRequests(req_off, pk_off, msgs, blob, sig_off, idx=idx)
+    parts = [p.slice(lo, hi) for lo, hi in shard_requests(sizes.tolist(), 3)]
+    assert sum(q.n_req for q in parts) == 40
+    assert np.array_equal(np.concatenate([q.msgs for q in parts]), msgs)
+    assert np.array_equal(np.concatenate([q.idx for q in parts]), idx)
+    assert np.array_equal(np.concatenate([q.sig_blob for q in parts]), blob)
+    for q in parts:
+        assert q.req_off[0] == 0 and q.pk_off[0] == 0 and q.sig_off[0] == 0
+        assert int(q.sig_off[-1]) == len(q.sig_blob) and int(q.pk_off[-1]) == len(q.idx)
+        assert int(q.req_off[-1]) * 32 == len(q.msgs) == 32 * (len(q.sig_off) - 1)
