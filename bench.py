@@ -43,13 +43,14 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# HIP hardware queues per process (HIP's default is 4).  The library keeps one call in
-# flight per queue (lb_create: 8 slots when GPU_MAX_HW_QUEUES >= 8); each call's merged
-# check ends in one-wave kernels (MSM bit sums, final exponentiation) during which its
-# queue's share of the GPU idles, so 8 calls in flight fill the SIMDs better: 2.94-2.95
-# vs 2.74-2.75 M sets/s (profiles/ab_r03/hwq).  Set before HIP initialises (torch import);
-# a Lodestar process sets it the same way before loading the addon.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP hardware queues per process (HIP's default, and the box's environment, is 4).
+# The library keeps one call in flight per queue (lb_create: GPU_MAX_HW_QUEUES slots,
+# up to 16); each call's merged check ends in one-wave kernels (MSM bit sums, final
+# exponentiation) during which its queue's share of the GPU idles, so more calls in
+# flight fill the SIMDs better: 2.74 / 2.89 / 2.98 / 3.03 M sets/s at 4 / 8 / 12 / 16
+# (profiles/ab_r03/hwq, hwq2).  Set before HIP initialises (torch import); the N-API
+# addon does the same for a Lodestar process (LB_HW_QUEUES overrides both).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LB_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -150,8 +151,7 @@ def main():
     ap.add_argument("--combine", choices=["auto", "on", "off"], default="auto",
                     help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on for N > 1)")
     ap.add_argument("--inflight", type=int,
-                    default=int(os.environ.get("LB_SLOTS",
-                                               "8" if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 8 else "4")),
+                    default=int(os.environ.get("LB_SLOTS", min(16, max(4, int(os.environ["GPU_MAX_HW_QUEUES"]))))),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
     a = ap.parse_args()
 
@@ -313,6 +313,34 @@ def main():
             lat.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.median(lat)) if lat else None
     lat_stages = {name: round(ms, 3) for name, ms in dev.last_stage_times()} if lat else None
+    # p50 of ONE set (the verifyOnMainThread shape: a 1-set request, core verify,
+    # BN/chain/validation/block.ts:146) and of one 128-set request through the
+    # synchronous host-buffer entry point (numpy in, verdicts out, PCIe included)
+    lat1, lat_host = [], []
+    if a.latency_reps > 0:
+        d_req1 = torch.tensor([0, 1], dtype=torch.int32, device=cuda)
+
+        def one_set():
+            dev.verify_requests_device(1, 1, d_req1.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
+                                       d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
+                                       d_valid[0].data_ptr(), d_err[0].data_ptr())
+        pk_h = np.frombuffer(b"".join(pks[:a.per_request]), np.uint8)
+        mg_h = np.frombuffer(b"".join(msgs[:a.per_request]), np.uint8)
+        sg_h = np.frombuffer(b"".join(sigs[:a.per_request]), np.uint8)
+        ro_h = np.array([0, a.per_request], np.uint32)
+        so_h = sig_off[:a.per_request + 1]
+        seed_h = hashlib.sha256(b"batch-rand").digest()
+        one_set()
+        assert dev.verify_requests(ro_h, pk_h, None, mg_h, sg_h, so_h, seed_h).valid.all()
+        for _ in range(a.latency_reps):
+            t1 = time.perf_counter()
+            one_set()
+            lat1.append((time.perf_counter() - t1) * 1e3)
+            t1 = time.perf_counter()
+            dev.verify_requests(ro_h, pk_h, None, mg_h, sg_h, so_h, seed_h)
+            lat_host.append((time.perf_counter() - t1) * 1e3)
+    p50_1 = float(np.median(lat1)) if lat1 else None
+    p50_host = float(np.median(lat_host)) if lat_host else None
 
     legs = {}
     if world == 1 and not a.no_legs:
@@ -361,6 +389,8 @@ def main():
         "ranks_joined": world,
         "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
         "p50_stage_ms": lat_stages,
+        "p50_ms_1set": round(p50_1, 3) if p50_1 is not None else None,
+        "p50_ms_128set_host": round(p50_host, 3) if p50_host is not None else None,
         "all_valid": ok,
         "overlap": "sync" if a.sync else f"{nbuf} calls in flight",
         "combine": ({"mode": "two-phase calls; per-step all-gather of the ranks' 576-byte Fp12 partials (gloo), "
@@ -435,6 +465,27 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         roof["pipeline_frac"] = round(pipe / peak, 5)
         roof["mads_per_set"] = round(oc["mads_per_set_total"])
     return roof
+
+
+def node_leg(pks, msgs, sigs, rounds: int = 4):
+    """The Lodestar path (tools/bench_node.js): BlsGpuVerifier in node -> N-API addon ->
+    lb_verify_requests_async, pubkeys by index; throughput and p50 latencies."""
+    import shutil
+    import tempfile
+    if not shutil.which("node") or not os.path.exists(os.path.join(ROOT, "lodestar_amd", "napi", "lodestar_bls.node")):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
+            with open(os.path.join(d, name + ".bin"), "wb") as f:
+                f.write(b"".join(items))
+        try:
+            out = subprocess.run(["node", os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)],
+                                 capture_output=True, text=True, timeout=300)
+        except subprocess.TimeoutExpired:
+            return {"error": "timeout"}
+    if out.returncode != 0:
+        return {"error": out.stderr[-500:]}
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off):
@@ -520,6 +571,7 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
     for pc in pend:
         allv &= all(dev.wait_same_message(pc)[1])
     el = time.perf_counter() - t1
+    legs["node"] = node_leg(pks, msgs, sigs)
     legs["same_message_inflight"] = {"sets_per_s": round(n_jobs * per_job * reps / el, 1), "packages": reps,
                                      "all_fast": bool(allv), "jobs": n_jobs, "sets_per_job": per_job,
                                      "api": f"lb_verify_same_message_batch_async, {nbuf} packages in flight "

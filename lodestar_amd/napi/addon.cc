@@ -806,10 +806,11 @@ napi_value ValidateRequests(napi_env env, napi_callback_info info) {
 }
 
 napi_value Init(napi_env env, napi_value exports) {
-  // 8 HIP hardware queues for this process unless the host chose otherwise: the library
-  // keeps one call in flight per queue (lb_slots), 2.94 vs 2.74 M sets/s over HIP's
-  // default 4 (profiles/ab_r03/hwq).  Before the first HIP call (lb_create).
-  setenv("GPU_MAX_HW_QUEUES", "8", 0);
+  // 16 HIP hardware queues for this process (LB_HW_QUEUES overrides): the library keeps
+  // one call in flight per queue (lb_slots), 3.03 vs 2.74 M sets/s over HIP's default 4
+  // (profiles/ab_r03/hwq2).  Before the first HIP call (lb_create).
+  const char* q = getenv("LB_HW_QUEUES");
+  setenv("GPU_MAX_HW_QUEUES", q ? q : "16", 1);
   napi_property_descriptor methods[] = {
       {"verifyRequests", nullptr, VerifyRequests, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verifyRequestsPartial", nullptr, VerifyRequestsPartial, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -1,0 +1,76 @@
+"use strict";
+// The path Lodestar takes, timed: BlsGpuVerifier (JS host) -> N-API addon ->
+// lb_verify_requests_async, pubkeys by validator index (the index2pubkey mirror).
+// Usage: node tools/bench_node.js DIR ROUNDS   (DIR: pks.bin n x 96, msgs.bin n x 32,
+// sigs.bin n x 96 of bench.py's workload).  Prints one JSON line:
+//   sets_per_s  ROUNDS x (n / 128) verifySignatureSets jobs of 128 sets, all queued at
+//               once (the pool packs up to 65,536 sets per package, capacity packages
+//               in flight), JS packing + addon + PCIe included;
+//   p50_ms_128set  one verifySignatureSets of 128 sets on an idle verifier;
+//   p50_ms_1set    one verifyOnMainThread set (gossip block proposer signature,
+//                  BN/chain/validation/block.ts:146 -> index.ts:174-187).
+const fs = require("fs");
+const path = require("path");
+const ROOT = path.join(__dirname, "..");
+const V = require(path.join(ROOT, "lodestar_amd", "js", "bls_gpu_verifier.js"));
+
+const dir = process.argv[2];
+const rounds = parseInt(process.argv[3] || "4", 10);
+const rd = (name) => new Uint8Array(fs.readFileSync(path.join(dir, name)));
+
+function median(xs) {
+  const s = xs.slice().sort((a, b) => a - b);
+  return s[Math.floor(s.length / 2)];
+}
+
+(async () => {
+  const pks = rd("pks.bin");
+  const msgs = rd("msgs.bin");
+  const sigs = rd("sigs.bin");
+  const n = msgs.length / 32;
+  const v = new V.BlsGpuVerifier({devices: [0]});
+  const tableSize = await v.syncPubkeys(Array.from({length: n}, (_, i) => pks.subarray(96 * i, 96 * i + 96)), 96);
+  const set = (i) => ({
+    type: "single",
+    pubkey: {index: i},
+    signingRoot: msgs.subarray(32 * i, 32 * i + 32),
+    signature: sigs.subarray(96 * i, 96 * i + 96),
+  });
+  const jobs = [];
+  for (let j = 0; j < n / 128; j++) jobs.push(Array.from({length: 128}, (_, k) => set(128 * j + k)));
+  const ms = () => Number(process.hrtime.bigint()) / 1e6;
+  // warm-up: one package of every job
+  let ok = (await Promise.all(jobs.map((js) => v.verifySignatureSets(js)))).every((x) => x === true);
+  const t0 = ms();
+  const all = [];
+  for (let r = 0; r < rounds; r++) for (const js of jobs) all.push(v.verifySignatureSets(js));
+  ok = ok && (await Promise.all(all)).every((x) => x === true);
+  const el = ms() - t0;
+  const lat128 = [];
+  const lat1 = [];
+  for (let r = 0; r < 11; r++) {
+    let t = ms();
+    ok = ok && (await v.verifySignatureSets(jobs[r % jobs.length])) === true;
+    lat128.push(ms() - t);
+    t = ms();
+    ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
+    lat1.push(ms() - t);
+  }
+  await v.close();
+  process.stdout.write(
+    JSON.stringify({
+      sets_per_s: Math.round((rounds * n * 1000) / el),
+      rounds,
+      sets_per_round: n,
+      p50_ms_128set: +median(lat128).toFixed(3),
+      p50_ms_1set: +median(lat1).toFixed(3),
+      all_valid: ok,
+      table_size: tableSize,
+      capacity: v.capacity,
+      api: "BlsGpuVerifier.verifySignatureSets -> N-API addon -> lb_verify_requests_async (validator indices)",
+    }) + "\n"
+  );
+})().catch((e) => {
+  console.error(e);
+  process.exit(1);
+});
