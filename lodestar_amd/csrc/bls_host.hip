@@ -76,6 +76,8 @@ struct PipeState {
 // jobs alone) on the same slot from the device-resident decoded signatures.
 struct SmState {
   bool active = false;
+  int phase = 0;                     // 1: phase 1 in flight, 2: phase 2 (retries) in flight
+  uint32_t nr = 0, retried_jobs = 0, fast_sets = 0;
   bool by_index = false;
   uint32_t nj = 0, ns = 0;
   uint8_t* out_valid = nullptr;     // caller: n_sets verdicts
@@ -123,6 +125,10 @@ struct Slot {
   uint8_t *out_valid = nullptr, *out_err = nullptr, *out_sst = nullptr;
   uint32_t out_nr = 0, out_ns = 0;
   SmState sm;
+  // an async call on an otherwise idle GPU runs as the two-stream DAG with the
+  // stream of an idle slot (borrowed); that slot is lent (busy) until the call retires
+  Slot* borrowed = nullptr;
+  Slot* lent_to = nullptr;
 };
 
 // Stats of a retired call, kept per ticket (lb_wait reports the stats of ITS
@@ -373,7 +379,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // instead and the work-efficient form is kept (LB_ACC_SPLIT=0|1 forces one)
   bool lone = true;
   for (int s = 0; s < ctx->n_slots; s++)
-    if (&ctx->slots[s] != &sl && ctx->slots[s].busy) lone = false;
+    if (&ctx->slots[s] != &sl && ctx->slots[s].busy && ctx->slots[s].lent_to != &sl) lone = false;
   const bool split = by_lines && (ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64));
   // merged pair (-g1, S_all) with S_all from the MSM: without a split its Miller
   // value is one extra workgroup of k_miller_acc (fold; its 512 request waves
@@ -639,13 +645,26 @@ int finish_partial(lb_ctx* ctx, Slot& sl, bool merged_ok) {
 // Wait for a slot's outstanding call and publish its stage times, stats and
 // (host-buffer calls) verdicts.  A two-phase call whose host verdict never came
 // runs its per-request tails (merged_ok = 0: every verdict computed alone).
-int sm_complete(lb_ctx* ctx, Slot& sl);
+int sm_advance(lb_ctx* ctx, Slot& sl, bool block);
+int sm_pump(lb_ctx* ctx);
+
+void release_borrowed(Slot& sl) {  // hand a borrowed stream back
+  if (!sl.borrowed) return;
+  sl.borrowed->busy = false;
+  sl.borrowed->lent_to = nullptr;
+  sl.st[1] = sl.st[0];
+  sl.borrowed = nullptr;
+}
 
 int finish_slot(lb_ctx* ctx, Slot& sl) {
-  if (!sl.busy) return LB_OK;
+  if (sl.lent_to) return finish_slot(ctx, *sl.lent_to);  // releases this slot
+  if (!sl.busy) {
+    release_borrowed(sl);  // (a submission that failed after borrowing)
+    return LB_OK;
+  }
   LB_TRY(finish_partial(ctx, sl, false));
+  while (sl.sm.active) LB_TRY(sm_advance(ctx, sl, true));  // same-message: phases 1 and 2
   LB_HIP(hipEventSynchronize(sl.done));
-  if (sl.sm.active) LB_TRY(sm_complete(ctx, sl));
   ctx->n_stages = sl.n_stages;
   for (int i = 0; i < sl.n_stages; i++) {
     float ms = 0.f;
@@ -669,8 +688,30 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
     if (sl.out_sst && sl.out_ns) memcpy(sl.out_sst, sl.h_out + 2 * a, sl.out_ns);
     sl.out_valid = sl.out_err = sl.out_sst = nullptr;
   }
+  release_borrowed(sl);
   sl.busy = false;
   return LB_OK;
+}
+
+// An async call on slot `sl` (single stream, just retired) while no other call is
+// in flight: the lowest latency is the two-stream DAG (hash_to_G2 + lines beside
+// the signature / MSM branch), so it borrows an idle slot's stream; the next call
+// that wants that slot waits for this one first (finish_slot).
+void borrow_idle_stream(lb_ctx* ctx, Slot& sl) {
+  if (sl.st[1] != sl.st[0] || sl.borrowed) return;
+  Slot* idle = nullptr;
+  for (int s = 0; s < ctx->n_slots; s++) {
+    Slot& o = ctx->slots[s];
+    if (&o == &sl) continue;
+    if (o.busy || o.partial_pending) return;  // not alone on the GPU
+    if (!idle && o.st[0] != sl.st[0]) idle = &o;
+  }
+  if (!idle) return;
+  sl.st[1] = idle->st[0];
+  sl.borrowed = idle;
+  idle->busy = true;
+  idle->ticket = 0;
+  idle->lent_to = &sl;
 }
 
 int begin_call(lb_ctx* ctx, Slot& sl) {
@@ -872,6 +913,7 @@ int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
                          uint8_t* d_set_status, bool partial, uint64_t* out_ticket) {
   LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
+  if (!partial) borrow_idle_stream(ctx, sl);  // (a pending two-phase call never holds a lent slot)
   LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(b->n_requests, b->n_sets)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   uint8_t* d_partial = partial ? ws.take<uint8_t>(LB_GT_BYTES) : nullptr;
@@ -954,6 +996,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
       al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed) + al(sz_rows);
   const size_t out_bytes = al(nr ? nr : 1) * 2 + al(ns ? ns : 1);
   LB_TRY(finish_slot(ctx, sl));
+  if (!partial) borrow_idle_stream(ctx, sl);
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
   LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
@@ -1052,6 +1095,7 @@ int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* b, uint
   LB_TRY(validate_batch(ctx, b));
   if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
   return submit_device(ctx, next_async_slot(ctx), b, d_valid, d_req_err, d_set_status, false, out_ticket);
 }
 
@@ -1061,6 +1105,7 @@ int lb_verify_requests_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* ou
   LB_TRY(validate_batch(ctx, b));
   if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
   return submit_host(ctx, next_async_slot(ctx), b, out_valid, out_req_err, out_set_status, false, out_ticket);
 }
 
@@ -1070,6 +1115,7 @@ int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* b, uin
   LB_TRY(validate_batch(ctx, b));
   if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
   Slot& sl = next_async_slot(ctx);
   if (flags & LB_BATCH_DEVICE)
     return submit_device(ctx, sl, b, out_valid, out_req_err, out_set_status, true, out_ticket);
@@ -1142,6 +1188,7 @@ int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* ou
 int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
   if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
   fill_stats(ctx, ticket, stats);
   return LB_OK;
@@ -1631,6 +1678,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   LB_HIP(hipMemcpyAsync(h_res + 3 * al256(nj), d_jpkst, nj, hipMemcpyDeviceToHost, sl.st[0]));
   SmState& m = sl.sm;
   m.active = true;
+  m.phase = 1;
   m.by_index = by_index;
   m.nj = nj;
   m.ns = ns;
@@ -1649,64 +1697,94 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   return end_call_async(ctx, sl);
 }
 
-// Completion of a same-message call after its phase 1: verdicts of the jobs
-// whose aggregate passed, and phase 2 for the sets of the others.
-int sm_complete(lb_ctx* ctx, Slot& sl) {
+// Progress of a same-message call.  Phase 1 done: verdicts of the jobs whose
+// aggregate passed, and phase 2 -- the sets of the other jobs, each its own
+// 1-set request -- enqueued on the same slot at once (sm_pump launches it from
+// any later library call, so it need not wait for the caller's lb_wait).
+// Phase 2 done: its verdicts.  block = false: return at once when the phase's
+// work is still in flight.
+int sm_advance(lb_ctx* ctx, Slot& sl, bool block) {
   SmState& m = sl.sm;
-  m.active = false;
+  if (!m.active) return LB_OK;
+  if (!block) {
+    const hipError_t q = hipEventQuery(sl.done);
+    if (q == hipErrorNotReady) return LB_OK;
+    if (q != hipSuccess) LB_HIP(q);
+  }
+  LB_HIP(hipEventSynchronize(sl.done));
   const uint32_t nj = m.nj, ns = m.ns;
-  const uint8_t *v = m.h_res, *e = v + al256(nj), *jb = v + 2 * al256(nj), *pst = v + 3 * al256(nj);
-  uint32_t fast_sets = 0, retried_jobs = 0, nr = 0;
-  for (uint32_t j = 0; j < nj; j++) {
-    // fast path: aggregated set valid, every signature validated, pubkeys aggregated
-    const bool fast = v[j] && e[j] == LB_REQ_OK && !jb[j] && pst[j] == LB_ST_OK;
-    if (m.out_job_fast) m.out_job_fast[j] = fast ? 1 : 0;
-    const uint32_t a = m.h_joff[j], b = m.h_joff[j + 1];
-    if (fast) {
-      for (uint32_t i = a; i < b; i++) m.out_valid[i] = 1;
-      fast_sets += b - a;
-    } else if (b > a) {
-      retried_jobs++;
-      for (uint32_t i = a; i < b; i++) {
-        m.h_rset[nr] = i;
-        m.h_rset[(size_t)ns + nr] = j;
-        nr++;
+  if (m.phase == 2) {
+    for (uint32_t r = 0; r < m.nr; r++)
+      m.out_valid[m.h_rset[r]] = (m.h_rout[r] && m.h_rout[al256(ns) + r] == LB_REQ_OK) ? 1 : 0;
+  } else {
+    const uint8_t *v = m.h_res, *e = v + al256(nj), *jb = v + 2 * al256(nj), *pst = v + 3 * al256(nj);
+    uint32_t fast_sets = 0, retried_jobs = 0, nr = 0;
+    for (uint32_t j = 0; j < nj; j++) {
+      // fast path: aggregated set valid, every signature validated, pubkeys aggregated
+      const bool fast = v[j] && e[j] == LB_REQ_OK && !jb[j] && pst[j] == LB_ST_OK;
+      if (m.out_job_fast) m.out_job_fast[j] = fast ? 1 : 0;
+      const uint32_t a = m.h_joff[j], b = m.h_joff[j + 1];
+      if (fast) {
+        for (uint32_t i = a; i < b; i++) m.out_valid[i] = 1;
+        fast_sets += b - a;
+      } else if (b > a) {
+        retried_jobs++;
+        for (uint32_t i = a; i < b; i++) {
+          m.h_rset[nr] = i;
+          m.h_rset[(size_t)ns + nr] = j;
+          nr++;
+        }
       }
     }
-  }
-  if (nr) {
-    Bump ws{sl.d_ws, m.ws_off, sl.ws_cap};
-    uint32_t* d_rset = ws.take<uint32_t>(2 * (size_t)ns);
-    g2j* d_rsig = ws.take<g2j>(nr);
-    uint8_t* d_rst = ws.take<uint8_t>(nr);
-    uint8_t* d_rmsg = ws.take<uint8_t>((size_t)nr * 32);
-    uint32_t* d_ridx = ws.take<uint32_t>(nr);
-    uint32_t* d_rreq = ws.take<uint32_t>((size_t)nr + 1);
-    uint8_t* d_rvalid = ws.take<uint8_t>(nr);
-    uint8_t* d_rerr = ws.take<uint8_t>(nr);
-    if (ws.off > ws.cap) {
-      ctx->err = "workspace overflow";
-      return LB_ERR_OUT_OF_MEMORY;
+    m.nr = nr;
+    m.retried_jobs = retried_jobs;
+    m.fast_sets = fast_sets;
+    if (nr) {
+      Bump ws{sl.d_ws, m.ws_off, sl.ws_cap};
+      uint32_t* d_rset = ws.take<uint32_t>(2 * (size_t)ns);
+      g2j* d_rsig = ws.take<g2j>(nr);
+      uint8_t* d_rst = ws.take<uint8_t>(nr);
+      uint8_t* d_rmsg = ws.take<uint8_t>((size_t)nr * 32);
+      uint32_t* d_ridx = ws.take<uint32_t>(nr);
+      uint32_t* d_rreq = ws.take<uint32_t>((size_t)nr + 1);
+      uint8_t* d_rvalid = ws.take<uint8_t>(nr);
+      uint8_t* d_rerr = ws.take<uint8_t>(nr);
+      if (ws.off > ws.cap) {
+        ctx->err = "workspace overflow";
+        m.active = false;
+        return LB_ERR_OUT_OF_MEMORY;
+      }
+      LB_HIP(hipMemcpyAsync(d_rset, m.h_rset, sizeof(uint32_t) * 2 * (size_t)ns, hipMemcpyHostToDevice, sl.st[0]));
+      hipLaunchKernelGGL(k_sm_retry_gather, dim3(blocks_for(nr)), dim3(TPB), 0, sl.st[0], nr, (const uint32_t*)d_rset,
+                         (const uint32_t*)(d_rset + ns), m.d_sig, m.d_sst, m.d_msgs,
+                         m.by_index ? (const uint32_t*)m.d_pks : (const uint32_t*)nullptr, d_rsig, d_rst, d_rmsg,
+                         d_ridx, d_rreq);
+      LB_HIP(hipGetLastError());
+      LB_TRY(run_pipeline(ctx, sl, nr, nr, d_rreq, m.by_index ? nullptr : m.d_pks, nullptr, d_ridx, d_rmsg, nullptr,
+                          nullptr, m.d_seed, d_rvalid, d_rerr, nullptr, ws, nullptr, d_rsig, d_rst));
+      LB_HIP(hipMemcpyAsync(m.h_rout, d_rvalid, nr, hipMemcpyDeviceToHost, sl.st[0]));
+      LB_HIP(hipMemcpyAsync(m.h_rout + al256(ns), d_rerr, nr, hipMemcpyDeviceToHost, sl.st[0]));
+      LB_TRY(end_call(ctx, sl));
+      m.phase = 2;
+      return LB_OK;
     }
-    LB_HIP(hipMemcpyAsync(d_rset, m.h_rset, sizeof(uint32_t) * 2 * (size_t)ns, hipMemcpyHostToDevice, sl.st[0]));
-    hipLaunchKernelGGL(k_sm_retry_gather, dim3(blocks_for(nr)), dim3(TPB), 0, sl.st[0], nr, (const uint32_t*)d_rset,
-                       (const uint32_t*)(d_rset + ns), m.d_sig, m.d_sst, m.d_msgs,
-                       m.by_index ? (const uint32_t*)m.d_pks : (const uint32_t*)nullptr, d_rsig, d_rst, d_rmsg, d_ridx,
-                       d_rreq);
-    LB_HIP(hipGetLastError());
-    LB_TRY(run_pipeline(ctx, sl, nr, nr, d_rreq, m.by_index ? nullptr : m.d_pks, nullptr, d_ridx, d_rmsg, nullptr,
-                        nullptr, m.d_seed, d_rvalid, d_rerr, nullptr, ws, nullptr, d_rsig, d_rst));
-    LB_HIP(hipMemcpyAsync(m.h_rout, d_rvalid, nr, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_HIP(hipMemcpyAsync(m.h_rout + al256(ns), d_rerr, nr, hipMemcpyDeviceToHost, sl.st[0]));
-    LB_TRY(end_call(ctx, sl));
-    LB_HIP(hipEventSynchronize(sl.done));
-    for (uint32_t r = 0; r < nr; r++)
-      m.out_valid[m.h_rset[r]] = (m.h_rout[r] && m.h_rout[al256(ns) + r] == LB_REQ_OK) ? 1 : 0;
   }
   // the package's worker bookkeeping (index.ts:557-568): jobs retried set by set,
   // sets verified by a passing aggregate (after phase 2's own merged-check stats)
-  sl.h_stats[0] = retried_jobs;
-  sl.h_stats[1] = fast_sets;
+  sl.h_stats[0] = m.retried_jobs;
+  sl.h_stats[1] = m.fast_sets;
+  m.active = false;
+  m.phase = 0;
+  return LB_OK;
+}
+
+// Launch the phase 2 of every same-message call whose phase 1 has completed
+// (called from every async entry point and lb_wait: no blocking).
+int sm_pump(lb_ctx* ctx) {
+  for (int s = 0; s < ctx->n_slots; s++) {
+    Slot& sl = ctx->slots[s];
+    if (sl.busy && sl.sm.active && sl.sm.phase == 1) LB_TRY(sm_advance(ctx, sl, false));
+  }
   return LB_OK;
 }
 
@@ -1719,6 +1797,7 @@ int lb_verify_same_message_batch_async(lb_ctx* ctx, const lb_same_message_batch*
   if (!ctx || !b || !out_ticket || (b->n_sets && !out_valid)) return LB_ERR_INVALID_ARGUMENT;
   LB_TRY(sm_validate(ctx, b));
   LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
   Slot& sl = next_async_slot(ctx);
   LB_TRY(finish_slot(ctx, sl));
   if (b->n_jobs == 0) {  // nothing to verify: a call that completes at once
@@ -1727,6 +1806,7 @@ int lb_verify_same_message_batch_async(lb_ctx* ctx, const lb_same_message_batch*
     *out_ticket = sl.ticket;
     return LB_OK;
   }
+  borrow_idle_stream(ctx, sl);
   LB_TRY(sm_submit(ctx, sl, b, out_valid, out_job_fast));
   *out_ticket = sl.ticket;
   return LB_OK;

@@ -189,3 +189,32 @@ def test_verify_distributed_two_ranks_one_gpu(workload, bad):
         assert p.exitcode == 0
     for _, v, e in res:
         assert (v, e) == want
+
+
+def test_async_lone_call_borrows_a_stream(device, workload):
+    """A lone async call runs as the two-stream DAG on an idle slot's stream (lower
+    latency); the next calls (one of which lands on the lent slot) wait for it and
+    every verdict stays right; a two-phase call never borrows."""
+    reqs = _corrupt(workload[:12], [4])
+    want = [k != 4 for k in range(12)]
+    pks, pk_off, msgs, sigs, req_off = [], [0], [], [], [0]
+    for r in reqs:
+        for s in r:
+            keys = [s.pubkey] if s.pubkey is not None else s.pubkeys
+            pks += [k.uncompressed for k in keys]
+            pk_off.append(len(pks))
+            msgs.append(s.signing_root)
+            sigs.append(s.signature)
+        req_off.append(len(msgs))
+    blob, offs = pack_blobs(sigs)
+    args = (np.array(req_off, np.uint32), np.frombuffer(b"".join(pks), np.uint8), np.array(pk_off, np.uint32),
+            np.frombuffer(b"".join(msgs), np.uint8), blob, offs)
+    for _ in range(3):
+        pcs = [device.verify_requests_async(*args, bytes(32))]
+        pcs += [device.verify_requests_async(*args, bytes(32)) for _ in range(device.slots() + 1)]
+        assert all([bool(v) for v in device.wait_call(pc).valid] == want for pc in pcs)
+    pp = device.verify_requests_async(*args, bytes(32), partial=True)
+    lone = device.verify_requests_async(*args, bytes(32))
+    assert [bool(v) for v in device.wait_call(lone).valid] == want
+    device.verify_finish(pp, False)
+    assert [bool(v) for v in device.wait_call(pp).valid] == want
