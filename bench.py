@@ -54,10 +54,11 @@ os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LB_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-# Roofline peak: v_mad_u64_u32 is quarter-rate on gfx950 (measured 30.5 of 32
-# per clk per CU, tools/microbench/mad_rate.hip); chip = 256 CU x 4 SIMD x 32
-# lanes / 4 x 2.4 GHz (MI355X_MICROARCH.md chip table).
-PEAK_MAD_PER_S = 256 * 4 * 32 / 4 * 2.4e9
+# Roofline peak: v_mad_u64_u32 is quarter-rate on gfx950: 32 per clk per CU at
+# 2.4 GHz over 256 CUs = 19.66 Tmad/s.  Measured: 1.877e13/s = 30.55 per clk per CU
+# (tools/microbench/mad_rate.hip, 8 waves/SIMD; profiles/prof_r03e/mad_rate.txt).
+# The larger of the two (the nominal one) prices every fraction.
+PEAK_MAD_PER_S = max(256 * 32 * 2.4e9, 1.877e13)
 
 
 def interop_sk_be(i: int) -> bytes:

@@ -22,6 +22,8 @@ STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
     "decode_sigs": "k_decode_sigs", "scalar_sig": "k_scalar_sig", "sum_tree": "k_sum_tree",
     "miller_acc": "k_miller_acc", "merge": "k_merge", "lines_S": "k_lines_S", "tail": "k_tail",
     "miller_wave": "k_pair_wc", "pubkeys_agg": "k_pubkeys_agg",
+    "msm_digits": "k_msm_scalars", "msm_chunks": "k_msm_chunks", "msm_buckets": "k_msm_buckets",
+    "msm_bits": "k_msm_bits", "msm_final": "k_msm_final", "msm_scatter": "k_msm_scatter",
 }
 
 
@@ -37,6 +39,9 @@ ALG_BYTES_PER_SET = {
     "scalar_sig": 288 + 288,          # sigma -> r sigma
     "lines": 144 + 288 + 68 * 288,    # r pk, H -> 68 lines
     "miller_acc": 68 * 288 + 2,       # lines (+ statuses) -> per-request F_k
+    # bucket MSM: 6 entries per set (2 half-points x 3 windows), each a 4-byte sorted
+    # index and the point's affine (x, y) = 192 B, and 6/16 chunk partials (288 B)
+    "msm_chunks": 6 * (4 + 192) + 6 * 288 // 16,
 }
 N_SETS = 65536
 
