@@ -148,9 +148,9 @@ struct lb_ctx {
   // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
   // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
   // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
-  static constexpr int kMaxSlots = 16;
+  static constexpr int kMaxSlots = 32;
   int n_slots = 4;
-  int streams_per_slot[kMaxSlots] = {2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+  int streams_per_slot[kMaxSlots] = {2};  // (set for every slot in lb_create)
   Slot slots[kMaxSlots];
   int next_slot = 0;
   uint64_t next_ticket = 1;
@@ -787,7 +787,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   // one single-stream slot per hardware queue HIP gives this process (4 by
   // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8 calls
   // in flight: 2.94 vs 2.74 M sets/s once the merged check's one-wave kernels
-  // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 16)
+  // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 32)
   if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
     const int v = atoi(e);
     ctx->n_slots = v < 4 ? 4 : v > lb_ctx::kMaxSlots ? lb_ctx::kMaxSlots : v;

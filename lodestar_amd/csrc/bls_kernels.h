@@ -63,6 +63,21 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #define LB_MSM_NONE 0xffffffffu
 
 namespace lb {
+// One lane's tower value in an LDS tree, padded so the record stride is an odd number of
+// 16-byte units: a wave's ds_read_b128 / ds_write_b128 of lane-strided records then hits
+// every bank once per lane group (MI355X_MICROARCH.md, LDS table).  An fp12 at its bare
+// 144-dword stride maps 16 lanes onto 4 bank groups (SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.36
+// in k_miller_acc's epilogue); a Jacobian G2 point at 72 dwords onto 8.
+template <class T, bool PAD = ((sizeof(T) / 16) % 2 == 0)>
+struct alignas(16) LdsRec {
+  T v;
+  uint32_t pad[4];
+};
+template <class T>
+struct alignas(16) LdsRec<T, false> {
+  T v;
+};
+
 // Where a set's pubkeys come from: the call's 96-byte uncompressed encodings
 // (the worker wire format, chain/bls/multithread/worker.ts:110-116) or the
 // device-resident pubkey table addressed by validator index (the index2pubkey

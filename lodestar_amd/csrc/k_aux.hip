@@ -7,24 +7,24 @@ namespace lb {
 // ---- generic point sums (one workgroup, LDS tree) ------------------------
 template <class F>
 __global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out) {
-  __shared__ jac<F> sh[256];
+  __shared__ LdsRec<jac<F>> sh[256];
   jac<F> acc;
   jac_set_inf(acc);
   for (uint32_t i = threadIdx.x; i < n; i += 256) {
     jac<F> t = in[i];
     jac_add(acc, acc, t);
   }
-  sh[threadIdx.x] = acc;
+  sh[threadIdx.x].v = acc;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
-      jac<F> m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      jac<F> m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
-      sh[threadIdx.x] = m;
+      sh[threadIdx.x].v = m;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = sh[0];
+  if (threadIdx.x == 0) out[0] = sh[0].v;
 }
 
 __global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96) {

@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
     if (threadIdx.x == 0) miller_neg_g1(Fx, Sx);
     return;
   }
-  __shared__ fp12 sh[TPB];
+  __shared__ LdsRec<fp12> sh[TPB];
   __shared__ uint32_t bad[RPW], err_empty[RPW], err_pk[RPW];
   const uint32_t sub = threadIdx.x / LPR, lane = threadIdx.x % LPR;
   const uint32_t k = blockIdx.x * RPW + sub;
@@ -151,18 +151,18 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_miller_acc(uint32_t n_req, co
     }
   }
   fp12_conj(f, f);  // x < 0
-  sh[threadIdx.x] = f;
+  sh[threadIdx.x].v = f;
   __syncthreads();
   for (uint32_t s = (uint32_t)LPR / 2; s > 0; s >>= 1) {
     if (lane < s) {
-      fp12 m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      fp12 m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       fp12_mul(m, m, o);
-      sh[threadIdx.x] = m;
+      sh[threadIdx.x].v = m;
     }
     __syncthreads();
   }
   if (live && lane == 0) {
-    fp12 tot = sh[threadIdx.x];
+    fp12 tot = sh[threadIdx.x].v;
     if (fS) {  // null: the tail kernel multiplies Miller(-g1, S_k) in (k_tail)
       fp12 s = fS[k];
       fp12_mul(tot, tot, s);

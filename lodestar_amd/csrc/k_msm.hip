@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t
 // One wave per bit position p = 11 w + k: G_p = sum of the buckets d of
 // window w whose bit k is set (512 of them for k < 10, only d = 1024 for k = 10).
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G) {
-  __shared__ g2j sh[TPB];
+  __shared__ LdsRec<g2j> sh[TPB];
   const uint32_t p = blockIdx.x;
   if (p >= LB_MSM_POS) return;
   const uint32_t w = p / LB_MSM_C, k = p % LB_MSM_C;
@@ -242,22 +242,22 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_bits(const g2j* __rest
     g2j t = bsum[w * LB_MSM_NB + d - 1];
     jac_add(acc, acc, t);
   }
-  sh[threadIdx.x] = acc;
+  sh[threadIdx.x].v = acc;
   __syncthreads();
   for (uint32_t s = TPB / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
-      g2j m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
-      sh[threadIdx.x] = m;
+      sh[threadIdx.x].v = m;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) G[p] = sh[0];
+  if (threadIdx.x == 0) G[p] = sh[0].v;
 }
 
 // One wave: S = sum_p 2^p G_p (lane p doubles p times, then an LDS tree), affine.
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_final(const g2j* __restrict__ G, g2a* __restrict__ S) {
-  __shared__ g2j sh[TPB];
+  __shared__ LdsRec<g2j> sh[TPB];
   const uint32_t p = threadIdx.x;
   g2j acc;
   jac_set_inf(acc);
@@ -266,18 +266,18 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_final(const g2j* __res
 #pragma unroll 1
     for (uint32_t t = 0; t < p; t++) jac_dbl(acc, acc);
   }
-  sh[p] = acc;
+  sh[p].v = acc;
   __syncthreads();
   for (uint32_t s = TPB / 2; s > 0; s >>= 1) {
     if (p < s) {
-      g2j m = sh[p], o = sh[p + s];
+      g2j m = sh[p].v, o = sh[p + s].v;
       jac_add(m, m, o);
-      sh[p] = m;
+      sh[p].v = m;
     }
     __syncthreads();
   }
   if (p == 0) {
-    g2j tot = sh[0];
+    g2j tot = sh[0].v;
     g2a sa;
     jac_to_aff(sa, tot);
     S[0] = sa;

@@ -10,7 +10,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_prod_tree(uint32_t n_req, co
                                                    const uint8_t* __restrict__ sig_status,
                                                    const uint8_t* __restrict__ pk_status, fp12* __restrict__ F,
                                                    uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err) {
-  __shared__ fp12 sh[TPB];
+  __shared__ LdsRec<fp12> sh[TPB];
   __shared__ uint32_t bad, err_empty, err_pk;
   const uint32_t k = blockIdx.x;
   if (k >= n_req) return;
@@ -37,18 +37,18 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_prod_tree(uint32_t n_req, co
       fp12_mul(acc, acc, t);
     }
   }
-  sh[threadIdx.x] = acc;
+  sh[threadIdx.x].v = acc;
   __syncthreads();
   for (int s = TPB / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-      fp12 m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      fp12 m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       fp12_mul(m, m, o);
-      sh[threadIdx.x] = m;
+      sh[threadIdx.x].v = m;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    fp12 tot = sh[0];
+    fp12 tot = sh[0].v;
     if (fS) {  // null: the tail kernel multiplies Miller(-g1, S_k) in (k_tail)
       fp12 s = fS[k];
       fp12_mul(tot, tot, s);

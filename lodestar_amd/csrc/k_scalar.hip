@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_scalar_pk(uint32_t n, cons
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                   const g2j* __restrict__ rsig, g2a* __restrict__ S,
                                                   const uint8_t* __restrict__ skip) {
-  __shared__ g2j sh[TPB];
+  __shared__ LdsRec<g2j> sh[TPB];
   const uint32_t k = blockIdx.x;
   if (k >= n_req || (skip && *skip)) return;
   const uint32_t a = req_off[k], b = req_off[k + 1];
@@ -62,18 +62,18 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_sum_tree(uint32_t n_req, c
     g2j t = rsig[i];
     jac_add(acc, acc, t);
   }
-  sh[threadIdx.x] = acc;
+  sh[threadIdx.x].v = acc;
   __syncthreads();
   for (int s = TPB / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-      g2j m = sh[threadIdx.x], o = sh[threadIdx.x + s];
+      g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
-      sh[threadIdx.x] = m;
+      sh[threadIdx.x].v = m;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    g2j tot = sh[0];
+    g2j tot = sh[0].v;
     g2a sa;
     jac_to_aff(sa, tot);
     S[k] = sa;

@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_single(uint32_t n_sets, PkSourc
 __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource pks,
                                                      const uint32_t* __restrict__ pk_off, g1j* __restrict__ out_pk,
                                                      uint8_t* __restrict__ pk_status) {
-  __shared__ g1j sh[TPB];
+  __shared__ LdsRec<g1j> sh[TPB];
   __shared__ uint32_t bad;
   if (!pk_off) return;
   for (uint32_t set = blockIdx.x; set < n_sets; set += gridDim.x) {
@@ -83,20 +83,20 @@ __global__ void __launch_bounds__(TPB) k_pubkeys_agg(uint32_t n_sets, PkSource p
         jac_add_aff(acc, acc, p);
       }
     }
-    sh[threadIdx.x] = acc;
+    sh[threadIdx.x].v = acc;
     __syncthreads();
     for (int s = TPB / 2; s > 0; s >>= 1) {
       if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-        g1j o = sh[threadIdx.x + s];
-        g1j m = sh[threadIdx.x];
+        g1j o = sh[threadIdx.x + s].v;
+        g1j m = sh[threadIdx.x].v;
         jac_add(m, m, o);
-        sh[threadIdx.x] = m;
+        sh[threadIdx.x].v = m;
       }
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      out_pk[set] = sh[0];
-      pk_status[set] = bad ? LB_ST_BAD_ENCODING : jac_is_inf(sh[0]) ? LB_ST_PK_INFINITY : LB_ST_OK;
+      out_pk[set] = sh[0].v;
+      pk_status[set] = bad ? LB_ST_BAD_ENCODING : jac_is_inf(sh[0].v) ? LB_ST_PK_INFINITY : LB_ST_OK;
     }
     __syncthreads();
   }
@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const
                                                           const g1j* __restrict__ job_pk, uint8_t* __restrict__ out_pk96,
                                                           uint8_t* __restrict__ out_sig192,
                                                           uint8_t* __restrict__ job_bad) {
-  __shared__ g2j sh[TPB];
+  __shared__ LdsRec<g2j> sh[TPB];
   __shared__ uint32_t bad;
   for (uint32_t j = blockIdx.x; j < n_jobs; j += gridDim.x) {
     const uint32_t a = job_off[j], b = job_off[j + 1];
@@ -133,14 +133,14 @@ __global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const
         jac_add(acc, acc, t);
       }
     }
-    sh[threadIdx.x] = acc;
+    sh[threadIdx.x].v = acc;
     __syncthreads();
     for (int s = TPB / 2; s > 0; s >>= 1) {
       if ((int)threadIdx.x < s && a + threadIdx.x + s < b) {
-        g2j o = sh[threadIdx.x + s];
-        g2j m = sh[threadIdx.x];
+        g2j o = sh[threadIdx.x + s].v;
+        g2j m = sh[threadIdx.x].v;
         jac_add(m, m, o);
-        sh[threadIdx.x] = m;
+        sh[threadIdx.x].v = m;
       }
       __syncthreads();
     }
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const
       if (bad) {
         for (int k = 0; k < 192; k++) os[k] = 0;
       } else {
-        g2j tot = sh[0];
+        g2j tot = sh[0].v;
         g2a s;
         jac_to_aff(s, tot);
         g2_serialize(os, s);

@@ -142,8 +142,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
                                                         const uint8_t* __restrict__ req_bad,
                                                         g2a* __restrict__ S_all, fp12* __restrict__ F_all,
                                                         const fp12* __restrict__ Fx) {
-  __shared__ g2j shs[TPB];
-  __shared__ fp12 shf[TPB];
+  __shared__ LdsRec<g2j> shs[TPB];
+  __shared__ LdsRec<fp12> shf[TPB];
   g2j acc;
   jac_set_inf(acc);
   fp12 f;
@@ -158,30 +158,30 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
     fp12 t = F[k];
     fp12_mul(f, f, t);
   }
-  shs[threadIdx.x] = acc;
-  shf[threadIdx.x] = f;
+  shs[threadIdx.x].v = acc;
+  shf[threadIdx.x].v = f;
   __syncthreads();
   for (int st = TPB / 2; st > 0; st >>= 1) {
     if ((int)threadIdx.x < st) {
       if (S) {
-        g2j m = shs[threadIdx.x], o = shs[threadIdx.x + st];
+        g2j m = shs[threadIdx.x].v, o = shs[threadIdx.x + st].v;
         jac_add(m, m, o);
-        shs[threadIdx.x] = m;
+        shs[threadIdx.x].v = m;
       }
-      fp12 a = shf[threadIdx.x], b = shf[threadIdx.x + st];
+      fp12 a = shf[threadIdx.x].v, b = shf[threadIdx.x + st].v;
       fp12_mul(a, a, b);
-      shf[threadIdx.x] = a;
+      shf[threadIdx.x].v = a;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     if (S) {
-      g2j tot = shs[0];
+      g2j tot = shs[0].v;
       g2a sa;
       jac_to_aff(sa, tot);
       S_all[0] = sa;
     }
-    F_all[0] = shf[0];
+    F_all[0] = shf[0].v;
   }
 }
 

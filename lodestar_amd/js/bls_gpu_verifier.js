@@ -81,16 +81,6 @@ function workerBatchStats(requestSizes, batchable, valid) {
   return {retries, sigsOk};
 }
 
-function pubkeyRef(pk) {
-  if (pk instanceof Uint8Array) {
-    if (pk.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
-    return {bytes: pk};
-  }
-  if (pk && typeof pk.index === "number") return {index: pk.index, bytes: pk.bytes || null};
-  if (pk && typeof pk.toBytes === "function") return pubkeyRef(pk.toBytes(false));
-  throw new TypeError("pubkey: Uint8Array(96), {index} or an object with toBytes()");
-}
-
 function concat(arrays, total) {
   const out = new Uint8Array(total);
   let o = 0;
@@ -101,94 +91,140 @@ function concat(arrays, total) {
   return out;
 }
 
-/** Requests (arrays of sets) -> the addon's batch (lb_request_batch layout). */
+/** Requests (arrays of sets) -> the addon's batch (lb_request_batch layout).  Two passes:
+ * count, then fill typed arrays allocated once (no per-set or per-key objects: a 65,536-set
+ * package was ~75 ms of main-thread JS with intermediate arrays, the node leg's bound). */
 function packRequests(requests, seed) {
-  const keys = [];
-  const pkOff = [0];
-  const msgs = [];
-  const sigs = [];
-  const sigOff = [0];
-  const reqOff = [0];
+  let nSets = 0;
+  let nKeys = 0;
+  let nIdx = 0;
   let sigBytes = 0;
   for (const req of requests) {
     for (const s of req) {
-      const ks = s.type === "aggregate" ? s.pubkeys || [] : [s.pubkey];
-      for (const k of ks) keys.push(pubkeyRef(k));
-      pkOff.push(keys.length);
+      if (s.type === "aggregate") {
+        const ks = s.pubkeys || [];
+        for (let q = 0; q < ks.length; q++) if (keyIndex(ks[q]) >= 0) nIdx++;
+        nKeys += ks.length;
+      } else {
+        if (keyIndex(s.pubkey) >= 0) nIdx++;
+        nKeys++;
+      }
       if (!(s.signingRoot instanceof Uint8Array) || s.signingRoot.length !== 32)
         throw new TypeError("signingRoot must be 32 bytes");
-      msgs.push(s.signingRoot);
-      sigs.push(s.signature);
       sigBytes += s.signature.length;
-      sigOff.push(sigBytes);
+      nSets++;
     }
-    reqOff.push(msgs.length);
   }
-  const batch = {
-    requestOffsets: Uint32Array.from(reqOff),
-    pkOffsets: Uint32Array.from(pkOff),
-    messages: concat(msgs, 32 * msgs.length),
-    signatures: concat(sigs, sigBytes),
-    sigOffsets: Uint32Array.from(sigOff),
-    seed,
+  const reqOff = new Uint32Array(requests.length + 1);
+  const pkOff = new Uint32Array(nSets + 1);
+  const sigOff = new Uint32Array(nSets + 1);
+  const messages = new Uint8Array(32 * nSets);
+  const signatures = new Uint8Array(sigBytes);
+  // all keys by validator index; a mixed package (a capella block's BLS-change keys beside
+  // validator keys): indices plus flagged indices naming rows of the shipped 96-byte keys
+  // (LB_PK_ROW_FLAG); no index at all: the 96-byte encodings
+  const idx = nIdx > 0 ? new Uint32Array(nKeys) : null;
+  const rowsN = nIdx > 0 ? nKeys - nIdx : nKeys;
+  const rows = rowsN > 0 ? new Uint8Array(96 * rowsN) : null;
+  let k = 0;
+  let row = 0;
+  let i = 0;
+  let so = 0;
+  const putKey = (pk) => {
+    const ix = keyIndex(pk);
+    if (ix >= 0) {
+      idx[k++] = ix;
+      return;
+    }
+    rows.set(keyBytes(pk), 96 * row);
+    if (idx) idx[k] = (LB_PK_ROW_FLAG | row) >>> 0;
+    k++;
+    row++;
   };
-  if (keys.length > 0 && keys.every((k) => k.index !== undefined)) {
-    batch.pubkeyIndices = Uint32Array.from(keys.map((k) => k.index));
-  } else if (keys.some((k) => k.index !== undefined)) {
-    // mixed package (a capella block's BLS-change keys beside validator keys): table
-    // indices, plus flagged indices naming rows of the shipped 96-byte keys (LB_PK_ROW_FLAG)
-    const rows = [];
-    batch.pubkeyIndices = Uint32Array.from(
-      keys.map((k) => {
-        if (k.index !== undefined) return k.index;
-        rows.push(k.bytes);
-        return (LB_PK_ROW_FLAG | (rows.length - 1)) >>> 0;
-      })
-    );
-    batch.pubkeys = concat(rows, 96 * rows.length);
-  } else {
-    batch.pubkeys = concat(
-      keys.map((k) => k.bytes),
-      96 * keys.length
-    );
+  for (let r = 0; r < requests.length; r++) {
+    for (const s of requests[r]) {
+      if (s.type === "aggregate") {
+        const ks = s.pubkeys || [];
+        for (let q = 0; q < ks.length; q++) putKey(ks[q]);
+      } else {
+        putKey(s.pubkey);
+      }
+      pkOff[i + 1] = k;
+      messages.set(s.signingRoot, 32 * i);
+      signatures.set(s.signature, so);
+      so += s.signature.length;
+      sigOff[i + 1] = so;
+      i++;
+    }
+    reqOff[r + 1] = i;
   }
+  const batch = {requestOffsets: reqOff, pkOffsets: pkOff, messages, signatures, sigOffsets: sigOff, seed};
+  if (idx) batch.pubkeyIndices = idx;
+  if (rows) batch.pubkeys = rows;
   return batch;
+}
+
+/** A key's validator index, or -1 for a key given by its bytes (a 96-byte uncompressed encoding,
+ * or an object with toBytes()). */
+function keyIndex(pk) {
+  if (pk && typeof pk.index === "number" && !(pk instanceof Uint8Array)) return pk.index;
+  if (pk instanceof Uint8Array) {
+    if (pk.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
+    return -1;
+  }
+  if (pk && typeof pk.toBytes === "function") return -1;
+  throw new TypeError("pubkey: Uint8Array(96), {index} or an object with toBytes()");
+}
+
+function keyBytes(pk) {
+  const b = pk instanceof Uint8Array ? pk : pk.toBytes(false);
+  if (!(b instanceof Uint8Array) || b.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
+  return b;
 }
 
 /** Same-message jobs -> the addon's lb_same_message_batch layout. */
 function packSameMessage(jobs, seed) {
-  const jobOff = [0];
-  const keys = [];
-  const sigs = [];
-  const sigOff = [0];
+  let nSets = 0;
+  let nIdx = 0;
   let sigBytes = 0;
   for (const job of jobs) {
     for (const s of job.sets) {
-      keys.push(pubkeyRef(s.publicKey));
-      sigs.push(s.signature);
+      if (keyIndex(s.publicKey) >= 0) nIdx++;
       sigBytes += s.signature.length;
-      sigOff.push(sigBytes);
+      nSets++;
     }
-    jobOff.push(keys.length);
   }
-  const batch = {
-    jobOffsets: Uint32Array.from(jobOff),
-    signatures: concat(sigs, sigBytes),
-    sigOffsets: Uint32Array.from(sigOff),
-    messages: concat(
-      jobs.map((j) => j.message),
-      32 * jobs.length
-    ),
-    seed,
-  };
-  if (keys.length > 0 && keys.every((k) => k.index !== undefined)) {
-    batch.pubkeyIndices = Uint32Array.from(keys.map((k) => k.index));
-  } else {
-    batch.pubkeys = concat(
-      keys.map((k) => k.bytes),
-      96 * keys.length
-    );
+  const byIndex = nSets > 0 && nIdx === nSets;
+  const jobOff = new Uint32Array(jobs.length + 1);
+  const sigOff = new Uint32Array(nSets + 1);
+  const signatures = new Uint8Array(sigBytes);
+  const messages = new Uint8Array(32 * jobs.length);
+  const idx = byIndex ? new Uint32Array(nSets) : null;
+  const pks = byIndex ? null : new Uint8Array(96 * nSets);
+  let i = 0;
+  let so = 0;
+  for (let j = 0; j < jobs.length; j++) {
+    messages.set(jobs[j].message, 32 * j);
+    for (const s of jobs[j].sets) {
+      if (byIndex) idx[i] = keyIndex(s.publicKey);
+      else {
+        const pk = s.publicKey;
+        // (a key by index alone in a package with byte keys: its bytes are needed)
+        const b = pk instanceof Uint8Array || typeof pk.toBytes === "function" ? keyBytes(pk) : pk.bytes;
+        if (!(b instanceof Uint8Array) || b.length !== 96)
+          throw new TypeError("same-message package mixing index-only and byte pubkeys");
+        pks.set(b, 96 * i);
+      }
+      signatures.set(s.signature, so);
+      so += s.signature.length;
+      sigOff[i + 1] = so;
+      i++;
+    }
+    jobOff[j + 1] = i;
   }
+  const batch = {jobOffsets: jobOff, signatures, sigOffsets: sigOff, messages, seed};
+  if (byIndex) batch.pubkeyIndices = idx;
+  else batch.pubkeys = pks;
   return batch;
 }
 
@@ -374,7 +410,7 @@ class BlsGpuVerifier {
     } else {
       if (job.opts.priority) this.jobs.unshift(job);
       else this.jobs.push(job);
-      setTimeout(this.runJob, 0);
+      this.scheduleRun();
     }
   }
 
@@ -383,7 +419,7 @@ class BlsGpuVerifier {
     for (const job of this.buffered.jobs) this.jobs.push(job);
     for (const job of this.buffered.prioritizedJobs) this.jobs.unshift(job);
     this.buffered = null;
-    setTimeout(this.runJob, 0);
+    this.scheduleRun();
   };
 
   prepareWork() {
@@ -396,6 +432,19 @@ class BlsGpuVerifier {
     }
     return jobs;
   }
+
+  /** setTimeout(runJob, 0) as the reference does after every queue change (index.ts:386,
+   * 453, 515), at most one pending: a package of 512 jobs queued at once schedules one run. */
+  scheduleRun() {
+    if (this.runScheduled) return;
+    this.runScheduled = true;
+    setTimeout(this.runJobScheduled, 0);
+  }
+
+  runJobScheduled = () => {
+    this.runScheduled = false;
+    this.runJob();
+  };
 
   runJob = () => {
     if (this.closed || this.idle.length === 0 || this.jobs.length === 0) return;
@@ -414,7 +463,7 @@ class BlsGpuVerifier {
     m.set(M.QUEUE_LENGTH, this.jobs.length);
     const p = this.dispatch(bi, jobs).finally(() => this.running.delete(p));
     this.running.add(p);
-    if (this.idle.length > 0 && this.jobs.length > 0) setTimeout(this.runJob, 0);
+    if (this.idle.length > 0 && this.jobs.length > 0) this.scheduleRun();
   };
 
   requestVerdict(r, k) {
@@ -457,7 +506,7 @@ class BlsGpuVerifier {
       this.idle.push(bi);
       m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
       for (const job of jobs) job.reject(e);
-      setTimeout(this.runJob, 0);
+      this.scheduleRun();
       return;
     }
     const backNs = hrNowNs();
@@ -516,7 +565,7 @@ class BlsGpuVerifier {
     }
     m.inc(M.SUCCESS_JOBS_SETS, success);
     m.inc(M.ERROR_JOBS_SETS, errors);
-    setTimeout(this.runJob, 0);
+    this.scheduleRun();
   }
 }
 
