@@ -152,7 +152,7 @@ def main():
     ap.add_argument("--combine", choices=["auto", "on", "off"], default="auto",
                     help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on for N > 1)")
     ap.add_argument("--inflight", type=int,
-                    default=int(os.environ.get("LB_SLOTS", min(32, max(4, int(os.environ["GPU_MAX_HW_QUEUES"]))))),
+                    default=int(os.environ.get("LB_SLOTS", min(16, max(4, int(os.environ["GPU_MAX_HW_QUEUES"]))))),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
     a = ap.parse_args()
 

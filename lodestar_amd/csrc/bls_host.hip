@@ -148,7 +148,9 @@ struct lb_ctx {
   // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
   // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
   // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
-  static constexpr int kMaxSlots = 32;
+  // (24 hardware queues failed: HSA_STATUS_ERROR_OUT_OF_RESOURCES at k_miller_acc's dispatch,
+  // whose 3.3 KB/lane private segment is reserved per queue; profiles/ab_r03/r03g_q24_fail.txt)
+  static constexpr int kMaxSlots = 16;
   int n_slots = 4;
   int streams_per_slot[kMaxSlots] = {2};  // (set for every slot in lb_create)
   Slot slots[kMaxSlots];
@@ -787,7 +789,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   // one single-stream slot per hardware queue HIP gives this process (4 by
   // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8 calls
   // in flight: 2.94 vs 2.74 M sets/s once the merged check's one-wave kernels
-  // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 32)
+  // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 16)
   if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
     const int v = atoi(e);
     ctx->n_slots = v < 4 ? 4 : v > lb_ctx::kMaxSlots ? lb_ctx::kMaxSlots : v;
