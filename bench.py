@@ -424,13 +424,14 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         return None
     dom = max(cands, key=lambda k: timing[k])
     oc = json.load(open(counts_path))
-    st = oc["stages"].get(dom)
+    pairs_org = os.environ.get("LB_ACC") == "pairs"
+    st = (oc.get("pairs_stages", oc["stages"]) if pairs_org else oc["stages"]).get(dom)
     if not st:
         return None
     per_set = st.get("mads_per_set", st["fp_mul_per_set"] * oc["mads_per_fp_mul"])
     # the iso launches are lone calls: k_miller_acc then splits requests in halves (one pair per
     # lane, its own Fp12 squarings), so its work per set is that organisation's count
-    lone = oc.get("lone_call_stages", {}).get(dom) if iso_ms else None
+    lone = oc.get("lone_call_stages", {}).get(dom) if iso_ms and pairs_org else None
     per_set_pipe = per_set
     split_env = os.environ.get("LB_ACC_SPLIT")  # bls_host.hip: 1 always, 0 never,
     split = split_env != "0" and (split_env == "1" or n_req >= 64)  # default: lone calls from 64 requests
@@ -459,12 +460,13 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         # the same kernel while other calls' kernels share the CUs (timed region, two pairs per lane)
         roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
         roof["in_pipeline_frac"] = round(per_set_pipe * n / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
-    if "mads_per_set_total" in oc:
+    tot_key = "pairs_mads_per_set_total" if pairs_org and "pairs_mads_per_set_total" in oc else "mads_per_set_total"
+    if tot_key in oc:
         # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
-        pipe = value * oc["mads_per_set_total"] / 1e12
+        pipe = value * oc[tot_key] / 1e12
         roof["pipeline_achieved"] = round(pipe, 4)
         roof["pipeline_frac"] = round(pipe / peak, 5)
-        roof["mads_per_set"] = round(oc["mads_per_set_total"])
+        roof["mads_per_set"] = round(oc[tot_key])
     return roof
 
 

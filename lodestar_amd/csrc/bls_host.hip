@@ -68,6 +68,11 @@ struct PipeState {
   uint8_t* d_valid = nullptr;
   uint8_t* d_mflag = nullptr;
   uint32_t* d_mstats = nullptr;
+  // steps organisation of the Miller accumulation (k_steps.hip): the lanes'
+  // level products G (per-request F_k only when the tails need them)
+  bool steps = false;
+  Rows rows{};
+  const uint32_t* d_G = nullptr;
 };
 
 // A same-message package in flight (lb_verify_same_message_batch[_async]):
@@ -168,6 +173,9 @@ struct lb_ctx {
   int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
   int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
   int acc_split = -1;   // LB_ACC_SPLIT: 1 always / 0 never split requests in halves; -1 = lone calls only
+  // Miller accumulation of the stored lines: 1 = step-major lanes + level products +
+  // one Horner chain (k_steps.hip, default), 0 = pair-major k_miller_acc (LB_ACC=pairs)
+  int acc_steps = 1;
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
   // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
   bool tail_wave = true;
@@ -333,6 +341,9 @@ int run_tails(lb_ctx* ctx, Slot& sl) {
     }
     LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
              p.d_lines, (const uint8_t*)p.d_mflag);
+    if (p.steps)
+      LB_STAGE("req_horner", 0, k_req_horner, p.n_req, TPB, p.n_req, p.n_sets, p.rows, p.d_req_off, p.d_G,
+               (const uint8_t*)p.d_bad, p.d_F, (const uint8_t*)p.d_mflag);
     LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
              (const fp12*)p.d_F, (const uint8_t*)p.d_bad, p.d_valid, (const uint8_t*)p.d_mflag);
     hipLaunchKernelGGL(k_merge_stats, dim3(1), dim3(TPB), 0, sl.st[0], p.n_req, p.d_req_off, (const uint8_t*)p.d_bad,
@@ -382,12 +393,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   bool lone = true;
   for (int s = 0; s < ctx->n_slots; s++)
     if (&ctx->slots[s] != &sl && ctx->slots[s].busy && ctx->slots[s].lent_to != &sl) lone = false;
-  const bool split = by_lines && (ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64));
+  // steps organisation (k_steps.hip): no split (a request already has one lane per set)
+  const bool steps = by_lines && tail_wave && n_sets && ctx->acc_steps;
+  const bool split = by_lines && !steps && (ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64));
   // merged pair (-g1, S_all) with S_all from the MSM: without a split its Miller
   // value is one extra workgroup of k_miller_acc (fold; its 512 request waves
   // leave SIMDs free), otherwise its lines are stored right after the MSM, on
   // stream 0 beside stream 1's hash/lines (lines_all), and k_tail multiplies it in
-  const bool fold = use_msm && by_lines && !split;
+  const bool fold = use_msm && by_lines && !split && !steps;
   uint32_t* d_lines =
       (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
@@ -411,6 +424,16 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2j* d_mcsum = use_msm ? ws.take<g2j>(max_chunks) : nullptr;
   g2j* d_mbsum = use_msm ? ws.take<g2j>(LB_MSM_BUCKETS) : nullptr;
   g2j* d_mG = use_msm ? ws.take<g2j>(LB_MSM_POS) : nullptr;
+  // steps organisation: size histogram + cursors, gt, row offsets, order, meta, G, level products
+  uint32_t* d_rhist = steps ? ws.take<uint32_t>(2 * ((size_t)ns + 1)) : nullptr;
+  uint32_t* d_rgt = steps ? ws.take<uint32_t>((size_t)ns + 1) : nullptr;
+  uint32_t* d_rowoff = steps ? ws.take<uint32_t>((size_t)ns + 1) : nullptr;
+  uint32_t* d_rpos = steps ? ws.take<uint32_t>(n_req) : nullptr;
+  uint32_t* d_rinv = steps ? ws.take<uint32_t>(n_req) : nullptr;
+  uint32_t* d_rmeta = steps ? ws.take<uint32_t>(1) : nullptr;
+  uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns) : nullptr;
+  fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
+  const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta};
   sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
@@ -422,6 +445,18 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, (const g2j*)d_q, d_h);
   }
   LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
+  if (steps) {  // size-descending order and row offsets (before stream 1's lines)
+    uint32_t* d_rcur = d_rhist + (ns + 1);
+    LB_HIP(hipMemsetAsync(d_rhist, 0, 2 * ((size_t)ns + 1) * sizeof(uint32_t), sl.st[0]));
+    hipLaunchKernelGGL(k_rows_hist, dim3(blocks_for(n_req, 256)), dim3(256), 0, sl.st[0], n_req, d_req_off, d_rhist);
+    LB_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(1024), 0, sl.st[0], n_sets, (const uint32_t*)d_rhist, d_rgt, d_rowoff,
+                       d_rmeta);
+    LB_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_rows_pos, dim3(blocks_for(n_req, 256)), dim3(256), 0, sl.st[0], n_req, d_req_off,
+                       (const uint32_t*)d_rgt, d_rcur, d_rpos, d_rinv);
+    LB_HIP(hipGetLastError());
+  }
   if (n_sets) {
     const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
     LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
@@ -434,7 +469,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
-  if (n_sets && (by_lines || by_wave)) {
+  if (steps) {
+    if (ctx->lines_waves == 1)
+      LB_STAGE("lines", 1, k_lines_rows<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
+               (const g1j*)d_rpk, (const g2j*)d_h, d_lines);
+    else
+      LB_STAGE("lines", 1, k_lines_rows<2>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
+               (const g1j*)d_rpk, (const g2j*)d_h, d_lines);
+  } else if (n_sets && (by_lines || by_wave)) {
     if (ctx->lines_waves == 1)
       LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
@@ -455,6 +497,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
                (const uint8_t*)d_sig_st, d_rsig, (const uint8_t*)nullptr);
   }
+  if (steps)  // request status (k_miller_acc's side reduction in the pairs organisation)
+    LB_STAGE("req_status", 0, k_req_status, n_req < 4096u ? n_req : 4096u, TPB, n_req, d_req_off,
+             (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_bad, d_req_err);
   if (use_msm) {
     // S_all = sum r_i sig_i over the good requests' sets: one bucket MSM (k_msm.hip)
     uint32_t* d_off = d_mhist + (LB_MSM_BUCKETS + 1);
@@ -479,6 +524,12 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
                (const uint8_t*)nullptr);
   } else {
     LB_STAGE("sum_tree", 0, k_sum_tree, n_req, TPB, n_req, d_req_off, (const g2j*)d_rsig, d_S, (const uint8_t*)nullptr);
+    if (steps && merged) {  // S_all of the good requests and its lines, ahead of the level products
+      LB_STAGE("merge", 0, k_merge, 1u, TPB, n_req, (const g2a*)d_S, (const fp12*)nullptr, (const uint8_t*)d_bad, d_Sall,
+               (fp12*)nullptr, (const fp12*)nullptr);
+      LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+               (const uint8_t*)nullptr);
+    }
   }
   if (tail_wave && !merged)
     LB_STAGE("lines_S", 0, k_lines_S, blocks_for(n_req), TPB, n_req, n_pairs, n_sets, (const g2a*)d_S, d_lines,
@@ -492,7 +543,18 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
   }
-  if (by_lines) {
+  if (steps) {
+    LB_STAGE("step_acc", 0, k_step_acc, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
+             (const uint32_t*)d_lines, d_G);
+    if (merged) {
+      LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, n_sets + n_req, rows, d_req_off,
+               (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
+      LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
+    } else {
+      LB_STAGE("req_horner", 0, k_req_horner, n_req, TPB, n_req, n_sets, rows, d_req_off, (const uint32_t*)d_G,
+               (const uint8_t*)d_bad, d_F, (const uint8_t*)nullptr);
+    }
+  } else if (by_lines) {
     const uint32_t nr = split ? 2 * n_req : n_req;
     const uint32_t* acc_off = d_req_off;
     fp12* acc_F = d_F;
@@ -550,6 +612,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   ps.d_valid = d_valid;
   ps.d_mflag = d_mflag;
   ps.d_mstats = d_mstats;
+  ps.steps = steps;
+  ps.rows = rows;
+  ps.d_G = d_G;
   if (merged) {
     // merged check: one tail for the whole call; per-request tails only if it fails.
     // LB_TAIL_PRIO=1 runs its chain of one-wave kernels on a shared high-priority
@@ -561,13 +626,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_HIP(hipStreamWaitEvent(ts, sl.dep[3], 0));
     }
     LB_HIP(hipMemsetAsync(d_mflag, 0, 2, ts));
-    LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, use_msm ? (const g2a*)nullptr : (const g2a*)d_S,
-                (const fp12*)d_F, (const uint8_t*)d_bad,
-                d_Sall, d_Fall, (const fp12*)d_Fx);
-    if (!use_msm)  // (with the MSM: folded into k_miller_acc, or stored right after the MSM)
-      LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
-                  (const uint8_t*)nullptr);
-    const uint32_t* merged_lines = fold ? nullptr : (const uint32_t*)d_lines;
+    if (!steps) {  // (steps: F_all from the level products and the Horner chain, S_all's lines included)
+      LB_STAGE_ON("merge", ts, k_merge, 1u, TPB, n_req, use_msm ? (const g2a*)nullptr : (const g2a*)d_S,
+                  (const fp12*)d_F, (const uint8_t*)d_bad,
+                  d_Sall, d_Fall, (const fp12*)d_Fx);
+      if (!use_msm)  // (with the MSM: folded into k_miller_acc, or stored right after the MSM)
+        LB_STAGE_ON("lines_all", ts, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
+                    (const uint8_t*)nullptr);
+    }
+    const uint32_t* merged_lines = (fold || steps) ? nullptr : (const uint32_t*)d_lines;
     if (partial) {
       // two-phase call: the merged Miller product goes to the host, which
       // combines it with the other GPUs' partials; the tails wait for its verdict
@@ -595,13 +662,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
   // (+ the bucket MSM: 2 W keys + 2 W sorted entries and 2 W / T chunk partials per set)
-  size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 +
+  // (+ the steps organisation: size histogram / cursors / gt / row offsets and the lanes' G values)
+  size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 + 16 + 576 +
                    (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 + (2 * LB_MSM_W * sizeof(g2j)) / LB_MSM_T + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
-  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
+  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
                            8 * 256;
-  return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * 256 + 4096;
+  return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -805,6 +873,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
+  if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);
     if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;

@@ -105,6 +105,15 @@ LB_DEV uint8_t pk_load(g1a& p, const PkSource& s, uint32_t k) {
   return g1_deserialize(p, s.bytes + (size_t)k * 96, 96);
 }
 
+// Row layout of the steps organisation (k_steps.hip): requests in size-descending
+// order, pair (k, i) of request k at slot rowoff[i] + pos[k]; meta[0] = rows.
+struct Rows {
+  const uint32_t* rowoff;
+  const uint32_t* inv;
+  const uint32_t* pos;
+  const uint32_t* meta;
+};
+
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint8_t* __restrict__ single_flag);
 __global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
@@ -236,6 +245,38 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t
                                                                   const g2j* __restrict__ csum, g2j* __restrict__ bsum);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_final(const g2j* __restrict__ G, g2a* __restrict__ S);
+__global__ void __launch_bounds__(256) k_rows_hist(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   uint32_t* __restrict__ hist);
+__global__ void __launch_bounds__(1024) k_rows_scan(uint32_t n_sets, const uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ gt, uint32_t* __restrict__ rowoff,
+                                                    uint32_t* __restrict__ meta);
+__global__ void __launch_bounds__(256) k_rows_pos(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                  const uint32_t* __restrict__ gt, uint32_t* __restrict__ cursor,
+                                                  uint32_t* __restrict__ pos, uint32_t* __restrict__ inv);
+template <int WAVES>
+__global__ void __launch_bounds__(TPB, WAVES) k_lines_rows(uint32_t n_sets, uint32_t n_pairs, Rows R,
+                                                           const uint32_t* __restrict__ req_off,
+                                                           const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                           uint32_t* __restrict__ lines);
+__global__ void __launch_bounds__(TPB) k_req_status(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                    const uint8_t* __restrict__ sig_status,
+                                                    const uint8_t* __restrict__ pk_status,
+                                                    uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err);
+__global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
+                                                            const uint32_t* __restrict__ req_off,
+                                                            const uint32_t* __restrict__ lines,
+                                                            uint32_t* __restrict__ G);
+__global__ void __launch_bounds__(256, 1) k_level_prod(uint32_t n_req, uint32_t n_sets, uint32_t n_pairs,
+                                                       uint32_t s_pair, Rows R, const uint32_t* __restrict__ req_off,
+                                                       const uint32_t* __restrict__ G,
+                                                       const uint8_t* __restrict__ req_bad,
+                                                       const uint32_t* __restrict__ lines, fp12* __restrict__ Pl);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_horner_all(const fp12* __restrict__ Pl, fp12* __restrict__ F_all);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, uint32_t n_sets, Rows R,
+                                                             const uint32_t* __restrict__ req_off,
+                                                             const uint32_t* __restrict__ G,
+                                                             const uint8_t* __restrict__ req_bad,
+                                                             fp12* __restrict__ F, const uint8_t* __restrict__ skip);
 __global__ void __launch_bounds__(TPB) k_msm_load(uint32_t n, const uint8_t* __restrict__ in192, g2j* __restrict__ out,
                                                   uint8_t* __restrict__ status);
 }  // namespace lb

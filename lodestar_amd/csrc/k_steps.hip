@@ -1,0 +1,398 @@
+// Step-major Miller accumulation ("steps" organisation of the stored lines).
+// Part of the MI355X BLS verification pipeline; see bls_host.hip for the DAG.
+//
+// The Miller value of a request is F_k = prod_j L_{k,j}^(2^(62 - lvl(j))) with
+// L_{k,j} = prod_{pairs i of k} l_{i,j} (68 lines j per pair; lvl(j) = number of
+// Fp12 squarings before line j).  The pair-major accumulation (k_miller_acc)
+// gives every lane a few pairs and all 68 steps, so each lane squares its
+// accumulator 62 times.  Here a lane takes 68 consecutive lines of its request
+// in step-major order -- lines t in [68 l, 68 l + 68) with j = t / n_k,
+// i = t mod n_k -- so a lane of a >= 68-set request spans at most two steps and
+// squares at most once; a request has n_k lanes (one per set, as before).
+// The squarings left are those of one Horner chain over the 63 levels per
+// merged check (k_horner_all, one wave) or per request on the failure path
+// (k_req_horner).  Work per pair: 68 x 11.5 Fp2 products instead of
+// 68 x 17.5 (two pairs per lane) or 68 x 25 (one pair per lane).
+//
+// Row layout: requests are ordered by size, descending (position pos(k)); row i
+// holds pair i of every request with n_k > i, so pair (k, i) lives at slot
+// rowoff[i] + pos(k) and the slots are exactly [0, n_sets).  A wave of 64
+// consecutive slots is 64 requests at the same lane index l: with equal sizes
+// every lane reads line (j, i) of its request at the same moment and the SoA
+// loads (word w of line j of slot q at lines[(j*72 + w)*n_pairs + q]) coalesce.
+#include "bls_kernels.h"
+#include "bls_wc12.h"
+
+namespace lb {
+
+// Levels of the 68 lines (loop order of miller_lines: the doubling line of bit
+// i = 62..0, then the addition line when bit i of |x| is set) and the first
+// line of each level (first[63] = 68).
+struct StepTab {
+  uint8_t lvl[LB_MILLER_LINES];
+  uint8_t first[64];
+};
+constexpr StepTab make_step_tab() {
+  StepTab t{};
+  int j = 0;
+  for (int i = 62; i >= 0; i--) {
+    const int l = 62 - i;
+    t.first[l] = (uint8_t)j;
+    t.lvl[j++] = (uint8_t)l;
+    if ((LB_X_ABS >> i) & 1ull) t.lvl[j++] = (uint8_t)l;
+  }
+  t.first[63] = (uint8_t)j;
+  return t;
+}
+__constant__ StepTab c_steps = make_step_tab();
+static_assert(make_step_tab().first[63] == LB_MILLER_LINES, "68 Miller lines");
+
+// ---- size-descending order of the requests and the row offsets ----------
+// hist[n] = number of requests of n sets (n <= n_sets; zeroed by the host)
+__global__ void __launch_bounds__(256) k_rows_hist(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                   uint32_t* __restrict__ hist) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n_req) atomicAdd(&hist[req_off[k + 1] - req_off[k]], 1u);
+}
+
+// gt[n] = #requests with more than n sets (= the first position of the size-n
+// requests), rowoff[i] = sum_{i' < i} gt[i'] for i in [0, n_sets], meta[0] =
+// number of rows (the largest request size).  One workgroup of 1024 threads.
+__global__ void __launch_bounds__(1024) k_rows_scan(uint32_t n_sets, const uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ gt, uint32_t* __restrict__ rowoff,
+                                                    uint32_t* __restrict__ meta) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t rmax;
+  const uint32_t m = n_sets + 1, tid = threadIdx.x;
+  const uint32_t per = (m + 1023) / 1024, b = tid * per, e = b + per < m ? b + per : m;
+  if (tid == 0) rmax = 0;
+  // suffix sums of hist: gt[n] = sum_{n' > n} hist[n']
+  uint32_t s = 0;
+  for (uint32_t n = b; n < e; n++) s += hist[n];
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive suffix scan of part
+    const uint32_t v = tid + d < 1024 ? part[tid + d] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t acc = tid + 1 < 1024 ? part[tid + 1] : 0u;  // sum over the segments after this one
+  for (uint32_t n = e; n-- > b;) {
+    gt[n] = acc;
+    acc += hist[n];
+    if (hist[n] && n > 0) atomicMax(&rmax, n);
+  }
+  __syncthreads();
+  // prefix sums of gt: rowoff[i] = sum_{i' < i} gt[i']
+  s = 0;
+  for (uint32_t n = b; n < e; n++) s += gt[n];
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive prefix scan
+    const uint32_t v = tid >= d ? part[tid - d] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  acc = tid ? part[tid - 1] : 0u;
+  for (uint32_t n = b; n < e; n++) {
+    rowoff[n] = acc;
+    acc += gt[n];
+  }
+  if (tid == 0) meta[0] = rmax;
+}
+
+// pos[k] = position of request k in the size-descending order, inv[pos] = k
+// (within one size the order is that of the atomics: any order keeps rows dense)
+__global__ void __launch_bounds__(256) k_rows_pos(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                  const uint32_t* __restrict__ gt, uint32_t* __restrict__ cursor,
+                                                  uint32_t* __restrict__ pos, uint32_t* __restrict__ inv) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_req) return;
+  const uint32_t n = req_off[k + 1] - req_off[k];
+  const uint32_t p = gt[n] + atomicAdd(&cursor[n], 1u);
+  pos[k] = p;
+  inv[p] = k;
+}
+
+// slot q -> (row i, position r): the largest i < rows with rowoff[i] <= q
+LB_DEV void slot_row(const Rows& R, uint32_t q, uint32_t& i, uint32_t& r) {
+  uint32_t lo = 0, hi = R.meta[0];  // rows [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (R.rowoff[mid] <= q)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  i = lo;
+  r = q - R.rowoff[lo];
+}
+
+// Lines of every set pair, stored at its slot: lane q is slot q (coalesced stores).
+template <int WAVES>
+__global__ void __launch_bounds__(TPB, WAVES) k_lines_rows(uint32_t n_sets, uint32_t n_pairs, Rows R,
+                                                           const uint32_t* __restrict__ req_off,
+                                                           const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                           uint32_t* __restrict__ lines) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_sets) return;
+  uint32_t i, r;
+  slot_row(R, q, i, r);
+  const uint32_t s = req_off[R.inv[r]] + i;
+  g1a p;
+  g2a h;
+  jac_pair_to_aff(p, h, P[s], Q[s]);
+  miller_lines(p, h, lines, n_pairs, q);
+}
+
+// Request status of the steps organisation (what k_miller_acc reduces on the
+// side): bad = empty request or any set not OK; the rejection code.  One wave
+// per request, grid-stride.
+__global__ void __launch_bounds__(TPB) k_req_status(uint32_t n_req, const uint32_t* __restrict__ req_off,
+                                                    const uint8_t* __restrict__ sig_status,
+                                                    const uint8_t* __restrict__ pk_status,
+                                                    uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err) {
+  for (uint32_t k = blockIdx.x; k < n_req; k += gridDim.x) {
+    const uint32_t a = req_off[k], b = req_off[k + 1];
+    bool bad = false, empty_agg = false, bad_pk = false;
+    for (uint32_t i = a + threadIdx.x; i < b; i += TPB) {
+      const uint8_t ss = sig_status[i], ps = pk_status[i];
+      bad |= ss != LB_ST_OK || ps != LB_ST_OK;
+      empty_agg |= ps == LB_ST_EMPTY_AGGREGATE;
+      bad_pk |= ps == LB_ST_BAD_ENCODING;
+    }
+    bad = __any(bad);
+    empty_agg = __any(empty_agg);
+    bad_pk = __any(bad_pk);
+    if (threadIdx.x == 0) {
+      req_bad[k] = (bad || a == b) ? 1 : 0;
+      req_err[k] = empty_agg ? LB_REQ_EMPTY_AGGREGATE : bad_pk ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+    }
+  }
+}
+
+// G of lane (request k, index l): the Horner product of its 68 lines, at the
+// level of its last line.  SoA over slots: word w at G[w * n_sets + q].
+LB_DEV void g_put(uint32_t* __restrict__ G, uint32_t n_sets, uint32_t q, const fp12& f) {
+  const uint32_t* v = &f.c0.c0.c0.l[0];
+#pragma unroll
+  for (int w = 0; w < 144; w++) G[(size_t)w * n_sets + q] = v[w];
+}
+LB_DEV void g_get(fp12& f, const uint32_t* __restrict__ G, uint32_t n_sets, uint32_t q) {
+  uint32_t* v = &f.c0.c0.c0.l[0];
+#pragma unroll
+  for (int w = 0; w < 144; w++) v[w] = G[(size_t)w * n_sets + q];
+}
+
+__global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
+                                                            const uint32_t* __restrict__ req_off,
+                                                            const uint32_t* __restrict__ lines,
+                                                            uint32_t* __restrict__ G) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_sets) return;
+  uint32_t l, r;
+  slot_row(R, q, l, r);
+  const uint32_t k = R.inv[r];
+  const uint32_t n = req_off[k + 1] - req_off[k];
+  const uint32_t t0 = (uint32_t)LB_MILLER_LINES * l;
+  uint32_t j = t0 / n, i = t0 - j * n;
+  int lvl = c_steps.lvl[j];
+  fp12 acc;
+  bool have = false;
+  fp2 l0, l1, l4;
+#pragma unroll 1
+  for (uint32_t c = 0; c < (uint32_t)LB_MILLER_LINES;) {
+    const int lj = c_steps.lvl[j];
+    if (lj != lvl) {  // one doubling step further: one squaring
+      if (have) fp12_sqr(acc, acc);
+      lvl = lj;
+    }
+    const uint32_t qa = R.rowoff[i] + r;
+    if (i + 1 < n && c + 1 < (uint32_t)LB_MILLER_LINES) {  // two lines of the same step
+      const uint32_t qb = R.rowoff[i + 1] + r;
+      fp2 m0, m1, m4, y1, y2;
+      fp6 x;
+      line_get(lines, n_pairs, qa, (int)j, l0, l1, l4);
+      line_get(lines, n_pairs, qb, (int)j, m0, m1, m4);
+      line_mul_line(x, y1, y2, l0, l1, l4, m0, m1, m4);
+      if (have) {
+        fp12_mul_by_sparse2(acc, acc, x, y1, y2);
+      } else {
+        acc.c0 = x;
+        fp2_zero(acc.c1.c0);
+        acc.c1.c1 = y1;
+        acc.c1.c2 = y2;
+        have = true;
+      }
+      i += 2;
+      c += 2;
+    } else {
+      line_get(lines, n_pairs, qa, (int)j, l0, l1, l4);
+      if (have) {
+        fp12_mul_line(acc, acc, l0, l1, l4);
+      } else {
+        fp6_zero(acc.c0);
+        fp6_zero(acc.c1);
+        acc.c0.c0 = l0;
+        acc.c0.c1 = l1;
+        acc.c1.c1 = l4;
+        have = true;
+      }
+      i += 1;
+      c += 1;
+    }
+    if (i >= n) {
+      i -= n;
+      j++;
+    }
+  }
+  g_put(G, n_sets, q, acc);
+}
+
+// [lo, hi): the lane indices l of an n-set request whose last line has level lvl
+LB_DEV void level_lanes(uint32_t n, int lvl, uint32_t& lo, uint32_t& hi) {
+  const int64_t a = (int64_t)c_steps.first[lvl] * n - (LB_MILLER_LINES - 1);
+  const int64_t b = (int64_t)c_steps.first[lvl + 1] * n - (LB_MILLER_LINES - 1);
+  lo = a <= 0 ? 0u : (uint32_t)((a + LB_MILLER_LINES - 1) / LB_MILLER_LINES);
+  hi = b <= 0 ? 0u : (uint32_t)((b + LB_MILLER_LINES - 1) / LB_MILLER_LINES);
+  if (hi > n) hi = n;
+  if (lo > hi) lo = hi;
+}
+
+// Merged check: P[lvl] = prod over the good requests' lanes at level lvl of G,
+// times the lines of level lvl of the merged pair (-g1, S_all) (slot s_pair).
+// One workgroup of LB_LVL_TPB threads per level: strided products, LDS tree.
+static constexpr int LB_LVL_TPB = 256;
+__global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, uint32_t n_sets, uint32_t n_pairs,
+                                                              uint32_t s_pair, Rows R,
+                                                              const uint32_t* __restrict__ req_off,
+                                                              const uint32_t* __restrict__ G,
+                                                              const uint8_t* __restrict__ req_bad,
+                                                              const uint32_t* __restrict__ lines,
+                                                              fp12* __restrict__ Pl) {
+  __shared__ LdsRec<fp12> sh[LB_LVL_TPB];
+  __shared__ uint8_t has[LB_LVL_TPB];
+  const int lvl = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  fp12 acc;
+  bool have = false;
+  for (uint32_t r = tid; r < n_req; r += LB_LVL_TPB) {
+    const uint32_t k = R.inv[r];
+    if (req_bad[k]) continue;
+    uint32_t lo, hi;
+    level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi);
+    for (uint32_t l = lo; l < hi; l++) {
+      fp12 g;
+      g_get(g, G, n_sets, R.rowoff[l] + r);
+      if (have) {
+        fp12_mul(acc, acc, g);
+      } else {
+        acc = g;
+        have = true;
+      }
+    }
+  }
+  if (have) sh[tid].v = acc;
+  has[tid] = have ? 1 : 0;
+  __syncthreads();
+  for (uint32_t s = LB_LVL_TPB / 2; s > 0; s >>= 1) {
+    if (tid < s && has[tid + s]) {
+      fp12 o = sh[tid + s].v;
+      if (has[tid]) {
+        fp12 m = sh[tid].v;
+        fp12_mul(m, m, o);
+        sh[tid].v = m;
+      } else {
+        sh[tid].v = o;
+        has[tid] = 1;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    have = has[0] != 0;
+    if (have) acc = sh[0].v;
+    if (s_pair != 0xffffffffu) {
+      for (int j = c_steps.first[lvl]; j < c_steps.first[lvl + 1]; j++) {
+        fp2 l0, l1, l4;
+        line_get(lines, n_pairs, s_pair, j, l0, l1, l4);
+        if (have) {
+          fp12_mul_line(acc, acc, l0, l1, l4);
+        } else {
+          fp6_zero(acc.c0);
+          fp6_zero(acc.c1);
+          acc.c0.c0 = l0;
+          acc.c0.c1 = l1;
+          acc.c1.c1 = l4;
+          have = true;
+        }
+      }
+    }
+    if (!have) fp12_one(acc);
+    Pl[lvl] = acc;
+  }
+}
+
+// F_all = conj(Horner over the 63 levels of P[lvl]) (x < 0): one wave, wave-
+// cooperative Fp12 (62 squarings + 62 products on the merged check's path).
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_horner_all(const fp12* __restrict__ Pl, fp12* __restrict__ F_all) {
+  __shared__ wc_smem S;
+  wc_init_tables(S);
+  wc_load12(S, WC_ACC, Pl[0]);
+#pragma unroll 1
+  for (int l = 1; l < 63; l++) {
+    wc_apply(S, LB_WC_SQR, WC_ACC, WC_ACC, WC_ACC);
+    wc_load12(S, WC_T0, Pl[l]);
+    wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_T0);
+  }
+  wc_apply(S, LB_WC_CONJ, WC_ACC, WC_ACC, WC_ACC);
+  if (threadIdx.x < 12) (&F_all->c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
+}
+
+// Per-request F_k (the failure path of a merged check, or every request of an
+// unmerged call): one wave per request, Horner over its lanes' G values.
+// skip (optional): nonzero when the merged check passed -> nothing to do.
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, uint32_t n_sets, Rows R,
+                                                             const uint32_t* __restrict__ req_off,
+                                                             const uint32_t* __restrict__ G,
+                                                             const uint8_t* __restrict__ req_bad,
+                                                             fp12* __restrict__ F, const uint8_t* __restrict__ skip) {
+  __shared__ wc_smem S;
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req || (skip && *skip) || req_bad[k]) return;  // (uniform per workgroup)
+  const uint32_t n = req_off[k + 1] - req_off[k], r = R.pos[k];
+  wc_init_tables(S);
+  bool started = false;
+#pragma unroll 1
+  for (int lvl = 0; lvl < 63; lvl++) {
+    if (started) wc_apply(S, LB_WC_SQR, WC_ACC, WC_ACC, WC_ACC);
+    uint32_t lo, hi;
+    level_lanes(n, lvl, lo, hi);
+    for (uint32_t l = lo; l < hi; l++) {
+      const int dst = started ? WC_T0 : WC_ACC;
+      if (threadIdx.x < 12) {
+        fp v;
+        const size_t q = (size_t)R.rowoff[l] + r;
+#pragma unroll
+        for (int w = 0; w < 12; w++) v.l[w] = G[(size_t)(12 * threadIdx.x + w) * n_sets + q];
+        S.slot[dst][threadIdx.x] = v;
+      }
+      __syncthreads();
+      if (started) wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_T0);
+      started = true;
+    }
+  }
+  if (!started) wc_set_one(S, WC_ACC);
+  wc_apply(S, LB_WC_CONJ, WC_ACC, WC_ACC, WC_ACC);
+  if (threadIdx.x < 12) (&F[k].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
+}
+
+#define LB_INST_LINES_ROWS(W)                                                                                    \
+  template __global__ void k_lines_rows<W>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,                \
+                                           const g1j* __restrict__, const g2j* __restrict__, uint32_t* __restrict__);
+LB_INST_LINES_ROWS(1)
+LB_INST_LINES_ROWS(2)
+
+}  // namespace lb

@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_pair_wc(uint32_t n, uint32_t
 // S_all = sum S_k and F_all = prod F_k over the requests not already false.
 // S == nullptr: S_all already came from the bucket MSM (k_msm_final); only F_all.
 // Fx != nullptr: Miller(-g1, S_all) computed by k_miller_acc, multiplied in.
+// F == nullptr: S_all only (the steps organisation forms F_all by levels, k_steps.hip).
 // One wave; the tail kernel then verifies (F_all, S_all) once, and the
 // per-request tails only run if that merged check fails.
 // The worker's bookkeeping of its merged batch (worker.ts:66-85): batchRetries
@@ -155,8 +156,10 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
       const g2a s = S[k];
       if (!s.inf) jac_add_aff(acc, acc, s);
     }
-    fp12 t = F[k];
-    fp12_mul(f, f, t);
+    if (F) {
+      fp12 t = F[k];
+      fp12_mul(f, f, t);
+    }
   }
   shs[threadIdx.x].v = acc;
   shf[threadIdx.x].v = f;
@@ -168,9 +171,11 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
         jac_add(m, m, o);
         shs[threadIdx.x].v = m;
       }
-      fp12 a = shf[threadIdx.x].v, b = shf[threadIdx.x + st].v;
-      fp12_mul(a, a, b);
-      shf[threadIdx.x].v = a;
+      if (F) {
+        fp12 a = shf[threadIdx.x].v, b = shf[threadIdx.x + st].v;
+        fp12_mul(a, a, b);
+        shf[threadIdx.x].v = a;
+      }
     }
     __syncthreads();
   }
@@ -181,7 +186,7 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const 
       jac_to_aff(sa, tot);
       S_all[0] = sa;
     }
-    F_all[0] = shf[0].v;
+    if (F) F_all[0] = shf[0].v;
   }
 }
 

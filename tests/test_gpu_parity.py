@@ -321,8 +321,8 @@ def test_mixed_workload_vs_c_oracle(device_modes, mixed_workload):
 
 @pytest.mark.parametrize("split,tail_prio", [("1", "0"), ("0", "0"), ("0", "1")])
 def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split, tail_prio):
-    """The Miller accumulation with every request split in two halves (what a lone
-    large call on an idle GPU runs: k_split_requests / k_join_halves, LB_ACC_SPLIT=1)
+    """The pair-major Miller accumulation (k_miller_acc, LB_ACC=pairs) with every
+    request split in two halves (k_split_requests / k_join_halves, LB_ACC_SPLIT=1)
     and never split, both forced onto the stored-lines organisation, and the merged
     check on the shared high-priority stream (LB_TAIL_PRIO=1): verdicts and
     rejection codes == the C oracle's (1-set requests have an empty half)."""
@@ -330,8 +330,8 @@ def test_mixed_workload_split_halves_vs_c_oracle(mixed_workload, split, tail_pri
 
     from lodestar_amd.native import Device
     from oracle import c_oracle as C
-    old = {k: os.environ.get(k) for k in ("LB_MILLER", "LB_ACC_SPLIT", "LB_TAIL_PRIO")}
-    os.environ.update(LB_MILLER="lines", LB_ACC_SPLIT=split, LB_TAIL_PRIO=tail_prio)
+    old = {k: os.environ.get(k) for k in ("LB_MILLER", "LB_ACC_SPLIT", "LB_TAIL_PRIO", "LB_ACC")}
+    os.environ.update(LB_MILLER="lines", LB_ACC_SPLIT=split, LB_TAIL_PRIO=tail_prio, LB_ACC="pairs")
     try:
         dev = Device(0)
     finally:
@@ -401,3 +401,58 @@ def mixed_workload_cache(device, inject):
     if inject not in _MIXED:
         _MIXED[inject] = _mixed_workload(device, inject=inject)
     return _MIXED[inject]
+
+
+@pytest.mark.parametrize("msm,merge", [("0", "8"), ("1", "8"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("inject", [True, False])
+def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
+    """The step-major Miller accumulation (k_steps.hip: requests ordered by size,
+    68 consecutive lines per lane, level products, one Horner chain), forced onto
+    this 1,500-set call of ragged requests (1 .. 128 sets): merged check with S_all
+    from the per-request sums (LB_MSM_MIN=0) or the bucket MSM (1), merged check
+    passing (no injections) or failing (per-request Horner values, k_req_horner), and
+    no merged check at all (LB_MERGE_MIN=0: every request's tail).  Verdicts and
+    rejection codes == the C oracle's."""
+    from oracle import c_oracle as C
+    args = mixed_workload_cache(device, inject)
+    seed = hashlib.sha256(b"steps-seed" + msm.encode() + merge.encode()).digest()
+    dev = _device_with_env(LB_MILLER="lines", LB_MSM_MIN=msm, LB_MERGE_MIN=merge)
+    try:
+        res = dev.verify_requests(*args, seed)
+        stages = dict(dev.last_stage_times())
+        valid, err = C.verify_requests(*args, seed, threads=16)
+        assert list(res.errors) == list(err)
+        assert list(res.valid) == list(valid)
+        assert "step_acc" in stages and "miller_acc" not in stages
+        if merge != "0":
+            assert "horner_all" in stages and "req_horner" in stages  # (skips itself when the check passes)
+            assert res.batch_retries == (1 if inject else 0)
+        else:
+            assert "req_horner" in stages and "horner_all" not in stages
+    finally:
+        dev.close()
+
+
+def test_steps_uniform_and_single_requests_vs_c_oracle(device):
+    """Row layout edge cases of the steps organisation: equal-size requests (the
+    coalesced C2 shape), one-set requests (a lane runs the whole Miller loop), a
+    request larger than 68 sets next to small ones, and an empty request."""
+    from oracle import c_oracle as C
+    req_off, pks, pk_off, msgs, blob, offs = mixed_workload_cache(device, True)
+    n = len(pk_off) - 1
+    sizes = [128] * 6 + [1] * 40 + [300, 0, 2, 67, 68, 69]
+    off = [0]
+    for z in sizes:
+        off.append(min(n, off[-1] + z))
+    off[-1] = n
+    seed = hashlib.sha256(b"steps-rows").digest()
+    dev = _device_with_env(LB_MILLER="lines")
+    try:
+        ro = np.array(off, np.uint32)
+        res = dev.verify_requests(ro, pks, pk_off, msgs, blob, offs, seed)
+        valid, err = C.verify_requests(ro, pks, pk_off, msgs, blob, offs, seed, threads=16)
+        assert list(res.errors) == list(err)
+        assert list(res.valid) == list(valid)
+        assert "step_acc" in dict(dev.last_stage_times())
+    finally:
+        dev.close()

@@ -51,9 +51,11 @@ def main():
            for i in range(n)]
     msgs = [hashlib.sha256(b"opcount" + i.to_bytes(8, "little")).digest() for i in range(n)]
 
-    def count(split):
-        # LB_ACC_SPLIT=0: two pairs per lane in k_miller_acc (calls overlapped, the timed region);
-        # 1: requests split in halves, one pair per lane (a lone call: the roofline's iso launch)
+    def count(acc, split=0):
+        # LB_ACC=steps (default): step-major lanes + level products + one Horner chain (k_steps.hip);
+        # LB_ACC=pairs: k_miller_acc with LB_ACC_SPLIT=0: two pairs per lane (calls overlapped) or
+        # 1: requests split in halves, one pair per lane (what a lone call ran in that organisation)
+        os.environ["LB_ACC"] = acc
         os.environ["LB_ACC_SPLIT"] = str(split)
         dev = native.Device(0)
         pks = dev.sk_to_pk(sks)
@@ -77,16 +79,21 @@ def main():
                              "mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n}
         return per, tot_mul, tot_sqr
 
-    per, tot_mul, tot_sqr = count(0)
-    lone, _, _ = count(1)
+    per, tot_mul, tot_sqr = count("steps")
+    pairs, p_mul, p_sqr = count("pairs", 0)
+    lone, _, _ = count("pairs", 1)
     n_req = n // a.per_request
     out = {"sets": n, "requests": n_req, "sets_per_request": a.per_request, "mads_per_fp_mul": MADS_PER_FPMUL,
            "mads_per_fp_sqr": MADS_PER_FPSQR,
-           "organisation": "LB_MILLER=lines, merged check, two pairs per lane in k_miller_acc (LB_ACC_SPLIT=0)",
+           "organisation": "LB_MILLER=lines, merged check, steps organisation of the Miller accumulation "
+                           "(k_step_acc + k_level_prod + k_horner_all, k_steps.hip)",
            "stages": per, "fp_mul_per_set_total": (tot_mul + tot_sqr) / n,
            "mads_per_set_total": (tot_mul * MADS_PER_FPMUL + tot_sqr * MADS_PER_FPSQR) / n,
-           "lone_call_organisation": "LB_ACC_SPLIT=1: requests split in halves, one pair per lane (what a lone "
-                                     "call runs, e.g. bench.py's iso launches)",
+           "pairs_organisation": "LB_ACC=pairs LB_ACC_SPLIT=0: k_miller_acc, two pairs per lane (rounds 2-3)",
+           "pairs_stages": pairs,
+           "pairs_mads_per_set_total": (p_mul * MADS_PER_FPMUL + p_sqr * MADS_PER_FPSQR) / n,
+           "lone_call_organisation": "LB_ACC=pairs LB_ACC_SPLIT=1: requests split in halves, one pair per lane "
+                                     "(what a lone call ran in the pairs organisation)",
            "lone_call_stages": {k: {"mads_per_set": v["mads_per_set"]} for k, v in lone.items()}}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
