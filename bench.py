@@ -295,13 +295,28 @@ def main():
         elapsed = float(tt.item())
     ok = all(bool(v.cpu().numpy().all()) for v in d_valid) and not any(bool(e.cpu().numpy().any()) for e in d_err)
 
-    # the same call, one at a time: per-kernel durations without other calls'
-    # kernels sharing the CUs (the roofline of the dominant kernel is priced on these)
+    # the same call, one at a time and on ONE stream (a context with LB_DAG=0: no kernel of
+    # the other DAG branch and no other call beside it): every kernel's duration alone on the
+    # GPU (the roofline of the dominant kernel is priced on these)
     iso = {}
-    for k in range(a.iso_reps):
-        step(k)
-        for name, ms in dev.last_stage_times():
-            iso.setdefault(name, []).append(ms)
+    if a.iso_reps > 0:
+        old_dag = os.environ.get("LB_DAG")
+        os.environ["LB_DAG"] = "0"
+        try:
+            iso_dev = Device(gpu)
+        finally:
+            if old_dag is None:
+                os.environ.pop("LB_DAG", None)
+            else:
+                os.environ["LB_DAG"] = old_dag
+        for k in range(a.iso_reps + 1):  # (+1: the context's first call is a warm-up)
+            iso_dev.verify_requests_device(n_req, n, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
+                                           d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
+                                           d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
+            if k:
+                for name, ms in iso_dev.last_stage_times():
+                    iso.setdefault(name, []).append(ms)
+        iso_dev.close()
     iso_ms = {k: float(np.median(v)) for k, v in iso.items()}
 
     # p50 latency of one 128-set batch (one request)
@@ -448,8 +463,9 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
             "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
             "algorithmic_mads_per_launch": mads,
             "launch_ms": round(timing[dom], 3),
-            "timing": "median of %d one-at-a-time calls after the timed region (HIP events on the "
-                      "kernel's stream)" % iso_reps if iso_ms else "timed region, calls overlapped"}
+            "timing": "median of %d one-at-a-time single-stream calls after the timed region (LB_DAG=0: "
+                      "the kernel alone on the GPU; HIP events on its stream)" % iso_reps
+                      if iso_ms else "timed region, calls overlapped"}
     if per_set != per_set_pipe:
         roof["organisation"] = ("lone call: requests split in halves, one pair per lane "
                                 "(profiles/op_counts.json lone_call_stages)")

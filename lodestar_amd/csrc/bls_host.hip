@@ -176,6 +176,11 @@ struct lb_ctx {
   // Miller accumulation of the stored lines: 1 = step-major lanes + level products +
   // one Horner chain (k_steps.hip, default), 0 = pair-major k_miller_acc (LB_ACC=pairs)
   int acc_steps = 1;
+  // LB_DAG=0: a call never borrows a second stream (every kernel of a lone call runs
+  // alone on the GPU: bench.py's per-kernel iso timings and their rocprof profile)
+  bool dag = true;
+  // LB_STEP_LDS=1: k_step_acc keeps its accumulator in LDS instead of registers
+  bool step_lds = false;
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
   // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
   bool tail_wave = true;
@@ -401,6 +406,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // leave SIMDs free), otherwise its lines are stored right after the MSM, on
   // stream 0 beside stream 1's hash/lines (lines_all), and k_tail multiplies it in
   const bool fold = use_msm && by_lines && !split && !steps;
+  // (steps + merged: the merged pair's lines come from a one-lane kernel before the
+  // accumulation; as an extra workgroup of k_step_acc they measured 4.8 -> 8.2 ms: the
+  // 1,025th wave waits for a SIMD of the 1,024 set waves, then runs the 3.4 ms line chain)
   uint32_t* d_lines =
       (by_lines || by_wave || tail_wave) ? ws.take<uint32_t>((size_t)n_pairs * LB_MILLER_LINES * 72) : nullptr;
   uint8_t* d_single = ws.take<uint8_t>(ns);
@@ -544,8 +552,12 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     return LB_ERR_OUT_OF_MEMORY;
   }
   if (steps) {
-    LB_STAGE("step_acc", 0, k_step_acc, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
-             (const uint32_t*)d_lines, d_G);
+    if (ctx->step_lds)
+      LB_STAGE("step_acc", 0, k_step_acc<true>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
+               (const uint32_t*)d_lines, d_G);
+    else
+      LB_STAGE("step_acc", 0, k_step_acc<false>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
+               (const uint32_t*)d_lines, d_G);
     if (merged) {
       LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, n_sets + n_req, rows, d_req_off,
                (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
@@ -768,7 +780,7 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
 // the signature / MSM branch), so it borrows an idle slot's stream; the next call
 // that wants that slot waits for this one first (finish_slot).
 void borrow_idle_stream(lb_ctx* ctx, Slot& sl) {
-  if (sl.st[1] != sl.st[0] || sl.borrowed) return;
+  if (!ctx->dag || sl.st[1] != sl.st[0] || sl.borrowed) return;
   Slot* idle = nullptr;
   for (int s = 0; s < ctx->n_slots; s++) {
     Slot& o = ctx->slots[s];
@@ -819,7 +831,7 @@ struct BorrowGuard {
 };
 int borrow_second_stream(lb_ctx* ctx, BorrowGuard& g) {
   Slot& s0 = ctx->slots[0];
-  if (ctx->streams_per_slot[0] == 1 && ctx->n_slots >= 2) {
+  if (ctx->dag && ctx->streams_per_slot[0] == 1 && ctx->n_slots >= 2) {
     LB_TRY(finish_slot(ctx, ctx->slots[1]));
     s0.st[1] = ctx->slots[1].st[0];
     g.active = true;
@@ -874,6 +886,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
+  if (const char* e = getenv("LB_DAG")) ctx->dag = atoi(e) != 0;
+  if (const char* e = getenv("LB_STEP_LDS")) ctx->step_lds = atoi(e) != 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);
     if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;

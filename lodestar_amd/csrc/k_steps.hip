@@ -186,27 +186,81 @@ LB_DEV void g_get(fp12& f, const uint32_t* __restrict__ G, uint32_t n_sets, uint
   for (int w = 0; w < 144; w++) v[w] = G[(size_t)w * n_sets + q];
 }
 
-__global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
-                                                            const uint32_t* __restrict__ req_off,
-                                                            const uint32_t* __restrict__ lines,
-                                                            uint32_t* __restrict__ G) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= n_sets) return;
-  uint32_t l, r;
-  slot_row(R, q, l, r);
-  const uint32_t k = R.inv[r];
-  const uint32_t n = req_off[k + 1] - req_off[k];
-  const uint32_t t0 = (uint32_t)LB_MILLER_LINES * l;
+// The lane's 68 lines (from line t0 = 68 l of its n-set request, step-major),
+// accumulated with the in-lane Horner rule; Acc holds the accumulator: registers
+// (AccReg) or this lane's LDS record (AccLds: each half of f read where it is used,
+// so its 144 registers leave the peak register set of the sparse product).
+struct AccReg {
+  fp12 f;
+  LB_DEV void sqr() { fp12_sqr(f, f); }
+  LB_DEV void mul_line(const fp2& l0, const fp2& l1, const fp2& l4) { fp12_mul_line(f, f, l0, l1, l4); }
+  LB_DEV void mul_sparse2(const fp6& x, const fp2& y1, const fp2& y2) { fp12_mul_by_sparse2(f, f, x, y1, y2); }
+  LB_DEV void set(const fp12& v) { f = v; }
+  LB_DEV void get(fp12& v) const { v = f; }
+};
+#define LB_LDS_FENCE() asm volatile("" ::: "memory")
+struct AccLds {
+  fp12* A;
+  LB_DEV void sqr() {
+    fp12 t = *A;
+    fp12_sqr(t, t);
+    *A = t;
+    LB_LDS_FENCE();
+  }
+  LB_DEV void mul_line(const fp2& l0, const fp2& l1, const fp2& l4) {
+    fp12 t = *A;
+    fp12_mul_line(t, t, l0, l1, l4);
+    *A = t;
+    LB_LDS_FENCE();
+  }
+  // fp12_mul_by_sparse2's formulas (17 Fp2 products), halves of f loaded per use
+  LB_DEV void mul_sparse2(const fp6& x, const fp2& y1, const fp2& y2) {
+    fp6 t1, s, t0, sm;
+    {
+      const fp6 c1 = A->c1;
+      fp6_mul_12(t1, c1, y1, y2);
+    }
+    LB_LDS_FENCE();
+    {
+      const fp6 c0 = A->c0, c1 = A->c1;
+      fp6_add(s, c0, c1);
+    }
+    sm.c0 = x.c0;
+    fp2_add(sm.c1, x.c1, y1);
+    fp2_add(sm.c2, x.c2, y2);
+    fp6_mul(s, s, sm);
+    LB_LDS_FENCE();
+    {
+      const fp6 c0 = A->c0;
+      fp6_mul(t0, c0, x);
+    }
+    fp6_sub(s, s, t0);
+    fp6_sub(s, s, t1);
+    A->c1 = s;
+    fp6_mul_v(t1, t1);
+    fp6_add(t0, t0, t1);
+    A->c0 = t0;
+    LB_LDS_FENCE();
+  }
+  LB_DEV void set(const fp12& v) {
+    *A = v;
+    LB_LDS_FENCE();
+  }
+  LB_DEV void get(fp12& v) const { v = *A; }
+};
+
+template <class Acc>
+LB_DEV void step_lines(Acc& acc, const uint32_t* __restrict__ lines, uint32_t n_pairs, const Rows& R, uint32_t r,
+                       uint32_t n, uint32_t t0) {
   uint32_t j = t0 / n, i = t0 - j * n;
   int lvl = c_steps.lvl[j];
-  fp12 acc;
   bool have = false;
   fp2 l0, l1, l4;
 #pragma unroll 1
   for (uint32_t c = 0; c < (uint32_t)LB_MILLER_LINES;) {
     const int lj = c_steps.lvl[j];
     if (lj != lvl) {  // one doubling step further: one squaring
-      if (have) fp12_sqr(acc, acc);
+      if (have) acc.sqr();
       lvl = lj;
     }
     const uint32_t qa = R.rowoff[i] + r;
@@ -218,12 +272,14 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uin
       line_get(lines, n_pairs, qb, (int)j, m0, m1, m4);
       line_mul_line(x, y1, y2, l0, l1, l4, m0, m1, m4);
       if (have) {
-        fp12_mul_by_sparse2(acc, acc, x, y1, y2);
+        acc.mul_sparse2(x, y1, y2);
       } else {
-        acc.c0 = x;
-        fp2_zero(acc.c1.c0);
-        acc.c1.c1 = y1;
-        acc.c1.c2 = y2;
+        fp12 v;
+        v.c0 = x;
+        fp2_zero(v.c1.c0);
+        v.c1.c1 = y1;
+        v.c1.c2 = y2;
+        acc.set(v);
         have = true;
       }
       i += 2;
@@ -231,13 +287,15 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uin
     } else {
       line_get(lines, n_pairs, qa, (int)j, l0, l1, l4);
       if (have) {
-        fp12_mul_line(acc, acc, l0, l1, l4);
+        acc.mul_line(l0, l1, l4);
       } else {
-        fp6_zero(acc.c0);
-        fp6_zero(acc.c1);
-        acc.c0.c0 = l0;
-        acc.c0.c1 = l1;
-        acc.c1.c1 = l4;
+        fp12 v;
+        fp6_zero(v.c0);
+        fp6_zero(v.c1);
+        v.c0.c0 = l0;
+        v.c0.c1 = l1;
+        v.c1.c1 = l4;
+        acc.set(v);
         have = true;
       }
       i += 1;
@@ -248,7 +306,33 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uin
       j++;
     }
   }
-  g_put(G, n_sets, q, acc);
+}
+
+// LDS = true: the accumulator lives in LDS (one 592-byte record per lane, 37 KB per wave,
+// four waves per CU at one wave per SIMD) instead of registers (LB_STEP_LDS=1).
+template <bool LDS>
+__global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
+                                                            const uint32_t* __restrict__ req_off,
+                                                            const uint32_t* __restrict__ lines,
+                                                            uint32_t* __restrict__ G) {
+  __shared__ LdsRec<fp12> sacc[LDS ? TPB : 1];
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_sets) return;
+  uint32_t l, r;
+  slot_row(R, q, l, r);
+  const uint32_t k = R.inv[r];
+  const uint32_t n = req_off[k + 1] - req_off[k];
+  fp12 out;
+  if constexpr (LDS) {
+    AccLds acc{&sacc[threadIdx.x].v};
+    step_lines(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    acc.get(out);
+  } else {
+    AccReg acc;
+    step_lines(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    acc.get(out);
+  }
+  g_put(G, n_sets, q, out);
 }
 
 // [lo, hi): the lane indices l of an n-set request whose last line has level lvl
@@ -389,6 +473,10 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
   if (threadIdx.x < 12) (&F[k].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
 }
 
+template __global__ void k_step_acc<false>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,
+                                           const uint32_t* __restrict__, uint32_t* __restrict__);
+template __global__ void k_step_acc<true>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,
+                                          const uint32_t* __restrict__, uint32_t* __restrict__);
 #define LB_INST_LINES_ROWS(W)                                                                                    \
   template __global__ void k_lines_rows<W>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,                \
                                            const g1j* __restrict__, const g2j* __restrict__, uint32_t* __restrict__);

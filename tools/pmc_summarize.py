@@ -18,12 +18,14 @@ from collections import defaultdict
 
 STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
     "hash_half": "k_hash_half", "hash_finish": "k_hash_finish", "req_flags": "k_req_flags",
-    "pubkeys": "k_pubkeys_single", "scalar_pk": "k_scalar_pk", "lines": "k_lines",
+    "pubkeys": "k_pubkeys_single", "scalar_pk": "k_scalar_pk", "lines": ("k_lines_rows", "k_lines"),
     "decode_sigs": "k_decode_sigs", "scalar_sig": "k_scalar_sig", "sum_tree": "k_sum_tree",
     "miller_acc": "k_miller_acc", "merge": "k_merge", "lines_S": "k_lines_S", "tail": "k_tail",
     "miller_wave": "k_pair_wc", "pubkeys_agg": "k_pubkeys_agg",
     "msm_digits": "k_msm_scalars", "msm_chunks": "k_msm_chunks", "msm_buckets": "k_msm_buckets",
     "msm_bits": "k_msm_bits", "msm_final": "k_msm_final", "msm_scatter": "k_msm_scatter",
+    "step_acc": "k_step_acc", "level_prod": "k_level_prod", "horner_all": "k_horner_all",
+    "req_status": "k_req_status", "req_horner": "k_req_horner", "lines_all": "k_lines_S",
 }
 
 
@@ -39,6 +41,8 @@ ALG_BYTES_PER_SET = {
     "scalar_sig": 288 + 288,          # sigma -> r sigma
     "lines": 144 + 288 + 68 * 288,    # r pk, H -> 68 lines
     "miller_acc": 68 * 288 + 2,       # lines (+ statuses) -> per-request F_k
+    "step_acc": 68 * 288 + 576,       # a lane's 68 lines -> its level product G (one lane per set)
+    "level_prod": 576,                # every G read once
     # bucket MSM: 6 entries per set (2 half-points x 3 windows), each a 4-byte sorted
     # index and the point's affine (x, y) = 192 B, and 6/16 chunk partials (288 B)
     "msm_chunks": 6 * (4 + 192) + 6 * 288 // 16,
@@ -66,10 +70,11 @@ def main():
             full[k] = row["Kernel_Name"]
             vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"_note": __doc__.strip().split("\n\n")[1].replace("\n", " ")}
-    for stage, prefix in STAGE_OF.items():
-        if prefix not in vals:
+    for stage, prefixes in STAGE_OF.items():
+        found = [p for p in (prefixes if isinstance(prefixes, tuple) else (prefixes,)) if p in vals]
+        if not found:
             continue
-        k = prefix
+        k = found[0]
         c = {n: sum(v) / len(v) for n, v in vals[k].items()}
         ent = {"kernel": full[k].split("(")[0], "counters": {n: round(x, 3) for n, x in c.items()}}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
