@@ -148,6 +148,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the secondary legs (host API, same-message, ...)")
+    ap.add_argument("--node-rounds", type=int, default=96,
+                    help="node leg: rounds of 512 x 128-set jobs (one 65,536-set package each) queued at once "
+                         "(enough packages past the 16 in flight that filling and draining the pipe is small)")
     ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
     ap.add_argument("--combine", choices=["auto", "on", "off"], default="auto",
                     help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on for N > 1)")
@@ -361,6 +364,11 @@ def main():
     legs = {}
     if world == 1 and not a.no_legs:
         legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off)
+        # the node leg runs with this process's context closed: two processes with 16 HIP
+        # hardware queues each oversubscribe the GPU's queue scheduler (the node p50s went
+        # 20 -> 39 ms with the bench's context alive)
+        dev.close()
+        legs["node"] = node_leg(pks, msgs, sigs, a.node_rounds)
 
     if rank != 0:
         if world > 1:
@@ -530,6 +538,23 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
     el = time.perf_counter() - t1
     legs["host_api"] = {"sets_per_s": round(n * reps / el, 1), "calls": reps, "all_valid": allv,
                         "api": f"lb_verify_requests_async, host buffers, {nbuf} calls in flight (PCIe included)"}
+    # (1b) the same with pubkeys by validator index into the device table (what the node
+    # leg's BlsGpuVerifier sends): the library side of the Lodestar path without JS
+    base = dev.pubkey_table_size()
+    dev.pubkey_table_append(pks)
+    idx = np.arange(base, base + n, dtype=np.uint32)
+    pend, allv = [], True
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        pend.append(dev.verify_requests_async(req_off, None, None, mg_h, blob_h, sig_off, seed, pk_indices=idx))
+        if len(pend) >= nbuf:
+            allv &= bool(dev.wait_call(pend.pop(0)).valid.all())
+    for pc in pend:
+        allv &= bool(dev.wait_call(pc).valid.all())
+    el = time.perf_counter() - t1
+    legs["host_api_indexed"] = {"sets_per_s": round(n * reps / el, 1), "calls": reps, "all_valid": allv,
+                                "api": f"lb_verify_requests_async, host buffers, pubkeys by validator index, "
+                                       f"{nbuf} calls in flight"}
     # (2) adversarial: one wrong-message set per call -> merged check fails, every request's tail runs
     bad = bytearray(b"".join(msgs))
     bad[32 * (n // 2):32 * (n // 2) + 32] = hashlib.sha256(b"wrong").digest()
@@ -590,7 +615,6 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
     for pc in pend:
         allv &= all(dev.wait_same_message(pc)[1])
     el = time.perf_counter() - t1
-    legs["node"] = node_leg(pks, msgs, sigs)
     legs["same_message_inflight"] = {"sets_per_s": round(n_jobs * per_job * reps / el, 1), "packages": reps,
                                      "all_fast": bool(allv), "jobs": n_jobs, "sets_per_job": per_job,
                                      "api": f"lb_verify_same_message_batch_async, {nbuf} packages in flight "

@@ -179,6 +179,12 @@ int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* batch, 
 int lb_verify_requests_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* out_request_valid,
                              uint8_t* out_request_error, uint8_t* out_set_status, uint64_t* out_ticket);
 int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats);
+/* Non-blocking completion test of an async call: *out_done = 1 when lb_wait(ticket)
+ * would return without waiting (the call's device work is complete, or it has
+ * retired), 0 while it runs (also launches a finished same-message phase 1's
+ * retries).  Lets a submission thread keep submitting while calls run (the N-API
+ * addon's worker loop) instead of blocking on the oldest call. */
+int lb_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_done);
 
 /*
  * Multi-GPU combine (BASELINE north_star: "the per-GPU

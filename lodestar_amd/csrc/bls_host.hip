@@ -1270,6 +1270,28 @@ int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* ou
   return LB_OK;
 }
 
+int lb_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_done) {
+  if (!ctx || !out_done) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
+  *out_done = 1;
+  Slot* sl = slot_of_ticket(ctx, ticket);
+  if (!sl) return LB_OK;  // retired
+  // (a same-message package's phase 1 still running: sm_pump above found it unfinished;
+  // in phase 2 its retries' end event decides)
+  if (sl->partial_pending || (sl->sm.active && sl->sm.phase == 1)) {
+    *out_done = 0;
+    return LB_OK;
+  }
+  const hipError_t q = hipEventQuery(sl->done);
+  if (q == hipErrorNotReady) {
+    *out_done = 0;
+    return LB_OK;
+  }
+  LB_HIP(q);
+  return LB_OK;
+}
+
 int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));

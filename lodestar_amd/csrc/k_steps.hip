@@ -362,21 +362,34 @@ __global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, ui
   const uint32_t tid = threadIdx.x;
   fp12 acc;
   bool have = false;
-  for (uint32_t r = tid; r < n_req; r += LB_LVL_TPB) {
+  auto take = [&](uint32_t q) {
+    fp12 g;
+    g_get(g, G, n_sets, q);
+    if (have) {
+      fp12_mul(acc, acc, g);
+    } else {
+      acc = g;
+      have = true;
+    }
+  };
+  // requests in size-descending order: the large ones first, their lanes of this level
+  // spread over all threads (a request of thousands of sets has tens of lanes per level),
+  // then one request per thread
+  uint32_t r0 = 0;
+  for (; r0 < n_req; r0++) {
+    const uint32_t k = R.inv[r0], n = req_off[k + 1] - req_off[k];
+    if (n <= 16u * LB_MILLER_LINES) break;
+    if (req_bad[k]) continue;
+    uint32_t lo, hi;
+    level_lanes(n, lvl, lo, hi);
+    for (uint32_t l = lo + tid; l < hi; l += LB_LVL_TPB) take(R.rowoff[l] + r0);
+  }
+  for (uint32_t r = r0 + tid; r < n_req; r += LB_LVL_TPB) {
     const uint32_t k = R.inv[r];
     if (req_bad[k]) continue;
     uint32_t lo, hi;
     level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi);
-    for (uint32_t l = lo; l < hi; l++) {
-      fp12 g;
-      g_get(g, G, n_sets, R.rowoff[l] + r);
-      if (have) {
-        fp12_mul(acc, acc, g);
-      } else {
-        acc = g;
-        have = true;
-      }
-    }
+    for (uint32_t l = lo; l < hi; l++) take(R.rowoff[l] + r);
   }
   if (have) sh[tid].v = acc;
   has[tid] = have ? 1 : 0;

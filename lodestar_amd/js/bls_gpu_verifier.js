@@ -489,7 +489,9 @@ class BlsGpuVerifier {
         const [s0, ns0] = process.hrtime(t0);
         if (def.some((j) => j.sets.some((x) => x.type === "aggregate")))
           m.observe(M.PUBKEYS_AGGREGATION_MAIN_THREAD, s0 + ns0 / 1e9);
+        const packedNs = hrNowNs();
         waits.push(backend.verifyRequests(batch));
+        if (this.trace) this.trace.push({dispatchNs, packedNs, submittedNs: hrNowNs(), inFlight: this.running.size});
       }
       if (same.length) {
         // jobItem.ts:72-74 times Signature.fromBytes on the main thread; here the bytes are
@@ -510,6 +512,16 @@ class BlsGpuVerifier {
       return;
     }
     const backNs = hrNowNs();
+    if (this.trace && def.length) {
+      for (let q = this.trace.length - 1; q >= 0; q--)
+        if (this.trace[q].dispatchNs === dispatchNs) {
+          this.trace[q].backNs = backNs;
+          this.trace[q].workerStartNs = outs[0].workerStartNs;
+          this.trace[q].workerEndNs = outs[0].workerEndNs;
+          this.trace[q].deviceMs = outs[0].deviceMs;
+          break;
+        }
+    }
     this.idle.push(bi);
     m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
     let k = 0;

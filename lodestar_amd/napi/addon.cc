@@ -252,8 +252,19 @@ void worker_loop(Context* c) {
     }
     if (!t) {  // retire the oldest call in flight
       Task* w = inflight.front();
-      inflight.pop_front();
       Task* owner = w->kind == Kind::Finish ? w->target : w;
+      if ((int)inflight.size() < c->capacity && !c->finalizing) {
+        // room for more calls: do not block on this one while the JS thread may queue
+        // the next package (blocking here held every new package back until the oldest
+        // call finished: ~12 of 16 calls in flight, 2.3 M sets/s through node)
+        int32_t done = 1;
+        if (lb_poll(c->ctx, owner->ticket, &done) == LB_OK && !done) {
+          std::unique_lock<std::mutex> lk(c->mu);
+          c->cv.wait_for(lk, std::chrono::microseconds(200), [&] { return !c->queue.empty() || c->finalizing; });
+          continue;
+        }
+      }
+      inflight.pop_front();
       const int rc = lb_wait(c->ctx, owner->ticket, &owner->stats);
       if (rc != LB_OK) fail(w, rc, c->ctx);
       if (w->kind == Kind::Finish) {

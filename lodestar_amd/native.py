@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
-    "lb_pubkeys_from_bytes",
+    "lb_pubkeys_from_bytes", "lb_poll",
 )
 
 LB_BATCH_DEVICE = 1
@@ -145,6 +145,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_verify_requests_device_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_Stats)]
+    lib.lb_poll.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_verify_requests_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                              ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_verify_requests_partial_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), u32, vp, vp, vp,
@@ -487,6 +488,12 @@ class Device:
     def finish_t(self, ticket: int, merged_ok: bool) -> None:
         self._check(self.lib.lb_verify_requests_finish(self._h, ticket, 1 if merged_ok else 0),
                     "lb_verify_requests_finish")
+
+    def poll(self, ticket: int) -> bool:
+        """True when wait(ticket) would return without blocking (lb_poll)."""
+        done = ctypes.c_int32(0)
+        self._check(self.lib.lb_poll(self._h, ticket, ctypes.byref(done)), "lb_poll")
+        return bool(done.value)
 
     def wait(self, ticket: int) -> float:
         """lb_wait on a ticket; returns device_ms (the call's stats in self.last_stats)."""

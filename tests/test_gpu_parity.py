@@ -433,14 +433,17 @@ def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
         dev.close()
 
 
-def test_steps_uniform_and_single_requests_vs_c_oracle(device):
+@pytest.mark.parametrize("layout", ["mixed", "one_large"])
+def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout):
     """Row layout edge cases of the steps organisation: equal-size requests (the
     coalesced C2 shape), one-set requests (a lane runs the whole Miller loop), a
-    request larger than 68 sets next to small ones, and an empty request."""
+    request larger than 68 sets next to small ones, an empty request; and a
+    1,200-set request beside small ones (its lanes of a level spread over all the
+    threads of k_level_prod)."""
     from oracle import c_oracle as C
-    req_off, pks, pk_off, msgs, blob, offs = mixed_workload_cache(device, True)
+    req_off, pks, pk_off, msgs, blob, offs = mixed_workload_cache(device, layout == "mixed")
     n = len(pk_off) - 1
-    sizes = [128] * 6 + [1] * 40 + [300, 0, 2, 67, 68, 69]
+    sizes = [128] * 6 + [1] * 40 + [300, 0, 2, 67, 68, 69] if layout == "mixed" else [3, 1200] + [20] * 8
     off = [0]
     for z in sizes:
         off.append(min(n, off[-1] + z))
@@ -454,5 +457,26 @@ def test_steps_uniform_and_single_requests_vs_c_oracle(device):
         assert list(res.errors) == list(err)
         assert list(res.valid) == list(valid)
         assert "step_acc" in dict(dev.last_stage_times())
+        if layout == "one_large":  # all valid: the merged check itself must pass (no per-request retry)
+            assert all(valid) and res.batch_retries == 0
     finally:
         dev.close()
+
+
+def test_poll_reports_completion_without_blocking(device, mixed_workload):
+    """lb_poll (the N-API worker's non-blocking retire test): False while a call
+    runs, True once its device work is done, True for a retired ticket; the
+    verdicts through poll-then-wait equal a plain wait's."""
+    import time
+    seed = hashlib.sha256(b"poll-seed").digest()
+    ref = device.verify_requests(*mixed_workload, seed)
+    pc = device.verify_requests_async(*mixed_workload, seed)
+    seen_busy = not device.poll(pc.ticket)
+    t0 = time.time()
+    while not device.poll(pc.ticket):
+        assert time.time() - t0 < 60
+        time.sleep(0.0005)
+    res = device.wait_call(pc)
+    assert seen_busy  # a 1,500-set call takes milliseconds: the first poll saw it running
+    assert device.poll(pc.ticket)  # retired
+    assert list(res.valid) == list(ref.valid) and list(res.errors) == list(ref.errors)

@@ -41,11 +41,44 @@ function median(xs) {
   const ms = () => Number(process.hrtime.bigint()) / 1e6;
   // warm-up: one package of every job
   let ok = (await Promise.all(jobs.map((js) => v.verifySignatureSets(js)))).every((x) => x === true);
+  // latency on an idle verifier before the throughput phase (LB_NODE_PRE=1)
+  const pre128 = [];
+  if (process.env.LB_NODE_PRE === "1") {
+    for (let r = 0; r < 11; r++) {
+      const t = Number(process.hrtime.bigint()) / 1e6;
+      ok = ok && (await v.verifySignatureSets(jobs[r % jobs.length])) === true;
+      pre128.push(Number(process.hrtime.bigint()) / 1e6 - t);
+    }
+  }
+  if (process.env.LB_JS_TRACE === "1") v.trace = [];
   const t0 = ms();
   const all = [];
   for (let r = 0; r < rounds; r++) for (const js of jobs) all.push(v.verifySignatureSets(js));
   ok = ok && (await Promise.all(all)).every((x) => x === true);
   const el = ms() - t0;
+  let trace = null;
+  if (v.trace) {
+    // per package: main-thread packing, the addon call, dispatch -> results back; gaps
+    // between consecutive dispatches; packages already in flight when one was dispatched
+    const tr = v.trace.filter((x) => x.backNs);
+    const avg = (f) => +(tr.reduce((s, x) => s + f(x), 0) / tr.length / 1e6).toFixed(3);
+    const gaps = tr.slice(1).map((x, q) => Number(x.dispatchNs - tr[q].dispatchNs) / 1e6);
+    trace = {
+      packages: tr.length,
+      pack_ms: avg((x) => Number(x.packedNs - x.dispatchNs)),
+      addon_call_ms: avg((x) => Number(x.submittedNs - x.packedNs)),
+      dispatch_to_back_ms: avg((x) => Number(x.backNs - x.dispatchNs)),
+      dispatch_gap_ms_p50: +median(gaps).toFixed(3),
+      in_flight_avg: +(tr.reduce((s, x) => s + x.inFlight, 0) / tr.length).toFixed(2),
+      // addon side: queued -> picked up by the submission thread, picked up -> retired,
+      // retired -> results on the JS thread; the call's own device time (first to last event)
+      to_worker_ms: avg((x) => (x.workerStartNs ? Number(x.workerStartNs) - Number(x.submittedNs) : 0)),
+      worker_ms: avg((x) => (x.workerEndNs ? Number(x.workerEndNs) - Number(x.workerStartNs) : 0)),
+      from_worker_ms: avg((x) => (x.workerEndNs ? Number(x.backNs) - Number(x.workerEndNs) : 0)),
+      device_ms: +(tr.reduce((s, x) => s + (x.deviceMs || 0), 0) / tr.length).toFixed(3),
+    };
+    v.trace = null;
+  }
   const lat128 = [];
   const lat1 = [];
   for (let r = 0; r < 11; r++) {
@@ -64,6 +97,8 @@ function median(xs) {
       sets_per_round: n,
       p50_ms_128set: +median(lat128).toFixed(3),
       p50_ms_1set: +median(lat1).toFixed(3),
+      ...(pre128.length ? {p50_ms_128set_before_throughput: +median(pre128).toFixed(3)} : {}),
+      ...(trace ? {trace} : {}),
       all_valid: ok,
       table_size: tableSize,
       capacity: v.capacity,
