@@ -179,8 +179,12 @@ struct lb_ctx {
   // LB_DAG=0: a call never borrows a second stream (every kernel of a lone call runs
   // alone on the GPU: bench.py's per-kernel iso timings and their rocprof profile)
   bool dag = true;
-  // LB_STEP_LDS=1: k_step_acc keeps its accumulator in LDS instead of registers
-  bool step_lds = false;
+  // LB_STEP_MODE: k_step_acc variant (0 registers + paired lines, 1 accumulator in LDS,
+  // 2 registers + one line at a time; k_steps.hip)
+  int step_mode = 0;
+  // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
+  // submission; the N-API addon sets it, lb_last_stage_times is then empty)
+  bool stage_events = true;
   // per-request tails: one wave per request (k_lines_S + k_tail, wave-cooperative
   // Fp12) or LB_TAIL=lane: one lane per request (k_miller_S + k_final)
   bool tail_wave = true;
@@ -292,7 +296,7 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
 // Launch `kern` on stream `s` of slot `sl`, bracketed by timing events.
 #define LB_STAGE_ON(name, strm, kern, grid, block, ...)                                    \
   do {                                                                                     \
-    const int si_ = sl.n_stages < Slot::kMaxStages ? sl.n_stages++ : -1;                   \
+    const int si_ = (ctx->stage_events && sl.n_stages < Slot::kMaxStages) ? sl.n_stages++ : -1; \
     hipStream_t strm_ = (strm);                                                            \
     LB_COUNT_SYNC();                                                                       \
     if (si_ >= 0) {                                                                        \
@@ -552,12 +556,16 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     return LB_ERR_OUT_OF_MEMORY;
   }
   if (steps) {
-    if (ctx->step_lds)
-      LB_STAGE("step_acc", 0, k_step_acc<true>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
-               (const uint32_t*)d_lines, d_G);
+#define LB_STEP_STAGE(M)                                                                                  \
+  LB_STAGE("step_acc", 0, k_step_acc<M>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,       \
+           (const uint32_t*)d_lines, d_G)
+    if (ctx->step_mode == 1)
+      LB_STEP_STAGE(1);
+    else if (ctx->step_mode == 2)
+      LB_STEP_STAGE(2);
     else
-      LB_STAGE("step_acc", 0, k_step_acc<false>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
-               (const uint32_t*)d_lines, d_G);
+      LB_STEP_STAGE(0);
+#undef LB_STEP_STAGE
     if (merged) {
       LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, n_sets + n_req, rows, d_req_off,
                (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
@@ -887,7 +895,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
   if (const char* e = getenv("LB_DAG")) ctx->dag = atoi(e) != 0;
-  if (const char* e = getenv("LB_STEP_LDS")) ctx->step_lds = atoi(e) != 0;
+  if (const char* e = getenv("LB_STEP_MODE")) ctx->step_mode = atoi(e);
+  if (const char* e = getenv("LB_STAGE_EVENTS")) ctx->stage_events = atoi(e) != 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);
     if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;

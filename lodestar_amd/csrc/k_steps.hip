@@ -249,7 +249,7 @@ struct AccLds {
   LB_DEV void get(fp12& v) const { v = *A; }
 };
 
-template <class Acc>
+template <bool PAIRED, class Acc>
 LB_DEV void step_lines(Acc& acc, const uint32_t* __restrict__ lines, uint32_t n_pairs, const Rows& R, uint32_t r,
                        uint32_t n, uint32_t t0) {
   uint32_t j = t0 / n, i = t0 - j * n;
@@ -264,7 +264,7 @@ LB_DEV void step_lines(Acc& acc, const uint32_t* __restrict__ lines, uint32_t n_
       lvl = lj;
     }
     const uint32_t qa = R.rowoff[i] + r;
-    if (i + 1 < n && c + 1 < (uint32_t)LB_MILLER_LINES) {  // two lines of the same step
+    if (PAIRED && i + 1 < n && c + 1 < (uint32_t)LB_MILLER_LINES) {  // two lines of the same step
       const uint32_t qb = R.rowoff[i + 1] + r;
       fp2 m0, m1, m4, y1, y2;
       fp6 x;
@@ -308,14 +308,16 @@ LB_DEV void step_lines(Acc& acc, const uint32_t* __restrict__ lines, uint32_t n_
   }
 }
 
-// LDS = true: the accumulator lives in LDS (one 592-byte record per lane, 37 KB per wave,
-// four waves per CU at one wave per SIMD) instead of registers (LB_STEP_LDS=1).
-template <bool LDS>
+// MODE 0: accumulator in registers, two lines of a step through the sparse x sparse
+// product (default); 1: the accumulator in LDS (one 592-byte record per lane, 37 KB per
+// wave, four waves per CU at one wave per SIMD; LB_STEP_MODE=1); 2: registers, one line
+// at a time (13 Fp2 products per line instead of 11.5, a smaller live set; LB_STEP_MODE=2).
+template <int MODE>
 __global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
                                                             const uint32_t* __restrict__ req_off,
                                                             const uint32_t* __restrict__ lines,
                                                             uint32_t* __restrict__ G) {
-  __shared__ LdsRec<fp12> sacc[LDS ? TPB : 1];
+  __shared__ LdsRec<fp12> sacc[MODE == 1 ? TPB : 1];
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n_sets) return;
   uint32_t l, r;
@@ -323,13 +325,13 @@ __global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uin
   const uint32_t k = R.inv[r];
   const uint32_t n = req_off[k + 1] - req_off[k];
   fp12 out;
-  if constexpr (LDS) {
+  if constexpr (MODE == 1) {
     AccLds acc{&sacc[threadIdx.x].v};
-    step_lines(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    step_lines<true>(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
     acc.get(out);
   } else {
     AccReg acc;
-    step_lines(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    step_lines<MODE == 0>(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
     acc.get(out);
   }
   g_put(G, n_sets, q, out);
@@ -486,10 +488,12 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
   if (threadIdx.x < 12) (&F[k].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
 }
 
-template __global__ void k_step_acc<false>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,
-                                           const uint32_t* __restrict__, uint32_t* __restrict__);
-template __global__ void k_step_acc<true>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,
-                                          const uint32_t* __restrict__, uint32_t* __restrict__);
+#define LB_INST_STEP(M)                                                                                         \
+  template __global__ void k_step_acc<M>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,                  \
+                                         const uint32_t* __restrict__, uint32_t* __restrict__);
+LB_INST_STEP(0)
+LB_INST_STEP(1)
+LB_INST_STEP(2)
 #define LB_INST_LINES_ROWS(W)                                                                                    \
   template __global__ void k_lines_rows<W>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,                \
                                            const g1j* __restrict__, const g2j* __restrict__, uint32_t* __restrict__);

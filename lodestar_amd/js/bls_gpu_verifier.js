@@ -302,6 +302,7 @@ class BlsGpuVerifier {
    * @param {object[]} [o.backends] Context-like objects instead (tests: mocks)
    * @param {boolean} [o.blsVerifyAllMultiThread]
    * @param {number} [o.maxSetsPerDispatch]
+   * @param {number} [o.prefetch] packages per GPU queued beyond its calls in flight (default 4)
    * @param {() => Uint8Array} [o.seedSource] 32-byte batch-randomness seed per call
    */
   constructor(o = {}) {
@@ -319,10 +320,17 @@ class BlsGpuVerifier {
     this.jobs = [];
     this.buffered = null;
     this.idle = [];
-    this.backends.forEach((b, i) => {
-      for (let k = 0; k < (b.capacity || 4); k++) this.idle.push(i);
-    });
-    this.capacity = this.idle.length;
+    // per GPU: the addon's calls in flight plus `prefetch` packages packed ahead and queued
+    // in the addon, so a slot that frees starts its next call at once instead of after the
+    // main thread has packed it (node leg: ~11.5 of 16 calls in flight without)
+    const prefetch = o.prefetch === undefined ? 4 : o.prefetch;
+    this.capacity = 0;  // the GPUs' calls in flight (the pool's "workers")
+    const per = this.backends.map((b) => b.capacity || 4);
+    per.forEach((c) => (this.capacity += c));
+    // tokens interleaved over the GPUs (the calls in flight first, then the prefetch)
+    for (let k = 0; k < Math.max(...per); k++) per.forEach((c, i) => k < c && this.idle.push(i));
+    for (let k = 0; k < prefetch; k++) per.forEach((c, i) => this.idle.push(i));
+    this.tokens = this.idle.length;
     this.running = new Set();
     this.closed = false;
   }
@@ -459,7 +467,7 @@ class BlsGpuVerifier {
     }
     const now = Date.now();
     for (const j of jobs) m.observe(M.JOB_WAIT_TIME, (now - j.added) / 1000);
-    m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+    m.set(M.WORKERS_BUSY, Math.min(this.capacity, this.tokens - this.idle.length));
     m.set(M.QUEUE_LENGTH, this.jobs.length);
     const p = this.dispatch(bi, jobs).finally(() => this.running.delete(p));
     this.running.add(p);
@@ -506,7 +514,7 @@ class BlsGpuVerifier {
     } catch (e) {
       // device failure rejects every job of the package (index.ts:503-512)
       this.idle.push(bi);
-      m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+      m.set(M.WORKERS_BUSY, Math.min(this.capacity, this.tokens - this.idle.length));
       for (const job of jobs) job.reject(e);
       this.scheduleRun();
       return;
@@ -519,11 +527,13 @@ class BlsGpuVerifier {
           this.trace[q].workerStartNs = outs[0].workerStartNs;
           this.trace[q].workerEndNs = outs[0].workerEndNs;
           this.trace[q].deviceMs = outs[0].deviceMs;
+          this.trace[q].workerSubmittedNs = outs[0].workerSubmittedNs;
+          this.trace[q].workerRetireNs = outs[0].workerRetireNs;
           break;
         }
     }
     this.idle.push(bi);
-    m.set(M.WORKERS_BUSY, this.capacity - this.idle.length);
+    m.set(M.WORKERS_BUSY, Math.min(this.capacity, this.tokens - this.idle.length));
     let k = 0;
     let success = 0;
     let errors = 0;

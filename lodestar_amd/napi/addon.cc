@@ -133,7 +133,7 @@ struct Task {
   int32_t i32 = 0;
   uint32_t u32 = 0;
   uint64_t ticket = 0;
-  uint64_t t_start = 0, t_end = 0;
+  uint64_t t_start = 0, t_end = 0, t_submitted = 0, t_retire = 0;
   int rc = LB_OK;
   std::string errmsg;
   Task* target = nullptr;  // Finish: the two-phase call it resumes
@@ -265,6 +265,7 @@ void worker_loop(Context* c) {
         }
       }
       inflight.pop_front();
+      owner->t_retire = now_ns();
       const int rc = lb_wait(c->ctx, owner->ticket, &owner->stats);
       if (rc != LB_OK) fail(w, rc, c->ctx);
       if (w->kind == Kind::Finish) {
@@ -288,6 +289,7 @@ void worker_loop(Context* c) {
         alloc_outputs(*t);
         lb_request_batch b = batch_of(*t);
         const int rc = lb_verify_requests_async(c->ctx, &b, t->valid.data(), t->err.data(), t->sst.data(), &t->ticket);
+        t->t_submitted = now_ns();
         if (rc != LB_OK) {
           fail(t, rc, c->ctx);
           complete(c, t);
@@ -468,6 +470,8 @@ napi_value verify_result(napi_env env, Task* t) {
   set_num(env, o, "deviceMs", t->stats.device_ms);
   set_num(env, o, "workerStartNs", (double)t->t_start);
   set_num(env, o, "workerEndNs", (double)t->t_end);
+  set_num(env, o, "workerSubmittedNs", (double)t->t_submitted);  // lb_verify_requests_async returned
+  set_num(env, o, "workerRetireNs", (double)t->t_retire);        // lb_wait called on it
   return o;
 }
 
@@ -822,6 +826,9 @@ napi_value Init(napi_env env, napi_value exports) {
   // (profiles/ab_r03/hwq2).  Before the first HIP call (lb_create).
   const char* q = getenv("LB_HW_QUEUES");
   setenv("GPU_MAX_HW_QUEUES", q ? q : "16", 1);
+  // no per-stage timing events in the library (nothing on the JS side reads them; they
+  // are two HIP calls per kernel on the submission thread); LB_STAGE_EVENTS=1 keeps them
+  setenv("LB_STAGE_EVENTS", "0", 0);
   napi_property_descriptor methods[] = {
       {"verifyRequests", nullptr, VerifyRequests, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verifyRequestsPartial", nullptr, VerifyRequestsPartial, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -6,7 +6,8 @@
 //   sets_per_s  ROUNDS x (n / 128) verifySignatureSets jobs of 128 sets, all queued at
 //               once (the pool packs up to 65,536 sets per package, capacity packages
 //               in flight), JS packing + addon + PCIe included;
-//   p50_ms_128set  one verifySignatureSets of 128 sets on an idle verifier;
+//   p50_ms_128set  one verifySignatureSets of 128 sets on an idle verifier (before the
+//                  throughput phase; *_after_throughput: the same after it);
 //   p50_ms_1set    one verifyOnMainThread set (gossip block proposer signature,
 //                  BN/chain/validation/block.ts:146 -> index.ts:174-187).
 const fs = require("fs");
@@ -41,14 +42,16 @@ function median(xs) {
   const ms = () => Number(process.hrtime.bigint()) / 1e6;
   // warm-up: one package of every job
   let ok = (await Promise.all(jobs.map((js) => v.verifySignatureSets(js)))).every((x) => x === true);
-  // latency on an idle verifier before the throughput phase (LB_NODE_PRE=1)
+  // latency on an idle verifier, before the throughput phase
   const pre128 = [];
-  if (process.env.LB_NODE_PRE === "1") {
-    for (let r = 0; r < 11; r++) {
-      const t = Number(process.hrtime.bigint()) / 1e6;
-      ok = ok && (await v.verifySignatureSets(jobs[r % jobs.length])) === true;
-      pre128.push(Number(process.hrtime.bigint()) / 1e6 - t);
-    }
+  const pre1 = [];
+  for (let r = 0; r < 11; r++) {
+    let t = Number(process.hrtime.bigint()) / 1e6;
+    ok = ok && (await v.verifySignatureSets(jobs[r % jobs.length])) === true;
+    pre128.push(Number(process.hrtime.bigint()) / 1e6 - t);
+    t = Number(process.hrtime.bigint()) / 1e6;
+    ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
+    pre1.push(Number(process.hrtime.bigint()) / 1e6 - t);
   }
   if (process.env.LB_JS_TRACE === "1") v.trace = [];
   const t0 = ms();
@@ -76,6 +79,10 @@ function median(xs) {
       worker_ms: avg((x) => (x.workerEndNs ? Number(x.workerEndNs) - Number(x.workerStartNs) : 0)),
       from_worker_ms: avg((x) => (x.workerEndNs ? Number(x.backNs) - Number(x.workerEndNs) : 0)),
       device_ms: +(tr.reduce((s, x) => s + (x.deviceMs || 0), 0) / tr.length).toFixed(3),
+      // inside the worker: lb_verify_requests_async itself, submitted -> lb_wait called, lb_wait
+      submit_ms: avg((x) => (x.workerSubmittedNs ? x.workerSubmittedNs - x.workerStartNs : 0)),
+      until_retire_ms: avg((x) => (x.workerRetireNs ? x.workerRetireNs - x.workerSubmittedNs : 0)),
+      wait_ms: avg((x) => (x.workerRetireNs ? x.workerEndNs - x.workerRetireNs : 0)),
     };
     v.trace = null;
   }
@@ -95,9 +102,11 @@ function median(xs) {
       sets_per_s: Math.round((rounds * n * 1000) / el),
       rounds,
       sets_per_round: n,
-      p50_ms_128set: +median(lat128).toFixed(3),
-      p50_ms_1set: +median(lat1).toFixed(3),
-      ...(pre128.length ? {p50_ms_128set_before_throughput: +median(pre128).toFixed(3)} : {}),
+      p50_ms_128set: +median(pre128).toFixed(3),
+      p50_ms_1set: +median(pre1).toFixed(3),
+      // the same after the throughput phase (a process that has just run 96 packages)
+      p50_ms_128set_after_throughput: +median(lat128).toFixed(3),
+      p50_ms_1set_after_throughput: +median(lat1).toFixed(3),
       ...(trace ? {trace} : {}),
       all_valid: ok,
       table_size: tableSize,
