@@ -1067,10 +1067,25 @@ static int check_host_batch(lb_ctx* ctx, const lb_request_batch* b) {
 // Host-buffer call on slot `sl`: inputs staged through the slot's pinned
 // buffer (one H2D copy), the pipeline, verdicts copied back into pinned memory
 // on the slot's stream and into the caller's buffers when the call retires.
+// LB_HOST_TRACE=1: host-side phases of every host-buffer submission on stderr (ms)
+static bool host_trace() {
+  static const int on = [] {
+    const char* e = getenv("LB_HOST_TRACE");
+    return e && atoi(e) ? 1 : 0;
+  }();
+  return on != 0;
+}
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
 static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* out_valid, uint8_t* out_req_err,
                        uint8_t* out_set_status, bool partial, uint64_t* out_ticket) {
+  const auto t0 = std::chrono::steady_clock::now();
+  double t_check = 0, t_finish = 0, t_stage = 0, t_pipe = 0;
   const uint32_t nr = b->n_requests, ns = b->n_sets;
   LB_TRY(check_host_batch(ctx, b));
+  t_check = ms_since(t0);
   const uint32_t* pk_off = b->pk_offsets;
   const size_t n_pk = pk_off ? pk_off[ns] : ns;
   const bool by_index = b->pubkey_indices != nullptr;
@@ -1090,6 +1105,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
       al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed) + al(sz_rows);
   const size_t out_bytes = al(nr ? nr : 1) * 2 + al(ns ? ns : 1);
   LB_TRY(finish_slot(ctx, sl));
+  t_finish = ms_since(t0);
   if (!partial) borrow_idle_stream(ctx, sl);
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
   LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
@@ -1108,6 +1124,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   stage(b->signatures, sz_sig);
   stage(b->seed, sz_seed);
   if (n_rows) stage(b->pubkeys, sz_rows);
+  t_stage = ms_since(t0);
   char* d_in = ws.take<char>(in_bytes);
   uint8_t* d_valid = ws.take<uint8_t>(nr ? nr : 1);
   uint8_t* d_err = ws.take<uint8_t>(nr ? nr : 1);
@@ -1142,6 +1159,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
     LB_TRY(run_pipeline(ctx, sl, nr, ns, d_req, by_index ? d_rows : d_pks, d_pko,
                         by_index ? (const uint32_t*)d_pks : nullptr, d_msg, d_sig, d_sigo, d_seed, d_valid, d_err, d_sst,
                         ws, d_partial));
+    t_pipe = ms_since(t0);
   } else if (partial) {
     memset(sl.h_partial, 0, LB_GT_BYTES);
     sl.h_partial[47] = 1;
@@ -1151,6 +1169,9 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   }
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
+  if (host_trace())
+    fprintf(stderr, "lb_host_trace sets=%u check=%.3f finish_slot=%.3f stage=%.3f pipeline=%.3f total=%.3f\n", ns,
+            t_check, t_finish, t_stage, t_pipe, ms_since(t0));
   return LB_OK;
 }
 

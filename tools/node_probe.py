@@ -26,12 +26,24 @@ def main():
         with open(os.path.join(d, name + ".bin"), "wb") as f:
             f.write(b"".join(items))
     res = {}
-    env = dict(os.environ, LB_NODE_PRE="1", LB_JS_TRACE="1")
+    env = dict(os.environ, LB_NODE_PRE="1", LB_JS_TRACE="1", LB_HOST_TRACE="1")
     for rounds, prof in ((96, False),):
         cmd = ["node"] + (["--cpu-prof", "--cpu-prof-dir=" + os.path.join(out, "cpuprof")] if prof else []) + \
               [os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
         key = "rounds%d%s" % (rounds, "_prof" if prof else "")
+        with open(os.path.join(out, key + "_stderr.txt"), "w") as f:
+            f.write(r.stderr)
+        ph = {}
+        for line in r.stderr.splitlines():
+            if line.startswith("lb_host_trace") and "sets=65536" in line:
+                for kv in line.split()[2:]:
+                    k, v = kv.split("=")
+                    ph.setdefault(k, []).append(float(v))
+        if ph:
+            import statistics
+            print(key, "host phases ms (mean / median):",
+                  {k: (round(statistics.mean(v), 3), round(statistics.median(v), 3)) for k, v in ph.items()}, flush=True)
         res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-800:]}
         print(key, json.dumps(res[key]), flush=True)
     with open(os.path.join(out, "node_probe.json"), "w") as f:
