@@ -305,6 +305,7 @@ template <class F>
 LB_DEV void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
   jac<F> acc;
   jac_set_inf(acc);
+#pragma unroll 1
   for (int i = 63; i >= 0; i--) {
     jac_dbl(acc, acc);
     if ((k >> i) & 1ull) jac_add(acc, acc, p);
@@ -413,6 +414,9 @@ LB_DEV void jac_mul_xabs(jac<F>& r, const jac<F>& p) {
   q.inf = false;
   jac<F> acc;
   jac_from_aff(acc, q);
+  // rolled: unrolled, the 63 inlined doublings made k_hash_finish (two ladders) 514 KB of
+  // straight-line code against a 64 KB instruction cache (the bit test is wave-uniform)
+#pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     jac_dbl(acc, acc);
     if ((LB_X_ABS >> i) & 1ull) jac_add_aff(acc, acc, q);

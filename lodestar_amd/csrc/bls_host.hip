@@ -182,6 +182,7 @@ struct lb_ctx {
   // LB_STEP_MODE: k_step_acc variant (0 registers + paired lines, 1 accumulator in LDS,
   // 2 registers + one line at a time; k_steps.hip)
   int step_mode = 0;
+  int step_waves = 1;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
   // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
   // submission; the N-API addon sets it, lb_last_stage_times is then empty)
   bool stage_events = true;
@@ -556,15 +557,19 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     return LB_ERR_OUT_OF_MEMORY;
   }
   if (steps) {
-#define LB_STEP_STAGE(M)                                                                                  \
-  LB_STAGE("step_acc", 0, k_step_acc<M>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,       \
+#define LB_STEP_STAGE(M, W)                                                                               \
+  LB_STAGE("step_acc", 0, (k_step_acc<M, W>), blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,  \
            (const uint32_t*)d_lines, d_G)
     if (ctx->step_mode == 1)
-      LB_STEP_STAGE(1);
+      LB_STEP_STAGE(1, 1);
+    else if (ctx->step_mode == 2 && ctx->step_waves == 2)
+      LB_STEP_STAGE(2, 2);
     else if (ctx->step_mode == 2)
-      LB_STEP_STAGE(2);
+      LB_STEP_STAGE(2, 1);
+    else if (ctx->step_waves == 2)
+      LB_STEP_STAGE(0, 2);
     else
-      LB_STEP_STAGE(0);
+      LB_STEP_STAGE(0, 1);
 #undef LB_STEP_STAGE
     if (merged) {
       LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, n_sets + n_req, rows, d_req_off,
@@ -896,6 +901,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
   if (const char* e = getenv("LB_DAG")) ctx->dag = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_MODE")) ctx->step_mode = atoi(e);
+  if (const char* e = getenv("LB_STEP_WAVES")) ctx->step_waves = atoi(e) == 2 ? 2 : 1;
   if (const char* e = getenv("LB_STAGE_EVENTS")) ctx->stage_events = atoi(e) != 0;
   if (const char* e = getenv("LB_ACC_LPR")) {
     const int v = atoi(e);

@@ -262,8 +262,8 @@ __global__ void __launch_bounds__(TPB) k_req_status(uint32_t n_req, const uint32
                                                     const uint8_t* __restrict__ sig_status,
                                                     const uint8_t* __restrict__ pk_status,
                                                     uint8_t* __restrict__ req_bad, uint8_t* __restrict__ req_err);
-template <int MODE>
-__global__ void __launch_bounds__(TPB, LB_W_ACC) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
+template <int MODE, int WAVES>
+__global__ void __launch_bounds__(TPB, WAVES) k_step_acc(uint32_t n_sets, uint32_t n_pairs, Rows R,
                                                             const uint32_t* __restrict__ req_off,
                                                             const uint32_t* __restrict__ lines,
                                                             uint32_t* __restrict__ G);
