@@ -170,7 +170,10 @@ struct lb_ctx {
   int miller_mode = 0;  // 0 auto, 1 lane, 2 lines, 3 wave
   uint32_t lines_min_sets = 8192;
   uint32_t wave_max_sets = 1024;
-  int lines_waves = 1;  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines (1 measured 1-2% faster)
+  // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines(_rows): 2 spills (3.4 -> 4.7 ms alone) but its
+  // waves share SIMDs with other calls' in the pipeline (profiles/ab_r03/ab_r03r, ab_r03s)
+  int lines_waves = 2;
+  int lines_waves_small = 1;  // k_lines for the calls below the steps organisation
   int acc_lpr = 64;     // LB_ACC_LPR: lanes per request in k_miller_acc (64, 32, 16)
   int acc_split = -1;   // LB_ACC_SPLIT: 1 always / 0 never split requests in halves; -1 = lone calls only
   // Miller accumulation of the stored lines: 1 = step-major lanes + level products +
@@ -181,8 +184,10 @@ struct lb_ctx {
   bool dag = true;
   // LB_STEP_MODE: k_step_acc variant (0 registers + paired lines, 1 accumulator in LDS,
   // 2 registers + one line at a time; k_steps.hip)
-  int step_mode = 0;
-  int step_waves = 1;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
+  // defaults: one line at a time at 2 waves/SIMD, which with 2-wave k_lines_rows measured
+  // 3.48-3.54 vs 3.35-3.37 M sets/s (profiles/ab_r03/ab_r03s, three rounds each)
+  int step_mode = 2;
+  int step_waves = 2;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
   // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
   // submission; the N-API addon sets it, lb_last_stage_times is then empty)
   bool stage_events = true;
@@ -490,7 +495,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_STAGE("lines", 1, k_lines_rows<2>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
                (const g1j*)d_rpk, (const g2j*)d_h, d_lines);
   } else if (n_sets && (by_lines || by_wave)) {
-    if (ctx->lines_waves == 1)
+    // (small calls are latency-bound: the spill-free one-wave build unless LB_LINES_WAVES=2)
+    if (ctx->lines_waves_small == 1)
       LB_STAGE("lines", 1, k_lines<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, 0u, (const g1j*)d_rpk,
                (const g2j*)d_h, d_lines);
     else
@@ -896,7 +902,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
-  if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = ctx->lines_waves_small = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
   if (const char* e = getenv("LB_DAG")) ctx->dag = atoi(e) != 0;
