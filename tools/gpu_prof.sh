@@ -16,6 +16,6 @@ LB_DAG=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$
 echo sync-prof-ok
 timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench_line.json 2> gpurun_out/${TAG}_bench.err
 echo bench-ok
-tools/pmc.sh gpurun_out/prof_${TAG}/pmc
-python3 tools/pmc_summarize.py gpurun_out/prof_${TAG}/pmc gpurun_out/prof_${TAG}/pmc_traffic_${TAG}.json > /dev/null
+[ -n "$PMC" ] && tools/pmc.sh gpurun_out/prof_${TAG}/pmc
+[ -n "$PMC" ] && python3 tools/pmc_summarize.py gpurun_out/prof_${TAG}/pmc gpurun_out/prof_${TAG}/pmc_traffic_${TAG}.json > /dev/null
 echo pmc-ok
