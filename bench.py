@@ -480,6 +480,15 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         roof["mads_per_set_launch"] = round(per_set)
         roof["mads_per_set_two_pairs_per_lane"] = round(per_set_pipe)
         roof["frac_at_two_pairs_per_lane_count"] = round(per_set_pipe * n / (timing[dom] * 1e-3) / 1e12 / peak, 5)
+    if iso_ms:
+        # every kernel with an op count, each alone on the GPU: ms and fraction of the mad peak
+        stages = oc.get("pairs_stages", oc["stages"]) if pairs_org else oc["stages"]
+        ka = {}
+        for k, ms in sorted(iso_ms.items(), key=lambda x: -x[1]):
+            m = stages.get(k, {}).get("mads_per_set")
+            if m and ms > 0.5:
+                ka[k] = {"ms": round(ms, 3), "frac": round(m * n / (ms * 1e-3) / 1e12 / peak, 4)}
+        roof["kernels_alone"] = ka
     if iso_ms and dom in stage_ms:
         # the same kernel while other calls' kernels share the CUs (timed region, two pairs per lane)
         roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
