@@ -1182,8 +1182,9 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
   if (host_trace())
-    fprintf(stderr, "lb_host_trace sets=%u check=%.3f finish_slot=%.3f stage=%.3f pipeline=%.3f total=%.3f\n", ns,
-            t_check, t_finish, t_stage, t_pipe, ms_since(t0));
+    fprintf(stderr, "lb_host_trace sets=%u check=%.3f finish_slot=%.3f stage=%.3f pipeline=%.3f total=%.3f dag=%d slot=%d\n",
+            ns, t_check, t_finish, t_stage, t_pipe, ms_since(t0), sl.st[1] != sl.st[0] ? 1 : 0,
+            (int)(&sl - ctx->slots));
   return LB_OK;
 }
 
