@@ -403,6 +403,26 @@ def mixed_workload_cache(device, inject):
     return _MIXED[inject]
 
 
+@pytest.mark.parametrize("mode,waves", [("0", "1"), ("1", "1"), ("0", "2")])
+def test_mixed_workload_step_variants_vs_c_oracle(device, mode, waves):
+    """The k_step_acc variants besides the default (one line at a time, two waves):
+    paired lines at one and two waves/SIMD, the accumulator in LDS (LB_STEP_MODE /
+    LB_STEP_WAVES), merged check failing and passing: verdicts == the C oracle's."""
+    from oracle import c_oracle as C
+    for inject in (True, False):
+        args = mixed_workload_cache(device, inject)
+        seed = hashlib.sha256(b"step-variant" + mode.encode() + waves.encode()).digest()
+        dev = _device_with_env(LB_MILLER="lines", LB_MSM_MIN="1", LB_STEP_MODE=mode, LB_STEP_WAVES=waves)
+        try:
+            res = dev.verify_requests(*args, seed)
+            valid, err = C.verify_requests(*args, seed, threads=16)
+            assert list(res.errors) == list(err)
+            assert list(res.valid) == list(valid)
+            assert res.batch_retries == (1 if inject else 0)
+        finally:
+            dev.close()
+
+
 @pytest.mark.parametrize("msm,merge", [("0", "8"), ("1", "8"), ("0", "0"), ("1", "1")])
 @pytest.mark.parametrize("inject", [True, False])
 def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
