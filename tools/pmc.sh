@@ -5,6 +5,7 @@
 # Runs on the GPU box:  tools/pmc.sh OUTDIR   then   python tools/pmc_summarize.py OUTDIR
 set -e
 OUT=${1:-gpurun_out/pmc}
+mkdir -p "$(dirname "$OUT")" "$OUT"
 export TMPDIR=/tmp
 export LB_DAG=0  # one stream: the kernels of a call one after the other
 CMD="python3 bench.py --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 0 --steps 1 --warmup 0 --inflight 1 --sync"
