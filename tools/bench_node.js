@@ -57,6 +57,19 @@ function median(xs) {
     ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
     pre1.push(Number(process.hrtime.bigint()) / 1e6 - t);
   }
+  const latSummary = (tr) => {
+    const avg = (f) => +(tr.reduce((s, x) => s + f(x), 0) / Math.max(tr.length, 1) / 1e6).toFixed(3);
+    return {
+      calls: tr.length,
+      pack_ms: avg((x) => Number(x.packedNs - x.dispatchNs)),
+      to_worker_ms: avg((x) => (x.workerStartNs ? Number(x.workerStartNs) - Number(x.submittedNs) : 0)),
+      worker_ms: avg((x) => (x.workerEndNs ? Number(x.workerEndNs) - Number(x.workerStartNs) : 0)),
+      submit_ms: avg((x) => (x.workerSubmittedNs ? x.workerSubmittedNs - x.workerStartNs : 0)),
+      until_retire_ms: avg((x) => (x.workerRetireNs ? x.workerRetireNs - x.workerSubmittedNs : 0)),
+      from_worker_ms: avg((x) => (x.workerEndNs ? Number(x.backNs) - Number(x.workerEndNs) : 0)),
+      device_ms: +(tr.reduce((s, x) => s + (x.deviceMs || 0), 0) / Math.max(tr.length, 1)).toFixed(3),
+    };
+  };
   let latTrace = null;
   if (v.trace) {
     const tr = v.trace.filter((x) => x.backNs);
@@ -110,6 +123,7 @@ function median(xs) {
   }
   const lat128 = [];
   const lat1 = [];
+  if (process.env.LB_JS_TRACE === "1") v.trace = [];
   for (let r = 0; r < 11; r++) {
     let t = ms();
     ok = ok && (await v.verifySignatureSets(jobs[r % jobs.length])) === true;
@@ -117,6 +131,14 @@ function median(xs) {
     t = ms();
     ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
     lat1.push(ms() - t);
+  }
+  let latTraceAfter = null;
+  if (v.trace) {
+    latTraceAfter = {
+      set128: latSummary(v.trace.filter((x, q) => x.backNs && q % 2 === 0)),
+      set1: latSummary(v.trace.filter((x, q) => x.backNs && q % 2 === 1)),
+    };
+    v.trace = null;
   }
   await v.close();
   process.stdout.write(
@@ -131,6 +153,7 @@ function median(xs) {
       p50_ms_1set_after_throughput: +median(lat1).toFixed(3),
       ...(trace ? {trace} : {}),
       ...(latTrace ? {latency_trace: latTrace} : {}),
+      ...(latTraceAfter ? {latency_trace_after_throughput: latTraceAfter} : {}),
       all_valid: ok,
       table_size: tableSize,
       capacity: v.capacity,
