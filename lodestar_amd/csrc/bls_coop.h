@@ -1,0 +1,181 @@
+// Row-cooperative Fp arithmetic for the latency path (gfx950).
+//
+// One Fp element per 16-lane DPP row: lane j of the row holds 32-bit limb j
+// (j < 12; lane 12 takes the carry of an unreduced sum, lanes 13-15 stay 0), so
+// a wave holds four independent elements and one Montgomery product is 12 CIOS
+// steps of two v_mad_u64_u32 per lane instead of 288 serial multiply-adds on
+// one lane.  The latency of a product -- not the work -- is what a lone
+// verification waits for: a one-lane product is a ~4k-cycle
+// dependent chain, this one ~0.7k.
+//
+// Broadcasts inside a row use DPP row_newbcast, limb shifts row_shl / row_shr.
+// Carries across limbs are resolved with carry-lookahead on the wave's ballot
+// masks (generate / propagate bits of all four rows at once in one 64-bit
+// scalar add), so no step ever walks the 12 limbs serially.
+//
+// Value invariant of the latency path: every stored element is < 2^383 (about
+// 4.9 p), normalized to 32-bit limbs.  A Montgomery product of two such values
+// is again < 2^383 (xy/R + p < 2^382 + 2^381), and a linear combination is
+// brought back under 2^383 by one quotient estimate from its top 64 bits
+// (reduce); predicates canonicalise to [0, p) first (canon).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bls_constants.h"
+
+namespace lb {
+namespace co {
+
+#define LB_CO __device__ __forceinline__
+
+static constexpr uint64_t ROW_LANE0 = 0x0001000100010001ull;
+static constexpr uint64_t ROW_LANE15 = 0x8000800080008000ull;
+static constexpr uint32_t N0 = LB_P_INV32;  // -p^-1 mod 2^32
+// DPP controls (gfx9 encoding): row_shl:1 -> lane j reads lane j+1; row_shr:1 -> lane j reads lane j-1
+static constexpr int DPP_ROW_SHL1 = 0x101;
+static constexpr int DPP_ROW_SHR1 = 0x111;
+static constexpr int DPP_ROW_BCAST0 = 0x150;  // row_newbcast:n = 0x150 + n
+
+LB_CO uint32_t lane64() { return __lane_id(); }
+LB_CO uint32_t lane16() { return __lane_id() & 15u; }
+
+template <int CTRL>
+LB_CO uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int I>
+LB_CO uint32_t bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_ROW_BCAST0 + I, 0xF, 0xF, false);
+}
+LB_CO uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+// bit (lane) of a wave-uniform mask, as 0 / 1
+LB_CO uint32_t lanebit(uint64_t m) { return (uint32_t)(m >> lane64()) & 1u; }
+// carry INTO each lane from generate / propagate masks (g, p disjoint):
+// the carries of the binary sum (g|p) + g; lane 15 of a row never carries out
+LB_CO uint64_t lookahead(uint64_t g, uint64_t p) {
+  g &= ~ROW_LANE15;
+  p &= ~ROW_LANE15;
+  const uint64_t a = g | p;
+  return (a + g) ^ a ^ g;
+}
+
+static constexpr uint32_t P_LIMB[12] = LB_P_LIMBS;
+static constexpr uint32_t HALF_P_LIMB[12] = LB_HALF_P_RAW_LIMBS;
+// limb j of a 12-limb constant for this lane (0 for lanes >= 12); a chain of
+// selects keeps the constant in registers, not in memory
+LB_CO uint32_t const_limb(const uint32_t (&c)[12]) {
+  const uint32_t j = lane16();
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) r = (j == (uint32_t)k) ? c[k] : r;
+  return r;
+}
+LB_CO uint32_t p_limb() { return const_limb(P_LIMB); }
+LB_CO uint32_t halfp_limb() { return const_limb(HALF_P_LIMB); }
+
+// Signed per-limb partials -> 32-bit limbs.  t: this lane's partial (lanes 13-15
+// of the row 0); the row's value sum_j t_j 2^(32 j) must be >= 0 and < 2^416.
+// NEG: some partials may be negative (a linear form with negative terms, or
+// after subtracting q p).  One DPP shift moves each partial's high word up a
+// limb, leaving per-limb carries in {-1, 0, 1}; those resolve by lookahead:
+// one pass adds the +1 carries, one subtracts the -1 carries.
+template <bool NEG>
+LB_CO uint32_t norm(int64_t t) {
+  const uint32_t lo = (uint32_t)t;
+  const uint64_t h = (uint64_t)(t >> 32);
+  const uint32_t hl = dpp<DPP_ROW_SHR1>((uint32_t)h);
+  const uint32_t hh = dpp<DPP_ROW_SHR1>((uint32_t)(h >> 32));
+  const int64_t u = (int64_t)(uint64_t)lo + (int64_t)(((uint64_t)hh << 32) | hl);
+  uint32_t v = (uint32_t)u;
+  const int32_t c = (int32_t)(u >> 32);
+  const uint32_t x = lanebit((ballot(c == 1) << 1) & ~ROW_LANE0);
+  {
+    const uint64_t g = ballot(x && v == 0xffffffffu);
+    const uint64_t p = ballot(x ? v == 0xfffffffeu : v == 0xffffffffu);
+    v = v + x + lanebit(lookahead(g, p));
+  }
+  if (NEG) {
+    const uint32_t y = lanebit((ballot(c == -1) << 1) & ~ROW_LANE0);
+    const uint64_t g = ballot(y && v == 0u);
+    const uint64_t p = ballot(y ? v == 1u : v == 0u);
+    v = v - y - lanebit(lookahead(g, p));
+  }
+  return v;
+}
+
+template <int I>
+struct MontStep {
+  LB_CO static void run(uint64_t& acc, uint32_t x, uint32_t y, uint32_t pj) {
+    const uint32_t xi = bcast<I>(x);
+    const uint64_t P = (uint64_t)xi * y + acc;
+    const uint32_t m = bcast<0>((uint32_t)P) * N0;
+    const uint64_t Q = (uint64_t)m * pj + (uint32_t)P;
+    const uint32_t qs = dpp<DPP_ROW_SHL1>((uint32_t)Q);
+    acc = (uint64_t)qs + (Q >> 32) + (P >> 32);
+    MontStep<I + 1>::run(acc, x, y, pj);
+  }
+};
+template <>
+struct MontStep<12> {
+  LB_CO static void run(uint64_t&, uint32_t, uint32_t, uint32_t) {}
+};
+
+// x y R^-1 (mod p) for x, y < 2^383 (normalized limbs), result < 2^383, normalized.
+// CIOS over the row: step i broadcasts x_i, every lane j adds x_i y_j, lane 0's
+// low word gives m, every lane adds m p_j, and the row shifts down one limb.
+// A lane's accumulator stays < 3 * 2^32 (64-bit), so the carries wait for one
+// lookahead at the end.
+LB_CO uint32_t mont_mul(uint32_t x, uint32_t y, uint32_t pj) {
+  uint64_t acc = 0;
+  MontStep<0>::run(acc, x, y, pj);
+  return norm<false>((int64_t)acc);
+}
+
+// T (normalized limbs 0..12, T < 2^404) -> T - q p < 2^383 with q = a slight
+// underestimate of floor(T / p) from T's top 64 bits (limbs 11, 12): the
+// quotient of t = floor(T / 2^352) by p_11 + 1 never overshoots floor(T / p)
+// (p < 2^352 (p_11 + 1), and the factor below 1/(p_11+1) absorbs the f64
+// rounding) and undershoots T / p by less than 1 + 2^-16, so the result is
+// < 1.03 p + 2^376 < 1.1 p: one conditional subtraction makes it canonical.
+LB_CO uint32_t reduce(uint32_t v, uint32_t pj) {
+  const uint32_t l11 = bcast<11>(v), l12 = bcast<12>(v);
+  const double th = (double)l12 * 4294967296.0 + (double)l11;
+  // 1 / (p_11 + 1), scaled by (1 - 2^-40) so the product never rounds up
+  constexpr double inv_d = (1.0 / 436277739.0) * (1.0 - 0x1p-40);
+  const uint32_t q = (uint32_t)(th * inv_d);
+  return norm<true>((int64_t)(uint64_t)v - (int64_t)((uint64_t)q * pj));
+}
+
+// borrow-lookahead subtraction d = v - m (v, m normalized, lanes 13.. zero);
+// returns d and sets `ge` (row-uniform) when v >= m
+LB_CO uint32_t sub_cmp(uint32_t v, uint32_t m, bool& ge) {
+  const uint64_t b = lookahead(ballot(v < m), ballot(v == m));
+  ge = ((b >> ((lane64() & ~15u) + 13u)) & 1u) == 0;  // no borrow into lane 13: v >= m
+  return v - m - lanebit(b);
+}
+
+// v < 2^383 -> v mod p (canonical)
+LB_CO uint32_t canon(uint32_t v, uint32_t pj) {
+  v = reduce(v, pj);  // < 1.1 p
+  bool ge;
+  const uint32_t d = sub_cmp(v, pj, ge);
+  return ge ? d : v;
+}
+
+// row-uniform predicates on normalized limbs
+LB_CO bool row_is_zero(uint32_t v) {
+  const uint64_t nz = ballot(v != 0u);
+  return ((nz >> (lane64() & ~15u)) & 0xffffull) == 0;
+}
+// canonical raw value c > (p-1)/2  (the ZCash "lexicographically largest" flag)
+LB_CO bool row_gt_half(uint32_t c) {
+  bool ge;
+  (void)sub_cmp(halfp_limb(), c, ge);  // (p-1)/2 >= c ?
+  return !ge;
+}
+// lowest bit of the row's value
+LB_CO uint32_t row_bit0(uint32_t v) { return bcast<0>(v) & 1u; }
+
+}  // namespace co
+}  // namespace lb
