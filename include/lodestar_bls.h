@@ -354,6 +354,17 @@ int lb_g2_mul(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* k,
  * verifyMultipleSignatures (BN/chain/bls/maybeBatch.ts:19-26), exposed for tests. */
 int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* g2_192, const uint64_t* raw, uint8_t* out192);
 
+/* The latency path's round programs alone (prog: 0 set_single, 1 set_batch, 2 fp12
+ * product, 3 final exponentiation == 1; or, with prog_words != NULL, a caller-encoded
+ * program of n_words words), one workgroup per instance: in16 = n x n_in records of 16
+ * words (canonical Montgomery limbs), in_flags n x n_inflag words; out16 / out_flags
+ * likewise; *out_ms = kernel time; stamps (optional, n_rounds): s_memtime after each
+ * round of instance 0.  Replaces nothing in the reference: the stages of blst's verify
+ * behind BN/chain/bls/maybeBatch.ts:19-38, exposed for parity tests and timing. */
+int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, size_t n_words, uint32_t n,
+                      const uint32_t* in16, const uint32_t* in_flags, uint32_t* out16, uint32_t* out_flags,
+                      float* out_ms, uint64_t* stamps);
+
 /* ---- synthetic data generation (bench / tests) ---------------------------- */
 /* SecretKey.fromBytes(sk).toPublicKey().toBytes(uncompressed) and
  * SecretKey.sign(msg).toBytes() (compressed), as the reference's own perf/unit

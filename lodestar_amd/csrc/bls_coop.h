@@ -104,7 +104,7 @@ LB_CO uint32_t norm(int64_t t) {
   return v;
 }
 
-template <int I>
+template <int I, int N>
 struct MontStep {
   LB_CO static void run(uint64_t& acc, uint32_t x, uint32_t y, uint32_t pj) {
     const uint32_t xi = bcast<I>(x);
@@ -113,23 +113,35 @@ struct MontStep {
     const uint64_t Q = (uint64_t)m * pj + (uint32_t)P;
     const uint32_t qs = dpp<DPP_ROW_SHL1>((uint32_t)Q);
     acc = (uint64_t)qs + (Q >> 32) + (P >> 32);
-    MontStep<I + 1>::run(acc, x, y, pj);
+    MontStep<I + 1, N>::run(acc, x, y, pj);
   }
 };
-template <>
-struct MontStep<12> {
+template <int N>
+struct MontStep<N, N> {
   LB_CO static void run(uint64_t&, uint32_t, uint32_t, uint32_t) {}
 };
 
-// x y R^-1 (mod p) for x, y < 2^383 (normalized limbs), result < 2^383, normalized.
-// CIOS over the row: step i broadcasts x_i, every lane j adds x_i y_j, lane 0's
-// low word gives m, every lane adds m p_j, and the row shifts down one limb.
-// A lane's accumulator stays < 3 * 2^32 (64-bit), so the carries wait for one
-// lookahead at the end.
+// x y R^-1 (mod p), R = 2^(32 N), normalized limbs in and out.  CIOS over the
+// row: step i broadcasts x_i, every lane j adds x_i y_j, lane 0's low word gives
+// m, every lane adds m p_j, and the row shifts down one limb.  A lane's
+// accumulator stays < 3 * 2^32 (64-bit), so the carries wait for one lookahead
+// at the end.  N = 12 (R = 2^384): x, y < 2^383 -> result < 2^383.  N = 13
+// (R = 2^416, the latency path's domain): x, y < 2^415 with x y < 2^416 (2^383 - p)
+// -> result < 2^383, so sums of many reduced values multiply unreduced.
+template <int N = 12>
 LB_CO uint32_t mont_mul(uint32_t x, uint32_t y, uint32_t pj) {
   uint64_t acc = 0;
-  MontStep<0>::run(acc, x, y, pj);
+  MontStep<0, N>::run(acc, x, y, pj);
   return norm<false>((int64_t)acc);
+}
+
+// 13-limb constant (R = 2^416 values may use limb 12)
+LB_CO uint32_t const_limb13(const uint32_t (&c)[13]) {
+  const uint32_t j = lane16();
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 13; k++) r = (j == (uint32_t)k) ? c[k] : r;
+  return r;
 }
 
 // T (normalized limbs 0..12, T < 2^404) -> T - q p < 2^383 with q = a slight

@@ -31,8 +31,13 @@
 #include <vector>
 
 #include "bls_kernels.h"
+#include "bls_lp.h"
+#include "bls_lp_progs.h"
 
 using namespace lb;
+
+// the latency path's round programs (gen_lp.py), embedded by lp_blob.hip
+extern "C" const uint32_t lb_lp_blob[];
 
 #ifdef LB_COUNT_OPS
 static unsigned long long opcount_read_reset() {
@@ -221,6 +226,8 @@ struct lb_ctx {
   uint8_t* d_aux = nullptr;
   uint8_t* h_aux = nullptr;
   size_t aux_cap = 0;
+  // latency path: the round programs in device memory (uploaded on first use)
+  uint32_t* d_lp = nullptr;
 };
 
 namespace {
@@ -864,6 +871,19 @@ int helper_slot(lb_ctx* ctx) {
   return LB_OK;
 }
 
+// latency path: upload the round programs once (2.6 MB)
+int lp_ensure(lb_ctx* ctx) {
+  if (ctx->d_lp) return LB_OK;
+  const size_t bytes = (size_t)LB_LP_BLOB_WORDS * 4;
+  if (hipMalloc(&ctx->d_lp, bytes) != hipSuccess) {
+    ctx->d_lp = nullptr;
+    ctx->err = "hipMalloc latency-path programs failed";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  LB_HIP(hipMemcpy(ctx->d_lp, lb_lp_blob, bytes, hipMemcpyHostToDevice));
+  return LB_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -988,6 +1008,7 @@ int lb_destroy(lb_ctx* ctx) {
   }
   if (ctx->d_aux) (void)hipFree(ctx->d_aux);
   if (ctx->h_aux) (void)hipHostFree(ctx->h_aux);
+  if (ctx->d_lp) (void)hipFree(ctx->d_lp);
   delete ctx;
   return LB_OK;
 }
@@ -2128,6 +2149,75 @@ int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw
   LB_HIP(hipMemcpyAsync(out192, d_out, 192, hipMemcpyDeviceToHost, ctx->stream));
   LB_HIP(hipStreamSynchronize(ctx->stream));
   return LB_OK;
+}
+
+// Round program on n instances, one workgroup each (tests, timing): prog_words
+// == nullptr runs the embedded program `prog` (LB_LP_PROG_*), else the caller's
+// encoded program (lodestar_amd/lpgen) of n_words words.  in16: n x n_in records
+// of 16 words (canonical Montgomery limbs), in_flags: n x n_inflag words; out16:
+// n x n_out records, out_flags: n x n_outflag words; *out_ms: kernel time;
+// stamps (optional): s_memtime after each round of instance 0.
+static int lp_program_run(lb_ctx* ctx, const uint32_t* d_prog, uint32_t n, uint32_t n_in, uint32_t n_inflag,
+                          uint32_t n_out, uint32_t n_outflag, uint32_t n_rounds, const uint32_t* in16,
+                          const uint32_t* in_flags, uint32_t* out16, uint32_t* out_flags, float* out_ms,
+                          uint64_t* stamps, Bump& ws) {
+  const size_t in_w = (size_t)n * n_in * 16, fl_w = (size_t)n * n_inflag + 1, out_w = (size_t)n * n_out * 16,
+               ofl_w = (size_t)n * n_outflag + 1;
+  void* d_in = nullptr;
+  LB_TRY(upload(ctx, ws, in16, in_w * 4, &d_in));
+  uint32_t* d_fl = ws.take<uint32_t>(fl_w);
+  if (n_inflag) LB_HIP(hipMemcpyAsync(d_fl, in_flags, (fl_w - 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  uint32_t* d_out = ws.take<uint32_t>(out_w);
+  uint32_t* d_ofl = ws.take<uint32_t>(ofl_w);
+  unsigned long long* d_st = stamps ? ws.take<unsigned long long>(n_rounds + 1) : nullptr;
+  if (ws.off > ws.cap) {
+    ctx->err = "workspace overflow";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  hipEvent_t e0, e1;
+  LB_HIP(hipEventCreate(&e0));
+  LB_HIP(hipEventCreate(&e1));
+  LB_HIP(hipEventRecord(e0, ctx->stream));
+  LB_LAUNCH(k_lp_program, n, LB_LP_TPB, d_prog, n, (const uint32_t*)d_in, n_in * 16u, (const uint32_t*)d_fl, n_inflag,
+            d_out, n_out * 16u, d_ofl, n_outflag, d_st);
+  LB_HIP(hipEventRecord(e1, ctx->stream));
+  LB_HIP(hipMemcpyAsync(out16, d_out, out_w * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (n_outflag) LB_HIP(hipMemcpyAsync(out_flags, d_ofl, (ofl_w - 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (stamps) LB_HIP(hipMemcpyAsync(stamps, d_st, (size_t)n_rounds * 8, hipMemcpyDeviceToHost, ctx->stream));
+  LB_HIP(hipStreamSynchronize(ctx->stream));
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (out_ms) *out_ms = ms;
+  return LB_OK;
+}
+
+int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, size_t n_words, uint32_t n,
+                      const uint32_t* in16, const uint32_t* in_flags, uint32_t* out16, uint32_t* out_flags,
+                      float* out_ms, uint64_t* stamps) {
+  if (!ctx || n == 0 || !in16 || !out16) return LB_ERR_INVALID_ARGUMENT;
+  if (!prog_words && prog >= LB_LP_NPROGS) return LB_ERR_INVALID_ARGUMENT;
+  if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500002u)) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(helper_slot(ctx));
+  const uint32_t* hw = prog_words ? prog_words : lb_lp_blob + LB_LP_PROGS[prog].off;
+  const uint32_t n_rounds = hw[1], n_in = hw[5], n_inflag = hw[6], n_out = hw[7], n_outflag = hw[8];
+  if ((n_inflag && !in_flags) || (n_outflag && !out_flags)) return LB_ERR_INVALID_ARGUMENT;
+  const size_t io = 4 * ((size_t)n * (n_in + n_out) * 16 + (size_t)n * (n_inflag + n_outflag) + 2) + 8 * (n_rounds + 1);
+  LB_TRY(ensure_ws(ctx, io + (prog_words ? 4 * n_words : 0) + 16384));
+  Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
+  const uint32_t* d_prog;
+  if (prog_words) {
+    void* d = nullptr;
+    LB_TRY(upload(ctx, ws, prog_words, n_words * 4, &d));
+    d_prog = (const uint32_t*)d;
+  } else {
+    LB_TRY(lp_ensure(ctx));
+    d_prog = ctx->d_lp + LB_LP_PROGS[prog].off;
+  }
+  return lp_program_run(ctx, d_prog, n, n_in, n_inflag, n_out, n_outflag, n_rounds, in16, in_flags, out16, out_flags,
+                        out_ms, stamps, ws);
 }
 
 int lb_sk_to_pk(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, uint8_t* out96) {

@@ -1,0 +1,43 @@
+// Latency path (round-program interpreter, k_lp.hip): sizes and opcodes shared
+// with the generator (lodestar_amd/lpgen/compile.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LB_LP_ROWS 32                     // units per round = 16-lane rows per workgroup
+#define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
+#define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
+#define LB_LP_MAX_FLAGS 512
+#define LB_LP_BLOCK_CAP 1024              // words of one round's encoded block
+#define LB_LP_RING 8192                   // LDS ring of the program stream (words, power of 2)
+#define LB_LP_CHUNK 1024                  // stream words fetched per round (2 per thread)
+#define LB_LP_HDR 10                      // header words of an encoded program
+
+#define LB_LP_OP_MUL 0
+#define LB_LP_OP_LIN 1
+#define LB_LP_OP_SEL 2
+#define LB_LP_OP_INV 3
+#define LB_LP_OP_CANON 4
+#define LB_LP_OP_ISZERO 5
+#define LB_LP_OP_BIT0 6
+#define LB_LP_OP_GTHALF 7
+#define LB_LP_OP_FOP 8
+
+// programs in the embedded blob (gen_lp.py -> lp_programs.bin, bls_lp_progs.h)
+#define LB_LP_PROG_SET_SINGLE 0
+#define LB_LP_PROG_SET_BATCH 1
+#define LB_LP_PROG_MUL 2
+#define LB_LP_PROG_FINAL 3
+#define LB_LP_NPROGS 4
+
+namespace lb {
+// k_lp.hip: instance b (one workgroup of LB_LP_TPB threads) runs the round program at
+// prog on in[b * in_stride ...]; stamps (diagnostic, usually nullptr): s_memtime after
+// every round of instance 0
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_program(const uint32_t* __restrict__ prog, uint32_t n,
+                                                          const uint32_t* __restrict__ in, uint32_t in_stride,
+                                                          const uint32_t* __restrict__ in_flags, uint32_t flag_stride,
+                                                          uint32_t* __restrict__ out, uint32_t out_stride,
+                                                          uint32_t* __restrict__ out_flags, uint32_t oflag_stride,
+                                                          unsigned long long* __restrict__ stamps);
+}  // namespace lb

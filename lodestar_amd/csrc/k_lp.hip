@@ -1,0 +1,382 @@
+// Latency path: the round-program interpreter (one workgroup per program
+// instance, one unit per 16-lane row per round; bls_coop.h arithmetic in the
+// 13-limb Montgomery domain, R = 2^416).
+//
+// A program (lodestar_amd/lpgen, encoding in lpgen/compile.py) is a sequence
+// of rounds; round r's units are independent, each reads LDS registers written
+// by earlier rounds and writes one register or flag.  The workgroup runs a
+// round between two barriers.  What a lone verification waits for is then the
+// DAG depth of its products (~1.8k rounds for hash_to_G2 + decode + Miller
+// loop) instead of the ~12k-product serial chains of the one-lane kernels
+// (DESIGN.md §7), so the fixed cost of a round is what the design minimises:
+//   * the program stream (the rounds' blocks back to back) flows through an LDS
+//     ring ~50 rounds ahead of execution (each round issues its share of the
+//     next chunk and stores the chunk issued the round before);
+//   * a unit is a fixed 20-word record loaded into registers during the
+//     PREVIOUS round, so a round starts with every register read of its forms
+//     already addressable: one LDS round trip, then arithmetic;
+//   * forms multiply unreduced (13-limb Montgomery: operands up to ~2^399).
+#include "bls_coop.h"
+#include "bls_kernels.h"
+#include "bls_lp.h"
+#include "bls_lp_progs.h"
+
+namespace lb {
+
+using namespace co;
+
+namespace {
+
+struct LpShared {
+  uint32_t reg[LB_LP_MAX_REGS * 16];
+  uint32_t flag[LB_LP_MAX_FLAGS];
+  uint32_t ring[LB_LP_RING];
+};
+static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
+static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
+constexpr uint32_t RMASK = LB_LP_RING - 1;
+constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk
+constexpr int RECW = 20;                      // fixed unit record (lpgen/compile.py)
+constexpr int NT = 8;                         // inline terms per operand
+static constexpr uint32_t INV_FIX[13] = LB_LP_INV_FIX_LIMBS;
+
+struct Desc {
+  uint32_t w[RECW];
+};
+
+LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
+#pragma unroll
+  for (int k = 0; k < RECW / 4; k++) {
+    const uint4 v = *reinterpret_cast<const uint4*>(ring + ((base + 4 * k) & RMASK));
+    d.w[4 * k] = v.x;
+    d.w[4 * k + 1] = v.y;
+    d.w[4 * k + 2] = v.z;
+    d.w[4 * k + 3] = v.w;
+  }
+}
+
+// sum_t c_t v_t + K p -> normalized limbs (partials signed 64-bit per lane)
+LB_CO uint32_t finish_form(uint64_t Pa, uint64_t Na, bool neg, bool red, uint32_t pj) {
+  uint32_t r = neg ? norm<true>((int64_t)(Pa - Na)) : norm<false>((int64_t)Pa);
+  if (red) r = reduce(r, pj);
+  return r;
+}
+
+template <int B>
+LB_CO uint32_t inline_form(const Desc& d, const uint32_t (&v)[NT], uint32_t n, uint32_t K, bool neg, bool red,
+                           uint32_t pj) {
+  if (n == 1 && K == 0 && (d.w[B] >> 16) == 1u) return v[0];  // a plain register
+  uint64_t Pa = (uint64_t)K * pj, Na = 0;
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    if ((uint32_t)t < n) {
+      const int32_t c = (int32_t)d.w[B + t] >> 16;
+      const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
+      Pa += (uint64_t)cp * v[t];
+      Na += (uint64_t)cn * v[t];
+    }
+  }
+  return finish_form(Pa, Na, neg, red, pj);
+}
+
+// ---- extended records (forms over 8 terms, multi-way selects), read from the ring
+struct Rec {
+  const uint32_t* ring;
+  uint32_t base;
+  LB_CO uint32_t operator[](uint32_t i) const { return ring[(base + i) & RMASK]; }
+};
+
+LB_CO uint32_t ext_form(const Rec& rec, int& o, const uint32_t* __restrict__ reg, uint32_t lane, uint32_t pj) {
+  const uint32_t hdr = rec[o];
+  const int nt = (int)(hdr & 255u);
+  const bool red = (hdr >> 8) & 1u, neg = (hdr >> 9) & 1u;
+  const uint32_t K = hdr >> 16;
+  const int t0 = o + 1;
+  o += 1 + nt;
+  uint64_t Pa = (uint64_t)K * pj, Na = 0;
+  for (int t = 0; t < nt; t += 4) {
+    uint32_t x[4], v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = t + k < nt ? rec[t0 + t + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = reg[(x[k] & 0xffffu) * 16u + lane];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t c = (int32_t)x[k] >> 16;
+      const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
+      Pa += (uint64_t)cp * v[k];
+      Na += (uint64_t)cn * v[k];
+    }
+  }
+  return finish_form(Pa, Na, neg, red, pj);
+}
+
+LB_CO void skip_form(const Rec& rec, int& o) { o += 1 + (int)(rec[o] & 255u); }
+
+// the one-operand units on a normalized value x; returns true when it wrote a flag
+LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_t lane, uint32_t pj, uint32_t& v) {
+  if (op == LB_LP_OP_LIN) {
+    v = x;
+    return false;
+  }
+  const uint32_t c = canon(x, pj);
+  if (op == LB_LP_OP_CANON) {
+    v = c;
+    return false;
+  }
+  if (op == LB_LP_OP_INV) {
+    // one lane of the row runs the binary-GCD inversion (bls_inv.h via fp_inv, which
+    // works in the R = 2^384 form: R384^2 / c); the row multiplies by R416^3 / R384^2
+    S.reg[dst * 16u + lane] = c;
+    if (lane == 0) {
+      fp a, r;
+#pragma unroll
+      for (int j = 0; j < 12; j++) a.l[j] = S.reg[dst * 16u + j];
+      fp_inv(r, a);
+#pragma unroll
+      for (int j = 0; j < 12; j++) S.reg[dst * 16u + j] = r.l[j];
+      S.reg[dst * 16u + 12] = 0u;
+    }
+    const uint32_t ri = S.reg[dst * 16u + lane];
+    v = mont_mul<13>(ri, const_limb13(INV_FIX), pj);
+    return false;
+  }
+  bool f;
+  if (op == LB_LP_OP_ISZERO)
+    f = row_is_zero(c);
+  else if (op == LB_LP_OP_BIT0)
+    f = row_bit0(c) != 0;
+  else
+    f = row_gt_half(c);
+  if (lane == 0) S.flag[dst] = f ? 1u : 0u;
+  return true;
+}
+
+LB_CO void ext_unit(const Rec& rec, LpShared& S, uint32_t lane, uint32_t pj) {
+  const uint32_t w0 = rec[0];
+  const uint32_t op = w0 & 15u, nops = (w0 >> 4) & 7u, nfl = (w0 >> 7) & 7u, dst = w0 >> 16;
+  int o = 1 + (int)nfl;
+  uint32_t v;
+  if (op == LB_LP_OP_SEL) {
+    uint32_t choice = nops - 1;
+    for (uint32_t i = 0; i < nfl; i++)
+      if (S.flag[rec[1 + i]] && choice == nops - 1) choice = i;
+    for (uint32_t i = 0; i < choice; i++) skip_form(rec, o);
+    v = ext_form(rec, o, S.reg, lane, pj);
+  } else {
+    const uint32_t x = ext_form(rec, o, S.reg, lane, pj);
+    if (op == LB_LP_OP_MUL) {
+      const uint32_t y = ext_form(rec, o, S.reg, lane, pj);
+      v = mont_mul<13>(x, y, pj);
+    } else if (single_op(op, dst, x, S, lane, pj, v)) {
+      return;
+    }
+  }
+  S.reg[dst * 16u + lane] = v;
+}
+
+// one unit from its prefetched record; every lane of the row calls it
+LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, uint32_t pj) {
+  const uint32_t w0 = d.w[0];
+  const uint32_t op = w0 & 15u, dst = w0 >> 19;
+  if (op == LB_LP_OP_FOP) {
+    if (lane == 0) {
+      const uint32_t x = d.w[2], fop = x & 7u, f1 = (x >> 3) & 0x1fffu, f2 = x >> 16;
+      uint32_t v;
+      if (fop == 0)
+        v = S.flag[f1] & S.flag[f2];
+      else if (fop == 1)
+        v = S.flag[f1] | S.flag[f2];
+      else if (fop == 2)
+        v = S.flag[f1] ^ S.flag[f2];
+      else if (fop == 3)
+        v = S.flag[f1] ^ 1u;
+      else
+        v = f1 & 1u;
+      S.flag[dst] = v;
+    }
+    return;
+  }
+  if ((w0 >> 18) & 1u) {
+    ext_unit(Rec{S.ring, cons + d.w[2]}, S, lane, pj);
+    return;
+  }
+  const uint32_t nx = (w0 >> 4) & 31u, ny = (w0 >> 9) & 31u;
+  const bool negx = (w0 >> 14) & 1u, negy = (w0 >> 15) & 1u, redx = (w0 >> 16) & 1u, redy = (w0 >> 17) & 1u;
+  const uint32_t Kx = d.w[1] & 0xffffu, Ky = d.w[1] >> 16;
+  // every register read of both forms (and a select's flag) in one LDS round trip
+  uint32_t vx[NT], vy[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) vx[t] = (uint32_t)t < nx ? S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane] : 0u;
+#pragma unroll
+  for (int t = 0; t < NT; t++) vy[t] = (uint32_t)t < ny ? S.reg[(d.w[11 + t] & 0xffffu) * 16u + lane] : 0u;
+  uint32_t v;
+  if (op == LB_LP_OP_SEL) {
+    if (S.flag[d.w[2]])
+      v = inline_form<3>(d, vx, nx, Kx, negx, redx, pj);
+    else
+      v = inline_form<11>(d, vy, ny, Ky, negy, redy, pj);
+  } else {
+    const uint32_t x = inline_form<3>(d, vx, nx, Kx, negx, redx, pj);
+    if (op == LB_LP_OP_MUL) {
+      const uint32_t y = inline_form<11>(d, vy, ny, Ky, negy, redy, pj);
+      v = mont_mul<13>(x, y, pj);
+    } else if (single_op(op, dst, x, S, lane, pj, v)) {
+      return;
+    }
+  }
+  S.reg[dst * 16u + lane] = v;
+}
+
+struct Stream {
+  const uint32_t* sp;  // first stream word
+  uint32_t sw;         // stream words
+  uint32_t cons;       // stream position of the round executing
+  uint32_t done;       // words stored in the ring (valid: [cons, done))
+  uint32_t issued;     // words requested (in registers: [done, issued))
+};
+
+// one round.  d / bw / nu: this round's record (row) and block header, prefetched;
+// the next round's are loaded into them.  pi: register chunk to issue into,
+// pw: the chunk issued last round.
+LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint32_t (&pi)[PFW],
+                    uint32_t (&pw)[PFW], uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
+                    unsigned long long* stamps, uint32_t r) {
+  const uint32_t cons_n = st.cons + bw;
+  // the ring must hold the next round's block: catch up synchronously when the
+  // prefetch ran dry (rare: it runs far ahead)
+  const uint32_t need = min(st.sw, cons_n + LB_LP_BLOCK_CAP);
+  while (st.done < need) {
+    const uint32_t n = min((uint32_t)LB_LP_CHUNK, st.issued - st.done);
+    if (n) {
+#pragma unroll
+      for (int k = 0; k < PFW; k++) {
+        const uint32_t i = tid + k * LB_LP_TPB;
+        if (i < n) S.ring[(st.done + i) & RMASK] = pw[k];
+      }
+      st.done += n;
+    } else {
+      const uint32_t m = min((uint32_t)LB_LP_CHUNK, st.sw - st.done);
+#pragma unroll
+      for (int k = 0; k < PFW; k++) {
+        const uint32_t i = tid + k * LB_LP_TPB;
+        if (i < m) S.ring[(st.done + i) & RMASK] = st.sp[st.done + i];
+      }
+      st.done += m;
+      st.issued = st.done;
+    }
+    __syncthreads();
+  }
+  const uint32_t pending = st.issued - st.done;  // words in pw
+  uint32_t n_new = 0;
+  if (st.issued < st.sw && st.issued + LB_LP_CHUNK <= st.cons + LB_LP_RING) {
+    n_new = min((uint32_t)LB_LP_CHUNK, st.sw - st.issued);
+#pragma unroll
+    for (int k = 0; k < PFW; k++) {
+      const uint32_t i = tid + k * LB_LP_TPB;
+      pi[k] = i < n_new ? st.sp[st.issued + i] : 0u;
+    }
+  }
+  // the next round's header and this row's record (consumed after the barrier)
+  Desc dn;
+  uint32_t bwn = 0, nun = 0;
+  if (cons_n < st.sw) {
+    const uint4 h = *reinterpret_cast<const uint4*>(S.ring + (cons_n & RMASK));
+    bwn = h.x;
+    nun = h.y;
+    load_desc(dn, S.ring, cons_n + 4 + RECW * row);
+  }
+  if (row < nu) run_unit(d, S, st.cons, lane, pj);
+#pragma unroll
+  for (int k = 0; k < PFW; k++) {
+    const uint32_t i = tid + k * LB_LP_TPB;
+    if (i < pending) S.ring[(st.done + i) & RMASK] = pw[k];
+  }
+  st.done += pending;
+  st.issued += n_new;
+  st.cons = cons_n;
+  d = dn;
+  bw = bwn;
+  nu = nun;
+  __syncthreads();
+  if (stamps && tid == 0) stamps[r] = __builtin_amdgcn_s_memtime();
+}
+
+}  // namespace
+
+// Run program `prog` for one instance on this workgroup.  Inputs i < split come
+// from in_a[16 i ...], the rest from in_b[16 (i - split) ...] (16-word records of
+// canonical limbs: R = 2^384 Montgomery for the set programs, this domain for
+// Miller values); in_flags: n_inflag words; out: n_out 16-word records;
+// out_flags: n_outflag words.  stamps (diagnostic, usually nullptr): s_memtime
+// after every round's barrier.
+LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_t* __restrict__ in_a, uint32_t split,
+                   const uint32_t* __restrict__ in_b, const uint32_t* __restrict__ in_flags,
+                   uint32_t* __restrict__ out, uint32_t* __restrict__ out_flags,
+                   unsigned long long* __restrict__ stamps = nullptr) {
+  const uint32_t tid = threadIdx.x, lane = tid & 15u, row = tid >> 4;
+  const uint32_t pj = p_limb();
+  const uint32_t n_rounds = prog[1], n_const = prog[4], n_in = prog[5], n_inflag = prog[6], n_out = prog[7],
+                 n_outflag = prog[8];
+  Stream st;
+  st.sw = prog[9];
+  uint32_t pos = LB_LP_HDR;
+  for (uint32_t i = row; i < n_const; i += LB_LP_ROWS) {
+    const uint32_t* c = prog + pos + 14 * i;
+    S.reg[c[0] * 16u + lane] = lane < 13 ? c[1 + lane] : 0u;
+  }
+  pos += 14 * n_const;
+  for (uint32_t i = row; i < n_in; i += LB_LP_ROWS) {
+    const uint32_t* src = i < split ? in_a + 16 * i : in_b + 16 * (i - split);
+    S.reg[prog[pos + i] * 16u + lane] = lane < 13 ? src[lane] : 0u;
+  }
+  pos += n_in;
+  for (uint32_t i = tid; i < n_inflag; i += LB_LP_TPB) S.flag[prog[pos + i]] = in_flags[i] ? 1u : 0u;
+  pos += n_inflag;
+  const uint32_t* outs = prog + pos;
+  pos += n_out;
+  const uint32_t* outfl = prog + pos;
+  pos += n_outflag;
+  st.sp = prog + pos;
+  st.cons = 0;
+  st.done = st.issued = min(st.sw, (uint32_t)(LB_LP_RING - LB_LP_CHUNK));
+  for (uint32_t i = tid; i < st.done; i += LB_LP_TPB) S.ring[i] = st.sp[i];
+  __syncthreads();
+  Desc d;
+  uint32_t bw = 0, nu = 0;
+  if (st.sw) {
+    const uint4 h = *reinterpret_cast<const uint4*>(S.ring);
+    bw = h.x;
+    nu = h.y;
+    load_desc(d, S.ring, 4 + RECW * row);
+  }
+  uint32_t pa[PFW], pb[PFW];
+#pragma unroll
+  for (int k = 0; k < PFW; k++) pa[k] = pb[k] = 0u;
+  uint32_t r = 0;
+#pragma unroll 1
+  for (; r + 1 < n_rounds; r += 2) {
+    lp_round(S, st, d, bw, nu, pa, pb, tid, lane, row, pj, stamps, r);
+    lp_round(S, st, d, bw, nu, pb, pa, tid, lane, row, pj, stamps, r + 1);
+  }
+  if (r < n_rounds) lp_round(S, st, d, bw, nu, pa, pb, tid, lane, row, pj, stamps, r);
+  for (uint32_t i = row; i < n_out; i += LB_LP_ROWS) out[16 * i + lane] = lane < 13 ? S.reg[outs[i] * 16u + lane] : 0u;
+  for (uint32_t i = tid; i < n_outflag; i += LB_LP_TPB) out_flags[i] = S.flag[outfl[i]];
+}
+
+// Test / stage entry: instance b runs `prog` on in[b * in_stride ...].
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_program(const uint32_t* __restrict__ prog, uint32_t n,
+                                                          const uint32_t* __restrict__ in, uint32_t in_stride,
+                                                          const uint32_t* __restrict__ in_flags, uint32_t flag_stride,
+                                                          uint32_t* __restrict__ out, uint32_t out_stride,
+                                                          uint32_t* __restrict__ out_flags, uint32_t oflag_stride,
+                                                          unsigned long long* __restrict__ stamps) {
+  __shared__ LpShared S;
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* ia = in + (size_t)b * in_stride;
+  lp_run(S, prog, ia, 0xffffffffu, ia, in_flags + (size_t)b * flag_stride, out + (size_t)b * out_stride,
+         out_flags + (size_t)b * oflag_stride, b == 0 ? stamps : nullptr);
+}
+
+}  // namespace lb

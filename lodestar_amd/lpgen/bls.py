@@ -1,0 +1,452 @@
+"""The latency path's round programs (build-time).
+
+Three programs, all restating the one-lane device algorithms (csrc/bls_hash.h,
+bls_curve.h, bls_pairing.h -- themselves pinned to the oracle) so the two paths
+agree point for point:
+
+* ``set_program(single)``: one signature set of a request -- hash_to_G2 of the
+  signing root, the signature's decompression and G2 subgroup check, and the
+  set's factor of the batch equation as a Miller value.  For a 1-set request
+  (core verify: blst ``Signature.verify``, reached from
+  BN/chain/bls/maybeBatch.ts:38) the pubkey's G1 subgroup check and the pairs
+  (pk, H(m)), (-g1, sig).  For a set of a >= 2-set request (blst
+  ``verifyMultipleSignatures``, maybeBatch.ts:19) the pairs (r pk, H(m)) and
+  (-r g1, sig): e(-g1, sum_i r_i sig_i) = prod_i e(-r_i g1, sig_i), so the
+  random scalar multiplies in G1 (a 32-step GLV ladder on Fp) instead of G2,
+  and the request's product needs no sum of G2 points before its Miller loop.
+* ``mul_program``: the product of two Miller values (the request's product
+  tree across its sets' workgroups).
+* ``final_program``: final exponentiation == 1 (the request's verdict).
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+
+from .dsl import Flag, Fp, Graph, P, select, select_n
+from .tower import (P34, Fp2, Fp6, Fp12, Jac, Ops, fp2_lex_largest, fp2_sgn0, fp_pow, jac_add, jac_add_aff,
+                    jac_dbl, jac_eq, jac_inf, jsel, line_mul_line)
+
+X_ABS = 0xD201000000010000
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def _load_constants() -> dict:
+    spec = importlib.util.spec_from_file_location("lb_gen_constants", os.path.join(_CSRC, "gen_constants.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.constants()
+
+
+C = _load_constants()
+HALF = (P + 1) // 2
+
+
+def c2(g: Graph, name: str) -> Fp2:
+    return Fp2.const(g, C[name])
+
+
+# ---------------------------------------------------------------------------
+# square roots (bls_field.h fp2_sqrt, bls_hash.h fp2_sqrt_with_norm_root)
+# ---------------------------------------------------------------------------
+def fp2_sqrt_in_fp(a0: Fp):
+    """fp2_sqrt's a.c1 == 0 branch: sqrt(a0) or u sqrt(-a0)"""
+    g = a0.g
+    c = fp_pow(a0, P34)
+    x0 = a0 * c
+    t = x0 * c
+    is_qr = g.is_zero(t - g.one()) | g.is_zero(a0)
+    z = g.zero()
+    return Fp2(select(is_qr, x0, z), select(is_qr, z, x0))
+
+
+def fp2_sqrt_from_norm_root(a: Fp2, s: Fp) -> Fp2:
+    g = a.g
+    half = g.const(HALF)
+    t = (a.c0 + s) * half
+    c = fp_pow(t, P34)
+    x0 = t * c
+    chk = x0.sqr()
+    a1c = (a.c1 * c) * half
+    direct = g.is_zero(chk - t)
+    return Fp2(select(direct, x0, -a1c), select(direct, a1c, x0))
+
+
+def fp2_sqrt(a: Fp2):
+    """(root, is_square) -- bls_field.h fp2_sqrt"""
+    g = a.g
+    n = a.norm()
+    t = fp_pow(n, P34)
+    s = t * n
+    ok = g.is_zero(s.sqr() - n)
+    main = fp2_sqrt_from_norm_root(a, s)
+    z1 = g.is_zero(a.c1)
+    r = select(z1, fp2_sqrt_in_fp(a.c0), main)
+    return r, z1 | ok
+
+
+# ---------------------------------------------------------------------------
+# hash_to_G2 (bls_hash.h): SSWU, 3-isogeny, Q0 + Q1, clear_cofactor
+# ---------------------------------------------------------------------------
+def map_to_curve_sswu(u: Fp2):
+    g = u.g
+    A = c2(g, "LB_SSWU_A")
+    B = c2(g, "LB_SSWU_B")
+    Z = c2(g, "LB_SSWU_Z")
+    tv1 = Z * u.sqr()
+    tv2 = tv1.sqr() + tv1
+    exceptional = tv2.is_zero()
+    t = tv2.inv()
+    t = Fp2(t.c0 + g.one(), t.c1)
+    x1 = t * c2(g, "LB_SSWU_MINUS_B_OVER_A")
+    x1 = select(exceptional, c2(g, "LB_SSWU_B_OVER_ZA"), x1)
+    gx1 = (x1.sqr() + A) * x1 + B
+    x2 = tv1 * x1
+    gx2 = (x2.sqr() + A) * x2 + B
+    n1 = gx1.norm()
+    e = fp_pow(n1, P34)
+    chk = e.sqr() * n1
+    sq1 = g.is_zero(chk - g.one()) | g.is_zero(n1)
+    s1 = n1 * e
+    nu = u.norm()
+    nu3 = nu.sqr() * nu
+    s2 = (nu3 * g.const(C["LB_SSWU_NZ3_SQRT"])) * s1
+    s2 = select(sq1, s1, s2)
+    x = select(sq1, x1, x2)
+    gx = select(sq1, gx1, gx2)
+    # fp2_sqrt_with_norm_root: gx.c1 == 0 takes fp2_sqrt, i.e. its a.c1 == 0 branch
+    # (one exponentiation from gx.c0, beside the main one)
+    z1 = g.is_zero(gx.c1)
+    y_main = fp2_sqrt_from_norm_root(gx, s2)
+    y = select(z1, fp2_sqrt_in_fp(gx.c0), y_main)
+    flip = fp2_sgn0(u) ^ fp2_sgn0(y)
+    y = select(flip, -y, y)
+    return x, y
+
+
+def iso_map_g2(x: Fp2, y: Fp2) -> Jac:
+    g = x.g
+
+    def k(n):
+        return c2(g, n)
+
+    xn = ((k("LB_ISO_XNUM3") * x + k("LB_ISO_XNUM2")) * x + k("LB_ISO_XNUM1")) * x + k("LB_ISO_XNUM0")
+    xd = (x + k("LB_ISO_XDEN1")) * x + k("LB_ISO_XDEN0")
+    yn = ((k("LB_ISO_YNUM3") * x + k("LB_ISO_YNUM2")) * x + k("LB_ISO_YNUM1")) * x + k("LB_ISO_YNUM0")
+    yd = ((x + k("LB_ISO_YDEN2")) * x + k("LB_ISO_YDEN1")) * x + k("LB_ISO_YDEN0")
+    kern = xd.is_zero() | yd.is_zero()
+    Z = xd * yd
+    yd2 = yd.sqr()
+    X = (xn * xd) * yd2
+    xd3 = xd.sqr() * xd
+    Y = ((y * yn) * xd3) * yd2
+    F = Ops(g, True)
+    return jsel(kern, jac_inf(F), Jac(X, Y, Z))
+
+
+def g2_psi(p: Jac) -> Jac:
+    g = p.X.g
+    return Jac(p.X.conj() * c2(g, "LB_PSI_CX"), p.Y.conj() * c2(g, "LB_PSI_CY"), p.Z.conj())
+
+
+def jac_mul_xabs(F: Ops, p: Jac, p_inf: Flag = None) -> Jac:
+    """[|x|]P on the shared-Z curve (bls_curve.h jac_mul_xabs): 63 doublings and
+    5 mixed additions of (X, Y); the result's Z times P's Z."""
+    qx, qy = p.X, p.Y
+    acc = Jac(qx, qy, F.one())
+    for i in range(62, -1, -1):
+        acc = jac_dbl(F, acc)
+        if (X_ABS >> i) & 1:
+            acc = jac_add_aff(F, acc, qx, qy)
+    acc = Jac(acc.X, acc.Y, acc.Z * p.Z)
+    if p_inf is None:
+        p_inf = F.is_zero(p.Z)
+    return jsel(p_inf, p, acc)
+
+
+def clear_cofactor_g2(p: Jac) -> Jac:
+    F = Ops(p.X.g, True)
+    A = jac_mul_xabs(F, p)
+    B = jac_add(F, g2_psi(p), A.neg())
+    t = g2_psi(g2_psi(jac_dbl(F, p)))
+    t = jac_add(F, t, p.neg())
+    D = jac_add(F, t, B.neg())
+    t = jac_mul_xabs(F, B).neg()
+    return jac_add(F, D, t)
+
+
+def hash_to_g2(u0: Fp2, u1: Fp2) -> Jac:
+    q = []
+    for u in (u0, u1):
+        x, y = map_to_curve_sswu(u)
+        q.append(iso_map_g2(x, y))
+    F = Ops(u0.g, True)
+    return clear_cofactor_g2(jac_add(F, q[0], q[1]))
+
+
+# ---------------------------------------------------------------------------
+# subgroup checks (bls_curve.h)
+# ---------------------------------------------------------------------------
+def g2_in_subgroup(p: Jac, p_inf: Flag) -> Flag:
+    F = Ops(p.X.g, True)
+    xp = jac_mul_xabs(F, p, p_inf).neg()
+    return p_inf | jac_eq(F, g2_psi(p), xp)
+
+
+def g1_in_subgroup(p: Jac, p_inf: Flag) -> Flag:
+    g = p.X.g
+    F = Ops(g, False)
+    t = jac_mul_xabs(F, p, p_inf)
+    t = jac_mul_xabs(F, t).neg()
+    ph = Jac(p.X * g.const(C["LB_G1_BETA"]), p.Y, p.Z)
+    return p_inf | jac_eq(F, ph, t)
+
+
+# ---------------------------------------------------------------------------
+# [a + b lambda] P on G1 (bls_curve.h jac_mul_glv_xy, shared-Z ladder)
+# ---------------------------------------------------------------------------
+def g1_glv_mul(p: Jac, a_bits, b_bits) -> Jac:
+    """a_bits / b_bits: flags of the 32-bit halves, most significant first."""
+    g = p.X.g
+    F = Ops(g, False)
+    X, Y = p.X, p.Y
+    wX = X * g.const(C["LB_G1_BETA"])
+    w2X = X * g.const(C["LB_G1_BETA2"])
+    acc = jac_inf(F)
+    for a, b in zip(a_bits, b_bits):
+        acc = jac_dbl(F, acc)
+        s1 = a & ~b
+        s2 = ~a & b
+        s3 = a & b
+        nz = a | b
+        qx = g.select_n([(s1, X), (s2, wX)], w2X)
+        qy = select(s3, -Y, Y)
+        acc = jac_add_aff(F, acc, qx, qy, skip=~nz)
+    out = Jac(acc.X, acc.Y, acc.Z * p.Z)
+    return jsel(F.is_zero(p.Z), p, out)
+
+
+# ---------------------------------------------------------------------------
+# Miller loop of two pairs sharing f (bls_pairing.h miller_dbl_step / miller_add_step)
+# with both points projective: no inversion ahead of the loop.
+#   P Jacobian (Xp, Yp, Zp): xp = Xp/Zp^2, yp = Yp/Zp^3 -- every line times Zp^3
+#     (an Fp scalar) uses (Xp Zp, Yp, Zp^3) instead of (xp, yp, 1);
+#   Q Jacobian (X, Y, Z) -> homogeneous (X Z, Y, Z^3) = (Xq, Yq, Zq); the chord of
+#     T + Q with th' = Y Zq - Yq Z, la' = X Zq - Xq Z (Zq times the affine-Q
+#     values) is the affine-Q chord times Zq^2 (an Fp2 scalar), and with T scaled
+#     by Zq the point formulas give Zq^4 times the affine-Q result (the same point).
+# Both scalings are killed by the final exponentiation.
+# ---------------------------------------------------------------------------
+def miller_dbl_step(T, P):
+    X, Y, Z = T
+    xpz, yp, zp3 = P
+    XX = X.sqr()
+    Bq = Y.sqr()
+    Cq = Z.sqr()
+    E = Cq.mul_xi().scale(12)
+    Fq = E.scale(3)
+    XY = X * Y
+    H = (Y + Z).sqr() - Bq - Cq
+    l0 = Bq - E
+    if zp3 is not None:
+        l0 = l0 * zp3
+    l1 = -(XX.scale(3) * xpz)
+    l4 = H * yp
+    X2 = (XY * (Bq - Fq)).scale(2)
+    Y2 = (Bq + Fq).sqr() - E.sqr().scale(12)
+    Z2 = (Bq * H).scale(4)
+    return (X2, Y2, Z2), (l0, l1, l4)
+
+
+def miller_add_step(T, Q, P):
+    X, Y, Z = T
+    Xq, Yq, Zq = Q
+    xpz, yp, zp3 = P
+    if Zq is None:  # affine Q
+        th = Y - Yq * Z
+        la = X - Xq * Z
+        Xs, Ys, Zs = X, Y, Z
+        l1 = -(th * xpz)
+        l4 = la * yp
+    else:
+        th = Y * Zq - Yq * Z
+        la = X * Zq - Xq * Z
+        Xs, Ys, Zs = X * Zq, Y * Zq, Z * Zq
+        l1 = -((th * Zq) * xpz)
+        l4 = (la * Zq) * yp
+    l0 = th * Xq - la * Yq
+    if zp3 is not None:
+        l0 = l0 * zp3
+    Cq = th.sqr()
+    D = la.sqr()
+    E = la * D
+    Fq = Zs * Cq
+    G = Xs * D
+    H = E + Fq - G.scale(2)
+    X2 = la * H
+    Y2 = th * (G - H) - Ys * E
+    Z2 = Zs * E
+    return (X2, Y2, Z2), (l0, l1, l4)
+
+
+def unit_line(g, void: Flag, line):
+    one = Fp2.one(g)
+    zero = Fp2.zero(g)
+    return (select(void, one, line[0]), select(void, zero, line[1]), select(void, zero, line[2]))
+
+
+def g1_line_point(p: Jac):
+    """(Xp Zp, Yp, Zp^3) of a Jacobian G1 point (zp3 None when Zp is the constant 1)"""
+    if p.Z.t == p.X.g.one().t:
+        return (p.X, p.Y, None)
+    return (p.X * p.Z, p.Y, p.Z.sqr() * p.Z)
+
+
+def g2_homogeneous(q: Jac):
+    """(X Z, Y, Z^3) of a Jacobian G2 point (affine: Zq None)"""
+    g = q.X.g
+    if q.Z.c0.t == g.one().t and not q.Z.c1.t:
+        return (q.X, q.Y, None)
+    return (q.X * q.Z, q.Y, q.Z.sqr() * q.Z)
+
+
+def miller2(pairs) -> Fp12:
+    """prod over two pairs (P: Jacobian G1, Q: Jacobian G2, void) of f_{|x|,Q}(P),
+    conjugated (x < 0), up to factors the final exponentiation kills.  A void pair
+    (an infinite point) contributes unit lines."""
+    g = pairs[0][0].X.g
+    Ps = [g1_line_point(p) for p, _, _ in pairs]
+    Qs = [g2_homogeneous(q) for _, q, _ in pairs]
+    Ts = [(q[0], q[1], q[2] if q[2] is not None else Fp2.one(g)) for q in Qs]
+    f = None
+    for i in range(62, -1, -1):
+        lines = []
+        for k, (_, _, void) in enumerate(pairs):
+            Ts[k], ln = miller_dbl_step(Ts[k], Ps[k])
+            lines.append(unit_line(g, void, ln))
+        x, y1, y2 = line_mul_line(*lines[0], *lines[1])
+        if f is None:
+            # f = l1 l2 as a full Fp12: (x0 + x1 v + x2 v^2) + (y1 v + y2 v^2) w
+            f = Fp12(x, Fp6(Fp2.zero(g), y1, y2))
+        else:
+            f = f.sqr().mat().mul_sparse2(x, y1, y2).mat()
+        if (X_ABS >> i) & 1:
+            lines = []
+            for k, (_, _, void) in enumerate(pairs):
+                Ts[k], ln = miller_add_step(Ts[k], Qs[k], Ps[k])
+                lines.append(unit_line(g, void, ln))
+            x, y1, y2 = line_mul_line(*lines[0], *lines[1])
+            f = f.mul_sparse2(x, y1, y2).mat()
+    return f.conj()
+
+
+# ---------------------------------------------------------------------------
+# final exponentiation (bls_pairing.h final_exp): f^(3 (p^12 - 1)/r)
+# ---------------------------------------------------------------------------
+def _gam(k):
+    return {e: C["LB_FROB%d_%d" % (k, e)] for e in range(1, 6)}
+
+
+def fp12_exp_x(a: Fp12) -> Fp12:
+    """a^x (x < 0) for cyclotomic a: 63 squarings, one round each -- every
+    squaring consumes the previous one's output as forms over its products and
+    the materialized value before it, materialized meanwhile (cyc_sqr's lin)."""
+    acc = a
+    acc_mat = a
+    for i in range(62, -1, -1):
+        acc = acc.cyc_sqr(acc_mat)
+        acc_mat = acc.mat()
+        if (X_ABS >> i) & 1:
+            acc = acc_mat = (acc_mat * a).mat()
+    return acc_mat.conj()
+
+
+def final_exp(f: Fp12) -> Fp12:
+    t0 = f.conj() * f.inv()
+    t0 = t0.mat()
+    f2 = (t0.frob(2, _gam(2)) * t0).mat()
+    a = (fp12_exp_x(f2) * f2.conj()).mat()
+    a = (fp12_exp_x(a) * a.conj()).mat()
+    b = (fp12_exp_x(a) * a.frob(1, _gam(1))).mat()
+    t0 = fp12_exp_x(fp12_exp_x(b))
+    c = (t0 * b.frob(2, _gam(2))).mat()
+    c = (c * b.conj()).mat()
+    t0 = (f2.cyc_sqr().mat() * f2).mat()
+    return c * t0
+
+
+# ---------------------------------------------------------------------------
+# programs
+# ---------------------------------------------------------------------------
+SET_INPUTS = ["u0c0", "u0c1", "u1c0", "u1c1", "sx0", "sx1", "sy0", "sy1", "pkX", "pkY", "pkZ"]
+SET_FLAGS = ["sig_inf", "sig_sign", "sig_comp"] + ["a%d" % i for i in range(32)] + ["b%d" % i for i in range(32)]
+
+
+def set_program(single: bool) -> Graph:
+    g = Graph("set_single" if single else "set_batch")
+    v = {n: g.input(n) for n in SET_INPUTS}
+    fl = {n: g.input_flag(n) for n in SET_FLAGS}
+    F1 = Ops(g, False)
+    F2 = Ops(g, True)
+    # hash_to_G2 of the signing root (hash_to_field done by the input stage)
+    H = hash_to_g2(Fp2(v["u0c0"], v["u0c1"]), Fp2(v["u1c0"], v["u1c1"]))
+    # Signature.fromBytes(validate=true): decompression / on-curve, G2 subgroup
+    sx = Fp2(v["sx0"], v["sx1"])
+    rhs = sx.sqr() * sx + c2(g, "LB_B2")
+    yc, sq = fp2_sqrt(rhs)
+    flip = fp2_lex_largest(yc) ^ fl["sig_sign"]
+    yc = select(flip, -yc, yc)
+    yu = Fp2(v["sy0"], v["sy1"])
+    on_u = (yu.sqr() - rhs).is_zero()
+    comp = fl["sig_comp"]
+    sy = select(comp, yc, yu)
+    on_curve = (comp & sq) | (~comp & on_u)
+    sig_inf = fl["sig_inf"]
+    sig = Jac(sx, sy, Fp2.one(g))
+    in_group = g2_in_subgroup(sig, sig_inf)
+    pk = Jac(v["pkX"], v["pkY"], v["pkZ"])
+    pk_inf = g.is_zero(v["pkZ"])
+    g1x = g.const(C["LB_G1_X"])
+    g1ny = g.const(C["LB_G1_NEG_Y"])
+    if single:
+        pk_ok = g1_in_subgroup(pk, pk_inf)
+        P1 = pk
+        P2 = None  # (-g1) affine
+    else:
+        pk_ok = None
+        a = [fl["a%d" % i] for i in range(32)]
+        b = [fl["b%d" % i] for i in range(32)]
+        P1 = g1_glv_mul(pk, a, b)
+        P2 = g1_glv_mul(Jac(g1x, g1ny, g.one()), a, b)
+    # the Miller loop takes every point projective (no inversion)
+    if P2 is None:
+        P2 = Jac(g1x, g1ny, g.one())
+        p2_inf = Flag(g, None, False)
+    else:
+        p2_inf = g.is_zero(P2.Z)
+    void1 = g.is_zero(P1.Z) | H.Z.is_zero()
+    void2 = sig_inf | p2_inf
+    f = miller2([(P1, H, void1), (P2, sig, void2)])
+    for k, x in enumerate(f.fps()):
+        g.output("f%d" % k, x)
+    g.output_flag("on_curve", on_curve)
+    g.output_flag("in_group", in_group)
+    if pk_ok is not None:
+        g.output_flag("pk_in_group", pk_ok)
+    return g
+
+
+def mul_program() -> Graph:
+    g = Graph("fp12_mul")
+    a = Fp12.from_fps([g.input_raw("a%d" % k) for k in range(12)])
+    b = Fp12.from_fps([g.input_raw("b%d" % k) for k in range(12)])
+    for k, x in enumerate((a * b).fps()):
+        g.output("f%d" % k, x)
+    return g
+
+
+def final_program() -> Graph:
+    g = Graph("final_exp")
+    f = Fp12.from_fps([g.input_raw("f%d" % k) for k in range(12)])
+    g.output_flag("is_one", final_exp(f).is_one())
+    return g

@@ -6,20 +6,28 @@ they only merge forms.  A product, select, inversion or predicate creates a
 node whose operands are forms -- the device unit evaluates each form limb-wise
 (bls_coop.h), so e.g. a Karatsuba operand (a0 + a1) costs no round of its own.
 
-Every materialized node has an exclusive upper bound on its (non-canonical)
-value; the latency path keeps all of them below 2^383 (bls_coop.h), so a
-form's worst case sum_pos c B + K p (K p covering the negative terms) decides
-whether its unit must reduce it before use.
+Arithmetic domain: 13-limb Montgomery form, R = 2^416 (bls_coop.h).  Every
+materialized node has an exclusive upper bound on its (non-canonical) value; a
+product of operands x, y is < x y / 2^416 + p, so products of forms up to
+~2^399 stay below 2^383 with no reduction, and a form's worst case
+sum_pos c B + K p (K p covering the negative terms) decides whether its unit
+reduces it first (rare).  Inputs arrive canonical in the one-lane code's
+Montgomery form (R = 2^384) and are converted by one product each.
 """
 from __future__ import annotations
 
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
-R = 1 << 384
+R = 1 << 416              # Montgomery radix of the latency path (13 x 32-bit limbs)
+R384 = 1 << 384           # the one-lane code's radix (inputs)
 RINV = pow(R, -1, P)
 B383 = 1 << 383
 LIMIT = 1 << 404          # a form's worst case must stay below this (reduce's quotient estimate)
 RED_BOUND = 11 * P // 10  # bound after reduce (< 1.1 p)
-MAX_TERMS = 16            # larger forms are materialized before a unit uses them
+MUL_LIMIT = R * (B383 - P - 1)  # operand bounds' product for a product < 2^383
+LIN_REDUCE = 1 << 390     # a materialized form above this is reduced first
+MAX_TERMS = 16            # larger operand forms are materialized before a unit uses them
+MAX_LIN_TERMS = 64        # a materializing (LIN) unit takes up to this many terms
+IN_CONV = R * R * pow(R384, -1, P) % P  # mont384(v) * IN_CONV / R = mont416(v)
 
 
 def mont(v: int) -> int:
@@ -55,8 +63,17 @@ class Graph:
         return len(self.kind) - 1
 
     def input(self, name: str) -> "Fp":
-        """A canonical (< p) Montgomery-form input, loaded before round 0."""
+        """An input given canonical in Montgomery form with R = 2^384 (the one-lane
+        code's form), loaded before round 0 and converted by one product."""
         n = self._new("in", (self.n_in,), P)
+        self.in_names.append(name)
+        self.n_in += 1
+        return self.mul(Fp(self, {n: 1}), self._const_stored(IN_CONV))
+
+    def input_raw(self, name: str) -> "Fp":
+        """An input already in this domain (R = 2^416), e.g. a Miller value passed
+        between programs."""
+        n = self._new("in", (self.n_in,), B383)
         self.in_names.append(name)
         self.n_in += 1
         return Fp(self, {n: 1})
@@ -121,7 +138,8 @@ class Graph:
         n = self._lin_cache.get(key)
         if n is not None:
             return n
-        if len(t) > MAX_TERMS or self.form_stats(t)[0] >= LIMIT:
+        if len(t) > MAX_LIN_TERMS or self.form_stats(t)[0] >= LIMIT:
+            assert len(t) > 1, "a single term out of range: materialize the chain earlier"
             # split into materialized halves
             items = list(key)
             half = len(items) // 2
@@ -131,7 +149,7 @@ class Graph:
         else:
             op = key
         worst, _ = self.form_stats(dict(op))
-        n = self._new("lin", (op,), min(worst, RED_BOUND) if worst > B383 else worst)
+        n = self._new("lin", (op,), RED_BOUND if worst > LIN_REDUCE else worst)
         self._lin_cache[key] = n
         return n
 
@@ -141,24 +159,44 @@ class Graph:
             return Fp(self, {})
         x = self.operand(a)
         y = self.operand(b)
-        bx = self._op_bound(x)
-        by = self._op_bound(y)
-        n = self._new("mul", (x, y), min(bx * by // R + P + 1, B383))
+        bx = self.form_stats(dict(x))[0]
+        by = self.form_stats(dict(y))[0]
+        rx = ry = 0
+        # reduce the larger operand(s) until the product stays below 2^383
+        while bx * by >= MUL_LIMIT:
+            if bx >= by and not rx:
+                rx, bx = 1, RED_BOUND
+            elif not ry:
+                ry, by = 1, RED_BOUND
+            else:
+                rx, bx = 1, RED_BOUND
+        n = self._new("mul", (x, y, rx, ry), bx * by // R + P + 1)
+        assert self.bound[n] <= B383
         return Fp(self, {n: 1})
 
     def _op_bound(self, op) -> int:
         worst, _ = self.form_stats(dict(op))
-        return RED_BOUND if worst > B383 else worst
+        return RED_BOUND if worst > LIN_REDUCE else worst
 
     def select(self, flag: "Flag", a: "Fp", b: "Fp") -> "Fp":
         """flag ? a : b"""
-        if flag.const is not None:
-            return a if flag.const else b
-        if a.t == b.t:
-            return a
-        x = self.operand(a)
-        y = self.operand(b)
-        n = self._new("sel", (flag.n, x, y), max(self._op_bound(x), self._op_bound(y), 1))
+        return self.select_n([(flag, a)], b)
+
+    def select_n(self, cases, default: "Fp") -> "Fp":
+        """The value of the first case whose flag is set, else default: ONE unit
+        (the flags are row-uniform; the unit evaluates only the chosen form)."""
+        live = []
+        for fl, v in cases:
+            if fl.const is None:
+                live.append((fl, v))
+            elif fl.const:
+                default = v
+                break
+        if all(v.t == default.t for _, v in live):
+            return default
+        ops = tuple(self.operand(v) for _, v in live) + (self.operand(default),)
+        flags = tuple(fl.n for fl, _ in live)
+        n = self._new("sel", (flags, ops), max([self._op_bound(o) for o in ops] + [1]))
         return Fp(self, {n: 1})
 
     def inv(self, a: "Fp") -> "Fp":
@@ -202,10 +240,9 @@ class Graph:
 
     # ---- outputs -----------------------------------------------------------
     def output(self, name: str, f: "Fp", canonical: bool = False):
-        if canonical:
-            n = self.canon(f).node()
-        else:
-            n = self.materialize(f) if f.t else self.materialize(Fp(self, {self.const(0).node_or_zero(): 1}))
+        if not f.t:
+            f = self._const_stored(0)
+        n = self.canon(f).node() if canonical else self.materialize(f)
         self.outs.append((name, n))
 
     def output_flag(self, name: str, fl: "Flag"):
@@ -275,9 +312,6 @@ class Fp:
         assert c == 1
         return n
 
-    def node_or_zero(self) -> int:
-        return self.node()
-
     def is_zero_form(self) -> bool:
         return not self.t
 
@@ -321,12 +355,29 @@ class Flag:
         return self.g.fop("not", self, None)
 
 
+def _parts(x):
+    if isinstance(x, tuple):
+        return list(x)
+    return [getattr(x, s) for s in type(x).__slots__]
+
+
+def _rebuild(x, parts):
+    if isinstance(x, tuple):
+        return tuple(parts)
+    return type(x)(*parts)
+
+
+def select_n(cases, default):
+    """First case (flag, value) whose flag is set, else default, on Fp or
+    structure-wise on tuples / tower elements / points (classes whose
+    __slots__ are their constructor arguments)."""
+    if isinstance(default, Fp):
+        return default.g.select_n(list(cases), default)
+    dp = _parts(default)
+    cps = [(f, _parts(v)) for f, v in cases]
+    return _rebuild(default, [select_n([(f, vp[i]) for f, vp in cps], dp[i]) for i in range(len(dp))])
+
+
 def select(flag: Flag, a, b):
-    """flag ? a : b on Fp or on tuples / tower elements (structure-wise)."""
-    if isinstance(a, Fp):
-        return a.g.select(flag, a, b)
-    if hasattr(a, "map2"):
-        return a.map2(lambda x, y: select(flag, x, y), b)
-    if isinstance(a, tuple):
-        return tuple(select(flag, x, y) for x, y in zip(a, b))
-    raise TypeError(type(a))
+    """flag ? a : b (structure-wise)"""
+    return select_n([(flag, a)], b)

@@ -169,6 +169,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_signing_roots_attestation_device.argtypes = [vp, u32, vp, vp, u32, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
+    lib.lb_lp_program_run.argtypes = [vp, u32, vp, ctypes.c_size_t, u32, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float),
+                                      vp]
     for name in EXPORTED_SYMBOLS:
         getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int
     _lib = lib
@@ -708,6 +710,30 @@ class Device:
         out = np.zeros(max(n, 1) * 96, np.uint8)
         self._check(self.lib.lb_sign(self._h, n, _ptr(k), _ptr(m), _ptr(out)), "lb_sign")
         return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
+
+    def lp_program_run(self, prog, inputs: np.ndarray, flags: np.ndarray, n_out: int, n_outflag: int,
+                       stamps: bool = False):
+        """One latency-path round program on n instances (lb_lp_program_run): prog = an
+        embedded program id or an encoded program (list of u32 words); inputs (n, n_in, 16)
+        u32 limb records, flags (n, n_inflag) u32 -> (out (n, n_out, 16), out_flags
+        (n, n_outflag), kernel ms[, per-round s_memtime stamps of instance 0])."""
+        inputs = np.ascontiguousarray(inputs, dtype=np.uint32)
+        n = inputs.shape[0]
+        fl = np.ascontiguousarray(flags, dtype=np.uint32) if flags is not None and flags.size else None
+        out = np.zeros((n, max(n_out, 1), 16), np.uint32)
+        ofl = np.zeros((n, max(n_outflag, 1)), np.uint32)
+        ms = ctypes.c_float(0)
+        words = None
+        if not isinstance(prog, int):
+            words = np.ascontiguousarray(np.array(prog, dtype=np.uint32))
+        n_rounds = int(words[1]) if words is not None else 4096
+        st = np.zeros(n_rounds, np.uint64) if stamps else None
+        self._check(self.lib.lb_lp_program_run(self._h, 0 if words is not None else prog, _ptr(words),
+                                               0 if words is None else words.size, n, _ptr(inputs), _ptr(fl),
+                                               _ptr(out), _ptr(ofl) if n_outflag else None, ctypes.byref(ms),
+                                               _ptr(st)), "lb_lp_program_run")
+        res = (out[:, :n_out], ofl[:, :n_outflag], float(ms.value))
+        return res + (st,) if stamps else res
 
     def last_stage_times(self) -> List[Tuple[str, float]]:
         ms = (ctypes.c_float * 32)()

@@ -1,0 +1,120 @@
+"""CPU checks of the latency path's round programs (lodestar_amd/lpgen): every
+program is compiled exactly as the build does and executed by the big-integer
+executor of its ENCODED words (lpgen.compile.Program.run: the device's
+arithmetic, value bounds asserted), against the oracle: hash_to_G2 inside the
+set programs (through the Miller value's final exponentiation), decompression
+and subgroup flags, core verify and the batch form with a random scalar, the
+Fp12 product and the final exponentiation."""
+import functools
+
+import pytest
+
+from lodestar_amd.lpgen import bls, compile as lpc
+from oracle import bls12_381 as O
+from tests.lp_helper import P, f12_fps, f12_from_out, mont, mont416, sample_sets, set_inputs
+
+
+@functools.lru_cache(maxsize=None)
+def prog(name):
+    g = {"single": lambda: bls.set_program(True), "batch": lambda: bls.set_program(False),
+         "mul": bls.mul_program, "final": bls.final_program}[name]()
+    return lpc.compile_graph(g, rows=32)
+
+
+def run_set(single, pk, msg, sig, raw=0):
+    fps, flags = set_inputs(pk, msg, sig, raw)
+    outs, oflags = prog("single" if single else "batch").run([mont(v) for v in fps], flags)
+    return f12_from_out(outs), oflags
+
+
+def test_program_shapes():
+    for name in ("single", "batch", "mul", "final"):
+        p = prog(name)
+        assert p.stats["regs"] <= 1024 and p.stats["flags"] <= 512
+    assert prog("single").n_rounds < 2600 and prog("final").n_rounds < 520
+
+
+def test_final_exp_program():
+    one = O.f12_mul(O.miller_loop(O.G1, O.G2), O.miller_loop(O.E1.neg(O.G1), O.G2))
+    not_one = O.miller_loop(O.G1, O.G2)
+    for f, want in ((one, 1), (not_one, 0)):
+        _, fl = prog("final").run([mont416(v) for v in f12_fps(f)], [])
+        assert fl == [want]
+        assert bool(want) == O.f12_is_one(O.final_exp(f))
+
+
+def test_mul_program():
+    a = O.miller_loop(O.G1, O.G2)
+    b = O.miller_loop(O.g1_mul(O.G1, 5), O.G2)
+    outs, _ = prog("mul").run([mont416(v) for v in f12_fps(a) + f12_fps(b)], [])
+    assert f12_from_out(outs) == O.f12_mul(a, b)
+
+
+@pytest.mark.parametrize("single", [True, False])
+def test_set_program_valid_and_wrong_message(single):
+    pks, msgs, sigs = sample_sets(2)
+    raw = 0 if single else 0xDEADBEEF12345678
+    f, fl = run_set(single, pks[0], msgs[0], sigs[0], raw)
+    assert all(fl) and O.f12_is_one(O.final_exp(f))
+    f, fl = run_set(single, pks[0], msgs[1], sigs[0], raw)  # wrong message
+    assert all(fl) and not O.f12_is_one(O.final_exp(f))
+    # the Miller value itself: e(pk, H) e(-g1, sig) up to the final exponentiation
+    if single:
+        f, _ = run_set(True, pks[1], msgs[1], sigs[1])
+        H = O.hash_to_g2(msgs[1])
+        ref = O.f12_mul(O.miller_loop(pks[1], H), O.miller_loop(O.E1.neg(O.G1), O.signature_from_bytes(sigs[1])))
+        assert O.final_exp(f) == O.final_exp(ref)
+
+
+def test_set_program_uncompressed_and_not_on_curve():
+    pks, msgs, sigs = sample_sets(1)
+    s = O.signature_from_bytes(sigs[0])
+    f, fl = run_set(True, pks[0], msgs[0], O.g2_to_bytes(s, compressed=False))
+    assert all(fl) and O.f12_is_one(O.final_exp(f))
+    # an x with no point on the curve: on_curve flag clear
+    b = bytearray(sigs[0])
+    for k in range(1, 50):
+        b[95] = (b[95] + 1) & 255
+        x1 = int.from_bytes(bytes(b[:48]), "big") & ((1 << 381) - 1)
+        x0 = int.from_bytes(bytes(b[48:]), "big")
+        rhs = O.f2_add(O.f2_mul(O.f2_sqr((x0, x1)), (x0, x1)), (4, 4))
+        if not O.f2_is_square(rhs):
+            break
+    _, fl = run_set(True, pks[0], msgs[0], bytes(b))
+    assert fl[0] == 0
+
+
+def test_set_program_not_in_subgroup():
+    # a point on E2 outside G2: a hashed point before cofactor clearing
+    pks, msgs, _ = sample_sets(1)
+    u = O.hash_to_field_fp2(b"not in G2", 2, O.DST_POP)
+    q = O.iso_map_g2(O.map_to_curve_sswu(u[0]))
+    assert O.E2.on_curve(q) and not O.g2_in_subgroup(q)
+    _, fl = run_set(True, pks[0], msgs[0], O.g2_to_bytes(q))
+    assert fl[0] == 1 and fl[1] == 0
+
+
+def test_set_program_pk_not_in_g1():
+    pks, msgs, sigs = sample_sets(1)
+    # a point on E1 outside G1 (x = 0 is not on E1: search small x)
+    x = 1
+    while True:
+        rhs = (x * x * x + 4) % P
+        if pow(rhs, (P - 1) // 2, P) == 1:
+            y = pow(rhs, (P + 1) // 4, P)
+            if not O.g1_in_subgroup((x, y)):
+                break
+        x += 1
+    _, fl = run_set(True, (x, y), msgs[0], sigs[0])
+    assert fl[2] == 0
+    _, fl = run_set(True, pks[0], msgs[0], sigs[0])
+    assert fl[2] == 1
+
+
+def test_batch_scalar_in_g1():
+    """sum over a 2-set batch: prod f_i -> final exp == 1 iff both valid"""
+    pks, msgs, sigs = sample_sets(2)
+    fs = [run_set(False, pks[i], msgs[i], sigs[i], 0x1111 * (i + 3) + (i << 40))[0] for i in range(2)]
+    assert O.f12_is_one(O.final_exp(O.f12_mul(fs[0], fs[1])))
+    bad = run_set(False, pks[1], msgs[0], sigs[1], 0x5555)[0]
+    assert not O.f12_is_one(O.final_exp(O.f12_mul(fs[0], bad)))

@@ -1,0 +1,120 @@
+"""Latency-path round costs on the GPU (diagnostic; writes gpurun_out/lp_probe.json).
+
+* synthetic chains: N rounds of one Fp product (x = x^2), of one linear unit,
+  of 32 products per round -> microseconds per round of each kind;
+* the embedded set/final programs with per-round s_memtime stamps of instance 0,
+  summarised by round composition (rounds holding an inversion / a product /
+  only linear units / only predicates and flag ops)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from lodestar_amd.lpgen import compile as lpc  # noqa: E402
+from lodestar_amd.lpgen.dsl import Graph  # noqa: E402
+from lodestar_amd.native import Device  # noqa: E402
+
+TICK_GHZ = 0.1  # s_memtime on gfx950 counts at the 100 MHz reference clock? calibrated below
+
+
+def chain(kind, n, width=1):
+    g = Graph("chain_%s_%d" % (kind, width))
+    xs = [g.input("x%d" % i) for i in range(width)]
+    for _ in range(n):
+        if kind == "mul":
+            xs = [x * x for x in xs]
+        else:
+            xs = [(x + x + x).mat() for x in xs]
+    for i, x in enumerate(xs):
+        g.output("o%d" % i, x)
+    return lpc.compile_graph(g, rows=32)
+
+
+def composition(words):
+    n_rounds = words[1]
+    n_const, n_in, n_inflag, n_out, n_outflag = words[4:9]
+    boff = 10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag
+    kinds = []
+    for r in range(n_rounds):
+        bw, nu = words[boff], words[boff + 1]
+        ops = {words[boff + 4 + 20 * u] & 15 for u in range(nu)}
+        boff += bw
+        if 3 in ops:
+            k = "inv"
+        elif 0 in ops:
+            k = "mul"
+        elif 1 in ops or 2 in ops or 4 in ops:
+            k = "lin/sel"
+        else:
+            k = "pred/flag"
+        kinds.append((k, nu, bw))
+    return kinds
+
+
+def main():
+    dev = Device(0)
+    out = {}
+    rng = np.random.default_rng(1)
+    for kind, width in (("mul", 1), ("lin", 1), ("mul", 32), ("mul", 4)):
+        p = chain(kind, 2000, width)
+        ins = np.zeros((1, width, 16), np.uint32)
+        ins[0, :, :11] = rng.integers(0, 2 ** 32, (width, 11), dtype=np.uint64).astype(np.uint32)
+        ms_list = []
+        for _ in range(3):
+            _, _, ms = dev.lp_program_run(p.words, ins, np.zeros((1, 0), np.uint32), width, 0)
+            ms_list.append(ms)
+        ms = min(ms_list)
+        out["chain_%s_w%d" % (kind, width)] = {"rounds": p.n_rounds, "ms": ms, "us_per_round": 1000 * ms / p.n_rounds}
+        print(kind, width, p.n_rounds, "rounds", "%.3f ms" % ms, "%.3f us/round" % (1000 * ms / p.n_rounds), flush=True)
+    # the embedded programs with stamps
+    from lodestar_amd.lpgen import bls
+    from tests.lp_helper import mont, sample_sets, set_inputs
+    pks, msgs, sigs = sample_sets(1)
+    fp, fl = set_inputs(pks[0], msgs[0], sigs[0])
+    rec = np.zeros((1, 11, 16), np.uint32)
+    for i, v in enumerate(fp):
+        mv = mont(v)
+        for j in range(12):
+            rec[0, i, j] = (mv >> (32 * j)) & 0xFFFFFFFF
+    gen = {"set_single": bls.set_program(True), "final": bls.final_program()}
+    for name, pid in (("set_single", 0), ("final", 3)):
+        p = lpc.compile_graph(gen[name], rows=32)
+        kinds = composition(p.words)
+        if name == "final":
+            rec_f = np.zeros((1, 12, 16), np.uint32)
+            rec_f[0, :, 0] = 1
+            ins, flg, no, nof = rec_f, np.zeros((1, 0), np.uint32), 0, 1
+        else:
+            ins, flg, no, nof = rec, np.array([fl], np.uint32), 12, 3
+        best = None
+        for _ in range(3):
+            t0 = time.time()
+            _, _, ms, st = dev.lp_program_run(p.words, ins, flg, no, nof, stamps=True)
+            if best is None or ms < best[0]:
+                best = (ms, st.copy())
+        ms, st = best
+        d = np.diff(st.astype(np.int64))
+        summ = {}
+        for (k, nu, bw), dt in zip(kinds[1:], d):
+            s = summ.setdefault(k, [0, 0])
+            s[0] += 1
+            s[1] += int(dt)
+        out[name] = {"rounds": p.n_rounds, "ms": ms, "us_per_round": 1000 * ms / p.n_rounds,
+                     "ticks_total": int(st[-1]) - int(st[0]),
+                     "by_kind": {k: {"rounds": v[0], "ticks": v[1], "ticks_per_round": v[1] / max(v[0], 1)}
+                                 for k, v in summ.items()},
+                     "slowest_rounds": [(int(i) + 1, kinds[int(i) + 1][0], int(d[i])) for i in np.argsort(d)[-8:]]}
+        print(name, json.dumps(out[name]), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "lp_probe.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    dev.close()
+
+
+if __name__ == "__main__":
+    main()
