@@ -50,7 +50,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # flight fill the SIMDs better: 2.74 / 2.89 / 2.98 / 3.03 M sets/s at 4 / 8 / 12 / 16
 # (profiles/ab_r03/hwq, hwq2).  Set before HIP initialises (torch import); the N-API
 # addon does the same for a Lodestar process (LB_HW_QUEUES overrides both).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LB_HW_QUEUES", "16")
+# (clamped to 16: lb_create refuses more, each queue reserving scratch for the largest
+# private segment at full occupancy)
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(16, int(os.environ.get("LB_HW_QUEUES", "16")))))
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001

@@ -47,6 +47,7 @@ extern "C" {
 #define LB_ERR_DEVICE (-2)           /* HIP runtime failure (maps to Promise rejection, index.ts:503-512) */
 #define LB_ERR_NO_DEVICE (-3)        /* no GPU / bad ordinal                      */
 #define LB_ERR_OUT_OF_MEMORY (-4)
+#define LB_ERR_RESOURCES (-5)        /* lb_create: more hardware queues than the scratch reservation allows */
 
 /* ---- per-request error codes (lb_verify_requests out_request_error) ----- */
 #define LB_REQ_OK 0
@@ -79,14 +80,29 @@ typedef struct lb_ctx lb_ctx;
 int lb_create(int device, lb_ctx** out_ctx);
 /* Release device memory and streams.  Safe on NULL. */
 int lb_destroy(lb_ctx* ctx);
-/* Human-readable message for the last error on this context (never NULL). */
+/* Human-readable message for the last error on this context (never NULL); with
+ * ctx == NULL, why the last lb_create failed. */
 const char* lb_last_error(const lb_ctx* ctx);
 /* Calls the context keeps in flight on the async entry points (one per HIP hardware
  * queue of the process: GPU_MAX_HW_QUEUES, 4 by default, up to 16; LB_SLOTS overrides):
- * the capacity a host keeps busy (the pool's worker count, multithread/index.ts:47). */
+ * the capacity a host keeps busy (the pool's worker count, multithread/index.ts:47).
+ * lb_create refuses GPU_MAX_HW_QUEUES > 16 with LB_ERR_RESOURCES: every queue reserves
+ * scratch for the largest private segment at full occupancy (lb_scratch_per_queue). */
 int lb_slots(const lb_ctx* ctx);
 /* Number of visible HIP devices (0 when none). */
 int lb_device_count(void);
+/* Scratch one hardware queue reserves for the library's kernels: the largest
+ * private segment per lane (*out_lane_bytes, optional) x 64 lanes x 32 waves per
+ * CU x CUs (*out_bytes). */
+int lb_scratch_per_queue(int device, uint64_t* out_bytes, uint32_t* out_lane_bytes);
+/* Calls (lb_verify_requests*, same-message packages' aggregated sets) of at most
+ * max_sets sets run the latency path: one workgroup per set executing the
+ * verification as a round program of row-cooperative Fp products (~2 ms for one
+ * set instead of ~17 ms), each request verified on its own; larger calls run the
+ * throughput pipeline (merged check, bucket MSM, step-major Miller accumulation).
+ * Default 1024 (LB_LP_MAX); 0 disables it.  The reference's analogue is the
+ * main-thread path for latency-critical callers (BN/chain/bls/multithread/index.ts:174-187). */
+int lb_set_latency_path(lb_ctx* ctx, uint32_t max_sets);
 
 /*
  * A batch of verification requests.  A request is one BlsWorkReq (one

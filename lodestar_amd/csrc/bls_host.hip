@@ -103,6 +103,8 @@ struct SmState {
   const uint8_t* d_msgs = nullptr;
   const uint8_t* d_seed = nullptr;
   size_t ws_off = 0;                 // bump offset after phase 1 (phase 2 allocates from here)
+  int err = 0;                       // a failed phase-2 launch: reported by this ticket's wait
+  std::string err_msg;
 };
 
 // One in-flight call: two streams (DAG), own workspace, staging and events.
@@ -166,6 +168,11 @@ struct lb_ctx {
   Slot slots[kMaxSlots];
   int next_slot = 0;
   uint64_t next_ticket = 1;
+  // the last tickets issued to two-phase calls: lb_verify_requests_finish accepts a
+  // ticket whose call a slot reuse already resumed only if it is one of these
+  static constexpr int kTwoPhaseRing = 256;
+  uint64_t two_phase[kTwoPhaseRing] = {};
+  int two_phase_pos = 0;
   std::string err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
   // Miller organisation: stored lines + one wave per pair (k_lines/k_pair_wc,
@@ -226,8 +233,11 @@ struct lb_ctx {
   uint8_t* d_aux = nullptr;
   uint8_t* h_aux = nullptr;
   size_t aux_cap = 0;
-  // latency path: the round programs in device memory (uploaded on first use)
+  // latency path: the round programs in device memory (uploaded on first use);
+  // calls of at most lp_max_sets sets run it instead of the throughput pipeline
+  // (LB_LP_MAX, lb_set_latency_path; 0 = never)
   uint32_t* d_lp = nullptr;
+  uint32_t lp_max_sets = 1024;
 };
 
 namespace {
@@ -333,6 +343,66 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
     LB_HIP(hipGetLastError());                                                             \
   } while (0)
 
+int lp_ensure(lb_ctx* ctx);
+
+// The latency path (k_lp.hip) for a small call: pubkeys -> per-set inputs -> one
+// workgroup per set (set program, the request's product tree, the root's final
+// exponentiation).  No merged check: every request is verified on its own, in
+// parallel, which is what the reference's verdicts are per request anyway.
+int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off, const uint8_t* d_pks,
+           const uint32_t* d_pk_off, const uint32_t* d_pk_idx, const uint8_t* d_msgs, const uint8_t* d_sigs,
+           const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
+           uint8_t* d_set_status, Bump& ws) {
+  LB_TRY(lp_ensure(ctx));
+  const uint32_t ns = n_sets ? n_sets : 1;
+  g1j* d_pk = ws.take<g1j>(ns);
+  uint8_t* d_pk_st = ws.take<uint8_t>(ns);
+  uint32_t* d_in16 = ws.take<uint32_t>((size_t)ns * LB_LP_NIN * 16);
+  uint32_t* d_fl = ws.take<uint32_t>((size_t)ns * LB_LP_NFL);
+  uint8_t* d_sig_st = d_set_status ? d_set_status : ws.take<uint8_t>(ns);
+  uint32_t* d_setreq = ws.take<uint32_t>(ns);
+  uint32_t* d_F = ws.take<uint32_t>((size_t)ns * 12 * 16);
+  uint32_t* d_cnt = ws.take<uint32_t>((size_t)LB_LP_TREE_LEVELS * ns);
+  if (ws.off > ws.cap) {
+    ctx->err = "workspace overflow";
+    return LB_ERR_OUT_OF_MEMORY;
+  }
+  LB_HIP(hipMemsetAsync(d_valid, 0, n_req, sl.st[0]));
+  LB_HIP(hipMemsetAsync(d_req_err, 0, n_req, sl.st[0]));
+  if (!n_sets) return LB_OK;  // every request empty: false
+  LB_HIP(hipMemsetAsync(d_cnt, 0, (size_t)LB_LP_TREE_LEVELS * ns * sizeof(uint32_t), sl.st[0]));
+  const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
+  LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
+  if (d_pk_off)
+    LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, n_sets < 16384u ? n_sets : 16384u, TPB, n_sets, src, d_pk_off, d_pk,
+             d_pk_st);
+  LB_STAGE("lp_prep", 0, k_lp_prep, blocks_for(n_sets), TPB, n_sets, d_req_off, n_req, d_msgs, d_sigs, d_sig_off,
+           (const g1j*)d_pk, d_seed, d_in16, d_fl, d_sig_st, d_setreq);
+  LpCall c;
+  c.prog_single = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SET_SINGLE].off;
+  c.prog_batch = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SET_BATCH].off;
+  c.prog_mul = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MUL].off;
+  c.prog_final = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_FINAL].off;
+  c.req_off = d_req_off;
+  c.set_req = d_setreq;
+  c.in16 = d_in16;
+  c.flags = d_fl;
+  c.sig_st = d_sig_st;
+  c.pk_st = d_pk_st;
+  c.F = d_F;
+  c.cnt = d_cnt;
+  c.valid = d_valid;
+  c.req_err = d_req_err;
+  c.n_sets = n_sets;
+  LB_STAGE("lp_verify", 0, k_lp_verify, n_sets, LB_LP_TPB, c);
+  PipeState& ps = sl.ps;
+  ps = PipeState{};
+  ps.n_req = n_req;
+  ps.n_sets = n_sets;
+  ps.d_valid = d_valid;
+  return LB_OK;
+}
+
 // stream `to` of the slot waits for everything enqueued so far on stream `from`
 int stream_wait(lb_ctx* ctx, Slot& sl, int from, int to, int ev) {
   LB_HIP(hipEventRecord(sl.dep[ev], sl.st[from]));
@@ -390,6 +460,11 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // d_sig_pre / d_sst_pre: signatures already decoded and validated (same-message
   // phase 2): no k_decode_sigs, d_sigs / d_sig_off unused
   const bool partial = d_partial != nullptr;
+  if (!partial && !d_sig_pre && n_sets <= ctx->lp_max_sets) {
+    sl.h_stats[0] = sl.h_stats[1] = 0;
+    return run_lp(ctx, sl, n_req, n_sets, d_req_off, d_pks, d_pk_off, d_pk_idx, d_msgs, d_sigs, d_sig_off, d_seed,
+                  d_valid, d_req_err, d_set_status, ws);
+  }
   const uint32_t ns = n_sets ? n_sets : 1;
   g2j* d_sig = d_sig_pre ? const_cast<g2j*>(d_sig_pre) : ws.take<g2j>(ns);
   g2j* d_rsig = ws.take<g2j>(ns);
@@ -771,7 +846,17 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
     return LB_OK;
   }
   LB_TRY(finish_partial(ctx, sl, false));
-  while (sl.sm.active) LB_TRY(sm_advance(ctx, sl, true));  // same-message: phases 1 and 2
+  while (sl.sm.active && sm_advance(ctx, sl, true) == LB_OK) {
+  }  // same-message: phases 1 and 2
+  if (sl.sm.err) {  // its phase 2 failed to launch (here or in another call's sm_pump)
+    const int rc = sl.sm.err;
+    ctx->err = sl.sm.err_msg;
+    sl.sm.err = 0;
+    for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(sl.st[i]);
+    release_borrowed(sl);
+    sl.busy = false;
+    return rc;
+  }
   LB_HIP(hipEventSynchronize(sl.done));
   ctx->n_stages = sl.n_stages;
   for (int i = 0; i < sl.n_stages; i++) {
@@ -835,6 +920,10 @@ int end_call_async(lb_ctx* ctx, Slot& sl) {
   if (!sl.partial_pending) LB_TRY(end_call(ctx, sl));
   sl.busy = true;
   sl.ticket = ctx->next_ticket++;
+  if (sl.partial_pending) {
+    ctx->two_phase[ctx->two_phase_pos] = sl.ticket;
+    ctx->two_phase_pos = (ctx->two_phase_pos + 1) % lb_ctx::kTwoPhaseRing;
+  }
   return LB_OK;
 }
 
@@ -897,6 +986,35 @@ int lb_device_count(void) {
   return n;
 }
 
+// Private-segment (scratch) reservation of one HIP hardware queue.  ROCr backs a
+// queue's scratch for a dispatch at full-device occupancy: private bytes per lane
+// x 64 lanes x 32 waves per CU x CUs, and keeps it for the queue's lifetime, so a
+// process with Q queues that run the pipeline's largest-scratch kernel reserves Q
+// times that.  At 24 queues the first 65,536-set calls failed with
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES (profiles/ab_r03/r03g_q24_fail.txt) with the
+// HBM otherwise free; 16 ran, which is the cap lb_create enforces.
+static std::string g_create_err = "null context";
+
+size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
+  const void* kernels[] = {(const void*)k_miller_acc<16>, (const void*)k_miller_acc<32>,
+                           (const void*)k_miller_acc<64>, (const void*)k_step_acc<0, 1>,
+                           (const void*)k_step_acc<0, 2>, (const void*)k_step_acc<1, 1>, (const void*)k_step_acc<2, 1>, (const void*)k_step_acc<2, 2>, (const void*)k_lines<1>,
+                           (const void*)k_lines<2>, (const void*)k_lines_rows<1>, (const void*)k_lines_rows<2>,
+                           (const void*)k_pair_wc, (const void*)k_miller_sets,
+                           (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
+                           (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
+                           (const void*)k_msm_buckets, (const void*)k_decode_sigs, (const void*)k_scalar_pk};
+  size_t lane = 0;
+  for (const void* k : kernels) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, k) == hipSuccess && a.localSizeBytes > lane) lane = a.localSizeBytes;
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+  if (out_lane_bytes) *out_lane_bytes = (uint32_t)lane;
+  return lane * 64 * 32 * (size_t)cus;
+}
+
 int lb_create(int device, lb_ctx** out_ctx) {
   if (!out_ctx) return LB_ERR_INVALID_ARGUMENT;
   *out_ctx = nullptr;
@@ -911,7 +1029,19 @@ int lb_create(int device, lb_ctx** out_ctx) {
   // left each call's queue idle at its end, profiles/ab_r03/hwq; up to 16)
   if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
     const int v = atoi(e);
-    ctx->n_slots = v < 4 ? 4 : v > lb_ctx::kMaxSlots ? lb_ctx::kMaxSlots : v;
+    if (v > lb_ctx::kMaxSlots) {
+      uint32_t lane = 0;
+      const size_t per_q = scratch_per_queue(device, &lane);
+      char msg[320];
+      snprintf(msg, sizeof msg,
+               "GPU_MAX_HW_QUEUES=%d exceeds %d: %u private bytes per lane reserve %.2f GB of scratch per "
+               "hardware queue (%.1f GB for %d queues); 24 queues failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES",
+               v, lb_ctx::kMaxSlots, lane, per_q / 1e9, per_q * (double)v / 1e9, v);
+      g_create_err = msg;
+      delete ctx;
+      return LB_ERR_RESOURCES;
+    }
+    ctx->n_slots = v < 4 ? 4 : v;
   }
   if (const char* e = getenv("LB_SLOTS")) {
     const int v = atoi(e);
@@ -922,6 +1052,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_LP_MAX")) ctx->lp_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = ctx->lines_waves_small = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
@@ -1013,7 +1144,16 @@ int lb_destroy(lb_ctx* ctx) {
   return LB_OK;
 }
 
-const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+
+int lb_scratch_per_queue(int device, uint64_t* out_bytes, uint32_t* out_lane_bytes) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || device < 0 || device >= n) return LB_ERR_NO_DEVICE;
+  if (!out_bytes) return LB_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(device) != hipSuccess) return LB_ERR_DEVICE;
+  *out_bytes = scratch_per_queue(device, out_lane_bytes);
+  return LB_OK;
+}
 
 int lb_slots(const lb_ctx* ctx) { return ctx ? ctx->n_slots : 0; }
 
@@ -1291,8 +1431,9 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
   if (!sl || !sl->partial_pending) {
     // a two-phase call another call's slot reuse already resumed (with merged_ok
     // = 0: every request re-verified alone, so its verdicts stand): nothing to do
-    if (ticket != 0 && ticket < ctx->next_ticket) return LB_OK;
-    ctx->err = "ticket is not a pending two-phase call";
+    for (int i = 0; ticket != 0 && i < lb_ctx::kTwoPhaseRing; i++)
+      if (ctx->two_phase[i] == ticket) return LB_OK;
+    ctx->err = "ticket is not a two-phase call (or one older than the last 256)";
     return LB_ERR_INVALID_ARGUMENT;
   }
   return finish_partial(ctx, *sl, merged_ok != 0);
@@ -1874,7 +2015,22 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
 // any later library call, so it need not wait for the caller's lb_wait).
 // Phase 2 done: its verdicts.  block = false: return at once when the phase's
 // work is still in flight.
+int sm_advance_launch(lb_ctx* ctx, Slot& sl, bool block);
+
+// One step of a same-message call; a failure ends the call (sm.active cleared) and
+// stays on its slot for its own ticket's wait to report.
 int sm_advance(lb_ctx* ctx, Slot& sl, bool block) {
+  const int rc = sm_advance_launch(ctx, sl, block);
+  if (rc != LB_OK) {
+    sl.sm.active = false;
+    sl.sm.phase = 0;
+    sl.sm.err = rc;
+    sl.sm.err_msg = ctx->err;
+  }
+  return rc;
+}
+
+int sm_advance_launch(lb_ctx* ctx, Slot& sl, bool block) {
   SmState& m = sl.sm;
   if (!m.active) return LB_OK;
   if (!block) {
@@ -1922,7 +2078,6 @@ int sm_advance(lb_ctx* ctx, Slot& sl, bool block) {
       uint8_t* d_rerr = ws.take<uint8_t>(nr);
       if (ws.off > ws.cap) {
         ctx->err = "workspace overflow";
-        m.active = false;
         return LB_ERR_OUT_OF_MEMORY;
       }
       LB_HIP(hipMemcpyAsync(d_rset, m.h_rset, sizeof(uint32_t) * 2 * (size_t)ns, hipMemcpyHostToDevice, sl.st[0]));
@@ -1954,7 +2109,8 @@ int sm_advance(lb_ctx* ctx, Slot& sl, bool block) {
 int sm_pump(lb_ctx* ctx) {
   for (int s = 0; s < ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
-    if (sl.busy && sl.sm.active && sl.sm.phase == 1) LB_TRY(sm_advance(ctx, sl, false));
+    // (another call's failure is not this caller's: it stays on that slot's ticket)
+    if (sl.busy && sl.sm.active && sl.sm.phase == 1) (void)sm_advance(ctx, sl, false);
   }
   return LB_OK;
 }
@@ -2198,7 +2354,7 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
                       float* out_ms, uint64_t* stamps) {
   if (!ctx || n == 0 || !in16 || !out16) return LB_ERR_INVALID_ARGUMENT;
   if (!prog_words && prog >= LB_LP_NPROGS) return LB_ERR_INVALID_ARGUMENT;
-  if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500002u)) return LB_ERR_INVALID_ARGUMENT;
+  if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500003u)) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(helper_slot(ctx));
   const uint32_t* hw = prog_words ? prog_words : lb_lp_blob + LB_LP_PROGS[prog].off;
@@ -2218,6 +2374,12 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
   }
   return lp_program_run(ctx, d_prog, n, n_in, n_inflag, n_out, n_outflag, n_rounds, in16, in_flags, out16, out_flags,
                         out_ms, stamps, ws);
+}
+
+int lb_set_latency_path(lb_ctx* ctx, uint32_t max_sets) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  ctx->lp_max_sets = max_sets;
+  return LB_OK;
 }
 
 int lb_sk_to_pk(lb_ctx* ctx, uint32_t n, const uint8_t* sk32, uint8_t* out96) {

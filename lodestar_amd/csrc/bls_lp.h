@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bls_kernels.h"
+
 #define LB_LP_ROWS 32                     // units per round = 16-lane rows per workgroup
 #define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
 #define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
@@ -12,6 +14,7 @@
 #define LB_LP_RING 8192                   // LDS ring of the program stream (words, power of 2)
 #define LB_LP_CHUNK 1024                  // stream words fetched per round (2 per thread)
 #define LB_LP_HDR 10                      // header words of an encoded program
+#define LB_LP_TREE_LEVELS 20              // product-tree levels (requests up to 2^20 sets)
 
 #define LB_LP_OP_MUL 0
 #define LB_LP_OP_LIN 1
@@ -40,4 +43,31 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_program(const uint32_t* __rest
                                                           uint32_t* __restrict__ out, uint32_t out_stride,
                                                           uint32_t* __restrict__ out_flags, uint32_t oflag_stride,
                                                           unsigned long long* __restrict__ stamps);
+
+// the small-call pipeline (k_lp.hip): one call's device state
+struct LpCall {
+  const uint32_t* prog_single;
+  const uint32_t* prog_batch;
+  const uint32_t* prog_mul;
+  const uint32_t* prog_final;
+  const uint32_t* req_off;
+  const uint32_t* set_req;
+  const uint32_t* in16;
+  const uint32_t* flags;
+  uint8_t* sig_st;    // prep status in, the signature's final status out (LB_SET_*)
+  uint8_t* pk_st;     // k_pubkeys_* status in, + the G1 check of 1-set requests
+  uint32_t* F;        // n_sets x 12 x 16 words: Miller values, then the tree's nodes
+  uint32_t* cnt;      // LB_LP_TREE_LEVELS x n_sets arrival counters (zeroed)
+  uint8_t* valid;     // n_req (zeroed)
+  uint8_t* req_err;   // n_req (zeroed)
+  uint32_t n_sets;
+};
+static constexpr uint32_t LB_LP_NIN = 11, LB_LP_NFL = 67;  // set program inputs / input flags
+__global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __restrict__ req_off, uint32_t n_req,
+                                                 const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ sigs,
+                                                 const uint32_t* __restrict__ sig_off, const g1j* __restrict__ pk,
+                                                 const uint8_t* __restrict__ seed, uint32_t* __restrict__ in16,
+                                                 uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
+                                                 uint32_t* __restrict__ set_req);
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c);
 }  // namespace lb

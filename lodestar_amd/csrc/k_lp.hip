@@ -364,6 +364,204 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
   for (uint32_t i = tid; i < n_outflag; i += LB_LP_TPB) out_flags[i] = S.flag[outfl[i]];
 }
 
+// ---------------------------------------------------------------------------
+// The small-call pipeline (lb_verify_requests on calls of at most lp_max_sets sets):
+//   k_lp_prep     one lane per set: hash_to_field of the signing root, the
+//                 signature's byte-level decode (Signature.fromBytes up to the
+//                 curve arithmetic), the pubkey (from k_pubkeys_*), the batch
+//                 scalar's GLV halves as flags -> the set program's inputs
+//   k_lp_verify   one workgroup per set: the set program (1-set requests: core
+//                 verify; >= 2 sets: the batch equation's factor of this set),
+//                 then the request's product tree across its sets' workgroups
+//                 (the second workgroup to reach a node multiplies), and at the
+//                 root the final exponentiation and the request's verdict.
+// Verdict rules: verifySignatureSetsMaybeBatch (BN/chain/bls/maybeBatch.ts:16-46),
+// exactly as the throughput pipeline applies them (bls_host.hip).
+// ---------------------------------------------------------------------------
+static constexpr uint32_t LP_NIN = LB_LP_NIN, LP_NFL = LB_LP_NFL;
+
+__global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __restrict__ req_off, uint32_t n_req,
+                                                 const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ sigs,
+                                                 const uint32_t* __restrict__ sig_off, const g1j* __restrict__ pk,
+                                                 const uint8_t* __restrict__ seed, uint32_t* __restrict__ in16,
+                                                 uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
+                                                 uint32_t* __restrict__ set_req) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // request of set i (binary search over the offsets)
+  uint32_t lo = 0, hi = n_req;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (req_off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  set_req[i] = lo;
+  uint32_t* rec = in16 + (size_t)i * LP_NIN * 16;
+  uint32_t* fl = flags + (size_t)i * LP_NFL;
+  auto put = [&](int k, const fp& v) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) rec[16 * k + j] = v.l[j];
+#pragma unroll
+    for (int j = 12; j < 16; j++) rec[16 * k + j] = 0u;
+  };
+  uint8_t m[32];
+  for (int k = 0; k < 32; k++) m[k] = msgs[(size_t)i * 32 + k];
+  fp2 u[2];
+  hash_to_field_fp2_2(u, m);
+  put(0, u[0].c0);
+  put(1, u[0].c1);
+  put(2, u[1].c0);
+  put(3, u[1].c1);
+  // Signature.fromBytes up to the curve arithmetic (bls_curve.h g2_deserialize)
+  const uint32_t a = sig_off[i], len = sig_off[i + 1] - a;
+  const uint8_t* b = sigs + a;
+  uint8_t st = LB_ST_OK;
+  bool inf = false, comp = false, sign = false;
+  fp x0, x1, y0, y1;
+  fp_zero(x0);
+  fp_zero(x1);
+  fp_zero(y0);
+  fp_zero(y1);
+  if (len == 0) {
+    st = LB_ST_BAD_ENCODING;
+  } else {
+    const uint8_t f = b[0];
+    comp = (f & 0x80) != 0;
+    if (len != (comp ? 96u : 192u)) {
+      st = LB_ST_BAD_ENCODING;
+    } else if (comp ? (f & 0x40) != 0 : (f & 0xe0) != 0) {
+      if ((f & 0x40) && (f & 0x3f) == 0 && bytes_zero(b + 1, (int)len - 1))
+        inf = true;
+      else
+        st = LB_ST_BAD_ENCODING;
+    } else {
+      sign = comp && (f & 0x20) != 0;
+      bool ok = fp_read_masked(x1, b, comp) && fp_read_masked(x0, b + 48, false);
+      if (ok && !comp) ok = fp_read_masked(y1, b + 96, false) && fp_read_masked(y0, b + 144, false);
+      if (!ok) st = LB_ST_BAD_ENCODING;
+    }
+  }
+  if (st != LB_ST_OK) {
+    fp_zero(x0);
+    fp_zero(x1);
+    fp_zero(y0);
+    fp_zero(y1);
+  }
+  put(4, x0);
+  put(5, x1);
+  put(6, y0);
+  put(7, y1);
+  const g1j p = pk[i];
+  put(8, p.X);
+  put(9, p.Y);
+  put(10, p.Z);
+  sig_st[i] = st;
+  fl[0] = inf ? 1u : 0u;
+  fl[1] = sign ? 1u : 0u;
+  fl[2] = comp ? 1u : 0u;
+  uint8_t sd[32];
+  for (int k = 0; k < 32; k++) sd[k] = seed[k];
+  const uint64_t r = batch_scalar(sd, i);
+  const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+  for (int k = 0; k < 32; k++) {
+    fl[3 + k] = (ra >> (31 - k)) & 1u;
+    fl[35 + k] = (rb >> (31 - k)) & 1u;
+  }
+}
+
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
+  __shared__ LpShared S;
+  __shared__ uint32_t sh_old, sh_bad, sh_err;
+  const uint32_t i = blockIdx.x, tid = threadIdx.x;
+  if (i >= c.n_sets) return;
+  const uint32_t k = c.set_req[i], base = c.req_off[k], n = c.req_off[k + 1] - base;
+  const bool single = n == 1;
+  uint32_t ofl[3];
+  uint32_t* Fi = c.F + (size_t)i * 12 * 16;
+  // 1. the set program
+  {
+    __shared__ uint32_t s_ofl[4];
+    lp_run(S, single ? c.prog_single : c.prog_batch, c.in16 + (size_t)i * LP_NIN * 16, 0xffffffffu, nullptr,
+           c.flags + (size_t)i * LP_NFL, Fi, s_ofl);
+    __syncthreads();
+    ofl[0] = s_ofl[0];
+    ofl[1] = s_ofl[1];
+    ofl[2] = single ? s_ofl[2] : 1u;
+  }
+  if (tid == 0) {
+    uint8_t st = c.sig_st[i];
+    const bool sig_inf = c.flags[(size_t)i * LP_NFL] != 0;
+    if (st == LB_ST_OK) {
+      if (!ofl[0])
+        st = LB_ST_NOT_ON_CURVE;
+      else if (!ofl[1])
+        st = LB_ST_NOT_IN_GROUP;
+      else if (single && sig_inf)
+        st = LB_ST_ZERO_SIGNATURE;
+    }
+    c.sig_st[i] = st;
+    uint8_t ps = c.pk_st[i];
+    if (ps == LB_ST_OK && !ofl[2]) ps = LB_ST_NOT_IN_GROUP;
+    c.pk_st[i] = ps;
+  }
+  // 2. the request's product tree: at level l the node of the positions
+  //    [q, q + 2^(l+1)) multiplies the values at q and q + 2^l; the second of
+  //    the two workgroups to arrive does it and continues upward
+  uint32_t pos = i - base;
+  for (uint32_t level = 0; (1u << level) < n; level++) {
+    const uint32_t step = 1u << level;
+    const uint32_t left = pos & ~(2 * step - 1);
+    if (left + step >= n) continue;  // no right sibling: the value passes up unchanged
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();  // release this workgroup's value (and set status)
+      sh_old = atomicAdd(c.cnt + (size_t)level * c.n_sets + base + left, 1u);
+      __threadfence();
+    }
+    __syncthreads();
+    if (sh_old == 0) return;  // the sibling's workgroup carries on
+    __threadfence();          // acquire the sibling's value
+    uint32_t* Fl = c.F + (size_t)(base + left) * 12 * 16;
+    const uint32_t* Fr = c.F + (size_t)(base + left + step) * 12 * 16;
+    lp_run(S, c.prog_mul, Fl, 12, Fr, nullptr, Fl, nullptr);
+    pos = left;
+  }
+  // 3. root: the request's verdict
+  __syncthreads();
+  __threadfence();
+  if (tid == 0) {
+    sh_bad = 0;
+    sh_err = LB_REQ_OK;
+  }
+  __syncthreads();
+  {
+    uint32_t bad = 0, empty = 0, badpk = 0;
+    for (uint32_t j = tid; j < n; j += LB_LP_TPB) {
+      const uint8_t ss = ((volatile uint8_t*)c.sig_st)[base + j], ps = ((volatile uint8_t*)c.pk_st)[base + j];
+      bad |= (ss != LB_ST_OK || ps != LB_ST_OK) ? 1u : 0u;
+      empty |= ps == LB_ST_EMPTY_AGGREGATE ? 1u : 0u;
+      badpk |= ps == LB_ST_BAD_ENCODING ? 1u : 0u;
+    }
+    if (bad) atomicOr(&sh_bad, 1u);
+    if (empty) atomicOr(&sh_err, 2u);
+    if (badpk) atomicOr(&sh_err, 1u);
+  }
+  __syncthreads();
+  uint32_t ok = 0;
+  if (!sh_bad) {
+    __shared__ uint32_t s_one;
+    lp_run(S, c.prog_final, c.F + (size_t)base * 12 * 16, 0xffffffffu, nullptr, nullptr, nullptr, &s_one);
+    __syncthreads();
+    ok = s_one;
+  }
+  if (tid == 0) {
+    c.valid[k] = ok ? 1 : 0;
+    c.req_err[k] = (sh_err & 2u) ? LB_REQ_EMPTY_AGGREGATE : (sh_err & 1u) ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+  }
+}
+
 // Test / stage entry: instance b runs `prog` on in[b * in_stride ...].
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_program(const uint32_t* __restrict__ prog, uint32_t n,
                                                           const uint32_t* __restrict__ in, uint32_t in_stride,

@@ -89,6 +89,13 @@ def fp2_sqrt(a: Fp2):
 # hash_to_G2 (bls_hash.h): SSWU, 3-isogeny, Q0 + Q1, clear_cofactor
 # ---------------------------------------------------------------------------
 def map_to_curve_sswu(u: Fp2):
+    """Simplified SWU onto E2' (bls_hash.h map_to_curve_sswu) with no inversion on
+    its path: x1 = N / D is kept as a fraction, g(x1) = U / D^3 = W / m with
+    W = U conj(D^3) and m = N(D^3) in Fp, so the norm exponentiation runs on
+    N(g(x1)) = N(W) / m^2 as N(W)^((p-3)/4) * m^((p+1)/2) (two exponentiations in
+    parallel; m^(-2 (p-3)/4) = m^((p+1)/2)) while m^-1 = m^(p-2) runs beside them;
+    from there on the values -- g(x), the norm root, x, y -- are the affine ones
+    of the one-lane code, so the same root and sign come out."""
     g = u.g
     A = c2(g, "LB_SSWU_A")
     B = c2(g, "LB_SSWU_B")
@@ -96,28 +103,34 @@ def map_to_curve_sswu(u: Fp2):
     tv1 = Z * u.sqr()
     tv2 = tv1.sqr() + tv1
     exceptional = tv2.is_zero()
-    t = tv2.inv()
-    t = Fp2(t.c0 + g.one(), t.c1)
-    x1 = t * c2(g, "LB_SSWU_MINUS_B_OVER_A")
-    x1 = select(exceptional, c2(g, "LB_SSWU_B_OVER_ZA"), x1)
-    gx1 = (x1.sqr() + A) * x1 + B
-    x2 = tv1 * x1
-    gx2 = (x2.sqr() + A) * x2 + B
-    n1 = gx1.norm()
-    e = fp_pow(n1, P34)
-    chk = e.sqr() * n1
-    sq1 = g.is_zero(chk - g.one()) | g.is_zero(n1)
-    s1 = n1 * e
+    # x1 = (-B/A)(1 + 1/tv2) = N / D;  tv2 == 0: x1 = B / (Z A)
+    N = select(exceptional, c2(g, "LB_SSWU_B_OVER_ZA"), (tv2 + Fp2.one(g)) * c2(g, "LB_SSWU_MINUS_B_OVER_A"))
+    D = select(exceptional, Fp2.one(g), tv2)
+    D2 = D.sqr()
+    V = D2 * D
+    BV = B * V
+    N2 = tv1 * N  # x2 = tv1 x1 = N2 / D
+    U1 = N * (N.sqr() + A * D2) + BV
+    U2 = N2 * (N2.sqr() + A * D2) + BV
+    Vc = V.conj()
+    W1 = U1 * Vc
+    W2 = U2 * Vc
+    m = V.norm()
+    nW1 = W1.norm()
+    e = fp_pow(nW1, P34) * fp_pow(m, (P + 1) // 2)  # = N(g(x1))^((p-3)/4)
+    minv = fp_pow(m, P - 2)
+    sq1 = g.is_zero(e.sqr() * nW1 - m.sqr()) | g.is_zero(nW1)
+    s1 = (nW1 * e) * minv.sqr()
     nu = u.norm()
     nu3 = nu.sqr() * nu
     s2 = (nu3 * g.const(C["LB_SSWU_NZ3_SQRT"])) * s1
-    s2 = select(sq1, s1, s2)
-    x = select(sq1, x1, x2)
-    gx = select(sq1, gx1, gx2)
+    s = select(sq1, s1, s2)
+    gx = select(sq1, W1, W2) * minv
+    x = (select(sq1, N, N2) * D.conj()) * (D.norm().sqr() * minv)
     # fp2_sqrt_with_norm_root: gx.c1 == 0 takes fp2_sqrt, i.e. its a.c1 == 0 branch
     # (one exponentiation from gx.c0, beside the main one)
     z1 = g.is_zero(gx.c1)
-    y_main = fp2_sqrt_from_norm_root(gx, s2)
+    y_main = fp2_sqrt_from_norm_root(gx, s)
     y = select(z1, fp2_sqrt_in_fp(gx.c0), y_main)
     flip = fp2_sgn0(u) ^ fp2_sgn0(y)
     y = select(flip, -y, y)

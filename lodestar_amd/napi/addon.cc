@@ -35,6 +35,7 @@
 #include <node_api.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstring>
@@ -767,7 +768,7 @@ napi_value New(napi_env env, napi_callback_info info) {
   lb_ctx* ctx = nullptr;
   const int rc = lb_create(device, &ctx);
   if (rc != LB_OK) {
-    napi_throw(env, make_error(env, rc, "lb_create(" + std::to_string(device) + ") failed: no usable HIP device"));
+    napi_throw(env, make_error(env, rc, "lb_create(" + std::to_string(device) + ") failed: " + lb_last_error(nullptr)));
     return nullptr;
   }
   if (capacity <= 0) capacity = lb_slots(ctx);
@@ -821,11 +822,16 @@ napi_value ValidateRequests(napi_env env, napi_callback_info info) {
 }
 
 napi_value Init(napi_env env, napi_value exports) {
-  // 16 HIP hardware queues for this process (LB_HW_QUEUES overrides): the library keeps
-  // one call in flight per queue (lb_slots), 3.03 vs 2.74 M sets/s over HIP's default 4
-  // (profiles/ab_r03/hwq2).  Before the first HIP call (lb_create).
-  const char* q = getenv("LB_HW_QUEUES");
-  setenv("GPU_MAX_HW_QUEUES", q ? q : "16", 1);
+  // 16 HIP hardware queues for this process: the library keeps one call in flight per
+  // queue (lb_slots), 3.03 vs 2.74 M sets/s over HIP's default 4 (profiles/ab_r03/hwq2).
+  // Before the first HIP call (lb_create).  A GPU_MAX_HW_QUEUES the host already set
+  // wins; LB_HW_QUEUES picks another count, clamped to [1, 16] -- lb_create refuses
+  // more (each queue reserves scratch for the largest private segment).
+  int nq = 16;
+  if (const char* q = getenv("LB_HW_QUEUES")) nq = atoi(q) < 1 ? 1 : atoi(q) > 16 ? 16 : atoi(q);
+  char qs[8];
+  snprintf(qs, sizeof qs, "%d", nq);
+  setenv("GPU_MAX_HW_QUEUES", qs, 0);
   // no per-stage timing events in the library (nothing on the JS side reads them; they
   // are two HIP calls per kernel on the submission thread); LB_STAGE_EVENTS=1 keeps them
   setenv("LB_STAGE_EVENTS", "0", 0);

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "lb_aggregate_pubkeys_indexed", "lb_signing_roots_attestation", "lb_signing_roots_chunks",
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
-    "lb_pubkeys_from_bytes", "lb_poll",
+    "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
 )
 
 LB_BATCH_DEVICE = 1
@@ -130,6 +130,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_last_error.restype = ctypes.c_char_p
     lib.lb_slots.argtypes = [vp]
     lib.lb_device_count.argtypes = []
+    lib.lb_scratch_per_queue.argtypes = [i32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     lib.lb_verify_requests.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
     lib.lb_verify_requests_device.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
     lib.lb_verify_same_message.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, ctypes.POINTER(u32)]
@@ -169,6 +170,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_signing_roots_attestation_device.argtypes = [vp, u32, vp, vp, u32, vp]
     lib.lb_sign.argtypes = [vp, u32, vp, vp, vp]
     lib.lb_last_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p), i32]
+    lib.lb_set_latency_path.argtypes = [vp, u32]
     lib.lb_lp_program_run.argtypes = [vp, u32, vp, ctypes.c_size_t, u32, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float),
                                       vp]
     for name in EXPORTED_SYMBOLS:
@@ -246,7 +248,8 @@ class Device:
         h = ctypes.c_void_p()
         rc = self.lib.lb_create(device, ctypes.byref(h))
         if rc != LB_OK:
-            raise LodestarBlsError(f"lb_create({device}) failed with {rc} (no GPU visible?)")
+            msg = self.lib.lb_last_error(None).decode(errors="replace")
+            raise LodestarBlsError(f"lb_create({device}) failed with {rc}: {msg}")
         self._h = h
         self.device = device
 
@@ -711,6 +714,10 @@ class Device:
         self._check(self.lib.lb_sign(self._h, n, _ptr(k), _ptr(m), _ptr(out)), "lb_sign")
         return [out[i * 96:(i + 1) * 96].tobytes() for i in range(n)]
 
+    def set_latency_path(self, max_sets: int) -> None:
+        """Calls of at most max_sets sets take the latency path (0: never)."""
+        self._check(self.lib.lb_set_latency_path(self._h, max_sets), "lb_set_latency_path")
+
     def lp_program_run(self, prog, inputs: np.ndarray, flags: np.ndarray, n_out: int, n_outflag: int,
                        stamps: bool = False):
         """One latency-path round program on n instances (lb_lp_program_run): prog = an
@@ -740,6 +747,16 @@ class Device:
         names = (ctypes.c_char_p * 32)()
         n = self.lib.lb_last_stage_times(self._h, ms, names, 32)
         return [(names[i].decode(), float(ms[i])) for i in range(min(n, 32))]
+
+
+def scratch_per_queue(device: int = 0) -> Tuple[int, int]:
+    """(scratch bytes one hardware queue reserves, largest private bytes per lane)."""
+    lib = load_library()
+    b, lane = ctypes.c_uint64(0), ctypes.c_uint32(0)
+    rc = lib.lb_scratch_per_queue(device, ctypes.byref(b), ctypes.byref(lane))
+    if rc != LB_OK:
+        raise LodestarBlsError(f"lb_scratch_per_queue failed ({rc})")
+    return int(b.value), int(lane.value)
 
 
 def device_count() -> int:

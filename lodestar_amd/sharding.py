@@ -59,7 +59,9 @@ class PackedRequests:
     """Requests already in the C-ABI layout (lb_request_batch): the shape a gossip
     replay of ~1 M sets takes without one Python object per set or per key.
     ``idx`` holds validator indices (device pubkey table) when not None, else
-    ``pks`` the 96-byte keys; ``msgs`` is n_sets x 32 bytes."""
+    ``pks`` the 96-byte keys; with both, a mixed package: ``idx`` entries carrying
+    LB_PK_ROW_FLAG name rows of ``pks`` (keys without a validator index).
+    ``msgs`` is n_sets x 32 bytes."""
     req_off: np.ndarray
     pk_off: np.ndarray
     msgs: np.ndarray
@@ -80,12 +82,23 @@ class PackedRequests:
         a, b = int(self.req_off[lo]), int(self.req_off[hi])
         ka, kb = int(self.pk_off[a]), int(self.pk_off[b])
         sa, sb = int(self.sig_off[a]), int(self.sig_off[b])
+        idx, pks = None, None
+        if self.idx is not None and self.pks is not None:
+            # mixed: keep the rows this slice names, renumbered from 0
+            from .native import LB_PK_ROW_FLAG
+            idx = self.idx[ka:kb].astype(np.uint32)
+            flagged = (idx & LB_PK_ROW_FLAG) != 0
+            rows = (idx[flagged] & ~np.uint32(LB_PK_ROW_FLAG)).astype(np.int64)
+            idx[flagged] = np.uint32(LB_PK_ROW_FLAG) | np.arange(len(rows), dtype=np.uint32)
+            pks = self.pks.reshape(-1, 96)[rows].reshape(-1) if len(rows) else np.zeros(1, np.uint8)
+        elif self.idx is not None:
+            idx = self.idx[ka:kb]
+        elif self.pks is not None:
+            pks = self.pks[96 * ka:96 * kb]
         return PackedRequests(
             (self.req_off[lo:hi + 1] - a).astype(np.uint32), (self.pk_off[a:b + 1] - ka).astype(np.uint32),
             self.msgs[32 * a:32 * b], self.sig_blob[sa:sb] if sb > sa else np.zeros(1, np.uint8),
-            (self.sig_off[a:b + 1] - sa).astype(np.uint32),
-            None if self.idx is None else self.idx[ka:kb],
-            None if self.pks is None else self.pks[96 * ka:96 * kb])
+            (self.sig_off[a:b + 1] - sa).astype(np.uint32), idx, pks)
 
 
 def _two_phase(backend) -> bool:

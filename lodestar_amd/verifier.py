@@ -318,7 +318,8 @@ class DeviceBackend:
         return pc, post
 
     def _submit_packed(self, p, partial: bool):
-        pc = self.dev.verify_requests_async(p.req_off, p.pks if p.idx is None else None, p.pk_off, p.msgs,
+        # (with both idx and pks: a mixed package, flagged indices naming rows of pks)
+        pc = self.dev.verify_requests_async(p.req_off, p.pks, p.pk_off, p.msgs,
                                             p.sig_blob, p.sig_off, self.seed_source(), pk_indices=p.idx,
                                             partial=partial)
 

@@ -23,18 +23,21 @@ def device():
     dev.close()
 
 
-@pytest.fixture(scope="session", params=["lane", "lines", "wave"])
+@pytest.fixture(scope="session", params=["lane", "lines", "wave", "lp"])
 def device_modes(request):
-    """A context per Miller organisation: one pair per lane (k_miller_sets),
-    stored lines + multi-pair accumulation (k_lines / k_miller_acc, which the
-    library otherwise picks only for calls of >= 8192 sets) and stored lines +
-    one wave per pair (k_lines / k_pair_wc, picked for calls of <= 1024 sets)."""
+    """A context per verification organisation.  Throughput pipeline (latency
+    path off): one pair per lane (k_miller_sets), stored lines + multi-pair
+    accumulation (k_lines / k_miller_acc, which the library otherwise picks only
+    for calls of >= 8192 sets) and stored lines + one wave per pair (k_lines /
+    k_pair_wc).  "lp": every call on the latency path (k_lp_verify, one
+    workgroup per set running the round programs), whatever its size."""
     import os
     from lodestar_amd.native import Device
     old = os.environ.get("LB_MILLER")
-    os.environ["LB_MILLER"] = request.param
+    os.environ["LB_MILLER"] = "auto" if request.param == "lp" else request.param
     try:
         dev = Device(0)
+        dev.set_latency_path(1 << 20 if request.param == "lp" else 0)
     finally:
         if old is None:
             os.environ.pop("LB_MILLER", None)

@@ -214,3 +214,39 @@ def test_packed_requests_slice_rebases_offsets():
         assert q.req_off[0] == 0 and q.pk_off[0] == 0 and q.sig_off[0] == 0
         assert int(q.sig_off[-1]) == len(q.sig_blob) and int(q.pk_off[-1]) == len(q.idx)
         assert int(q.req_off[-1]) * 32 == len(q.msgs) == 32 * (len(q.sig_off) - 1)
+
+
+def test_packed_requests_slice_mixed_rows():
+    """A mixed package (validator indices + byte keys named by LB_PK_ROW_FLAG
+    indices): each slice keeps exactly the rows it names, renumbered from 0, so
+    every key resolves to the same bytes / index as in the whole package."""
+    import numpy as np
+    from lodestar_amd.native import LB_PK_ROW_FLAG
+    from lodestar_amd.sharding import PackedRequests, shard_requests
+    rng = np.random.default_rng(2)
+    sizes = rng.integers(1, 5, 30)
+    req_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    n = int(req_off[-1])
+    pk_off = np.arange(n + 1, dtype=np.uint32)
+    is_row = rng.random(n) < 0.3
+    rows = rng.integers(0, 256, (int(is_row.sum()), 96)).astype(np.uint8)
+    idx = np.where(is_row, 0, rng.integers(0, 1000, n)).astype(np.uint32)
+    idx[is_row] = LB_PK_ROW_FLAG | np.arange(int(is_row.sum()), dtype=np.uint32)
+    sig_off = np.arange(n + 1, dtype=np.uint32) * 96
+    p = PackedRequests(req_off, pk_off, np.zeros(32 * n, np.uint8), np.zeros(96 * n, np.uint8), sig_off,
+                       idx=idx, pks=rows.reshape(-1))
+
+    def resolve(q):
+        out = []
+        for v in q.idx:
+            v = int(v)
+            out.append(bytes(q.pks.reshape(-1, 96)[v ^ LB_PK_ROW_FLAG]) if v & LB_PK_ROW_FLAG else v)
+        return out
+    whole = resolve(p)
+    got = []
+    for lo, hi in shard_requests(sizes.tolist(), 4):
+        q = p.slice(lo, hi)
+        n_rows = int(((q.idx & LB_PK_ROW_FLAG) != 0).sum())
+        assert n_rows == 0 or len(q.pks) == 96 * n_rows
+        got += resolve(q)
+    assert got == whole
