@@ -194,6 +194,15 @@ int lb_verify_requests_device_async(lb_ctx* ctx, const lb_request_batch* batch, 
                                     uint8_t* d_out_request_error, uint8_t* d_out_set_status, uint64_t* out_ticket);
 int lb_verify_requests_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* out_request_valid,
                              uint8_t* out_request_error, uint8_t* out_set_status, uint64_t* out_ticket);
+/* The priority lane: like lb_verify_requests_async, but on a slot of its own whose
+ * stream runs at the device's highest priority, outside the round robin of the
+ * calls in flight -- for priority jobs and verifyOnMainThread callers (the
+ * reference puts them at the queue front / on the main thread, index.ts:174-187,
+ * 327-357, 544-555).  Calls of at most lb_set_latency_path's size take the latency
+ * path.  One priority call in flight: a second first waits for the first.  The
+ * synchronous lb_verify_requests uses this lane for calls of that size too. */
+int lb_verify_requests_priority_async(lb_ctx* ctx, const lb_request_batch* batch, uint8_t* out_request_valid,
+                                      uint8_t* out_request_error, uint8_t* out_set_status, uint64_t* out_ticket);
 int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats);
 /* Non-blocking completion test of an async call: *out_done = 1 when lb_wait(ticket)
  * would return without waiting (the call's device work is complete, or it has

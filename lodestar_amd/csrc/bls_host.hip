@@ -164,8 +164,13 @@ struct lb_ctx {
   // whose 3.3 KB/lane private segment is reserved per queue; profiles/ab_r03/r03g_q24_fail.txt)
   static constexpr int kMaxSlots = 16;
   int n_slots = 4;
-  int streams_per_slot[kMaxSlots] = {2};  // (set for every slot in lb_create)
-  Slot slots[kMaxSlots];
+  int streams_per_slot[kMaxSlots + 1] = {2};  // (set for every slot in lb_create)
+  // slots[n_slots] is the priority lane: one stream at the device's highest
+  // priority, outside the async round robin, for latency-critical calls
+  // (lb_verify_requests_priority_async, and lb_verify_requests of at most
+  // lp_max_sets sets): they never queue behind the calls in flight
+  Slot slots[kMaxSlots + 1];
+  Slot& prio() { return slots[n_slots]; }
   int next_slot = 0;
   uint64_t next_ticket = 1;
   // the last tickets issued to two-phase calls: lb_verify_requests_finish accepts a
@@ -891,7 +896,7 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
 // the signature / MSM branch), so it borrows an idle slot's stream; the next call
 // that wants that slot waits for this one first (finish_slot).
 void borrow_idle_stream(lb_ctx* ctx, Slot& sl) {
-  if (!ctx->dag || sl.st[1] != sl.st[0] || sl.borrowed) return;
+  if (!ctx->dag || sl.st[1] != sl.st[0] || sl.borrowed || &sl == &ctx->prio()) return;
   Slot* idle = nullptr;
   for (int s = 0; s < ctx->n_slots; s++) {
     Slot& o = ctx->slots[s];
@@ -928,7 +933,7 @@ int end_call_async(lb_ctx* ctx, Slot& sl) {
 }
 
 Slot* slot_of_ticket(lb_ctx* ctx, uint64_t ticket) {
-  for (int s = 0; s < ctx->n_slots; s++)
+  for (int s = 0; s <= ctx->n_slots; s++)
     if (ctx->slots[s].busy && ctx->slots[s].ticket == ticket) return &ctx->slots[s];
   return nullptr;
 }
@@ -956,7 +961,7 @@ int borrow_second_stream(lb_ctx* ctx, BorrowGuard& g) {
 
 // Idle slot 0 for the synchronous helper entry points.
 int helper_slot(lb_ctx* ctx) {
-  for (int i = 0; i < ctx->n_slots; i++) LB_TRY(finish_slot(ctx, ctx->slots[i]));
+  for (int i = 0; i <= ctx->n_slots; i++) LB_TRY(finish_slot(ctx, ctx->slots[i]));
   return LB_OK;
 }
 
@@ -1066,12 +1071,16 @@ int lb_create(int device, lb_ctx** out_ctx) {
   }
   for (int s = 0; s < lb_ctx::kMaxSlots; s++)
     ctx->streams_per_slot[s] = ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;
+  ctx->streams_per_slot[ctx->n_slots] = 1;  // the priority lane
   // LB_SLOT0_STREAMS=1|2 overrides slot 0's two-stream DAG (the synchronous, lowest-latency slot)
   if (const char* e = getenv("LB_SLOT0_STREAMS")) ctx->streams_per_slot[0] = atoi(e) == 1 ? 1 : 2;
-  for (int s = 0; ok && s < ctx->n_slots; s++) {
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  for (int s = 0; ok && s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++)
-      ok = hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking) == hipSuccess;
+      ok = (s == ctx->n_slots ? hipStreamCreateWithPriority(&sl.st[i], hipStreamNonBlocking, prio_greatest)
+                              : hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking)) == hipSuccess;
     if (ctx->streams_per_slot[s] == 1) sl.st[1] = sl.st[0];
     for (int i = 0; ok && i < 8; i++) ok = hipEventCreateWithFlags(&sl.dep[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < Slot::kMaxStages; i++)
@@ -1086,8 +1095,6 @@ int lb_create(int device, lb_ctx** out_ctx) {
   ctx->stream = ctx->slots[0].st[0];
   // the host combine's one-wave final exponentiation must not queue behind the
   // calls in flight (their 1-wave/SIMD kernels fill every SIMD): highest priority
-  int prio_least = 0, prio_greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
   ok = ok && hipStreamCreateWithPriority(&ctx->aux_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
   {
     // off by default: one shared high-priority stream for every slot's merged check
@@ -1107,7 +1114,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
 int lb_destroy(lb_ctx* ctx) {
   if (!ctx) return LB_OK;
   (void)hipSetDevice(ctx->device);
-  for (int s = 0; s < ctx->n_slots; s++) {
+  for (int s = 0; s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     for (int i = 0; i < ctx->streams_per_slot[s]; i++)
       if (sl.st[i]) (void)hipStreamSynchronize(sl.st[i]);
@@ -1513,6 +1520,10 @@ int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d
   if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   uint64_t t = 0;
+  if (b->n_sets <= ctx->lp_max_sets) {  // latency path: the priority lane, beside any calls in flight
+    LB_TRY(submit_device(ctx, ctx->prio(), b, d_valid, d_req_err, d_set_status, false, &t));
+    return lb_wait(ctx, t, stats);
+  }
   BorrowGuard g{ctx};
   LB_TRY(borrow_second_stream(ctx, g));
   LB_TRY(submit_device(ctx, ctx->slots[0], b, d_valid, d_req_err, d_set_status, false, &t));  // slot 0: DAG
@@ -1530,10 +1541,24 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
     return LB_OK;
   }
   uint64_t t = 0;
+  if (b->n_sets <= ctx->lp_max_sets) {  // latency path: the priority lane, beside any calls in flight
+    LB_TRY(submit_host(ctx, ctx->prio(), b, out_valid, out_req_err, out_set_status, false, &t));
+    return lb_wait(ctx, t, stats);
+  }
   BorrowGuard g{ctx};  // synchronous host API: slot 0 (two-stream DAG, lowest latency)
   LB_TRY(borrow_second_stream(ctx, g));
   LB_TRY(submit_host(ctx, ctx->slots[0], b, out_valid, out_req_err, out_set_status, false, &t));
   return lb_wait(ctx, t, stats);
+}
+
+int lb_verify_requests_priority_async(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_valid,
+                                      uint8_t* out_req_err, uint8_t* out_set_status, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return LB_ERR_INVALID_ARGUMENT;
+  LB_TRY(validate_batch(ctx, b));
+  if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  LB_TRY(sm_pump(ctx));
+  return submit_host(ctx, ctx->prio(), b, out_valid, out_req_err, out_set_status, false, out_ticket);
 }
 // ---- helpers for small host-buffer calls ----------------------------------
 static int upload(lb_ctx* ctx, Bump& ws, const void* src, size_t n, void** out) {
@@ -2107,7 +2132,7 @@ int sm_advance_launch(lb_ctx* ctx, Slot& sl, bool block) {
 // Launch the phase 2 of every same-message call whose phase 1 has completed
 // (called from every async entry point and lb_wait: no blocking).
 int sm_pump(lb_ctx* ctx) {
-  for (int s = 0; s < ctx->n_slots; s++) {
+  for (int s = 0; s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     // (another call's failure is not this caller's: it stays on that slot's ticket)
     if (sl.busy && sl.sm.active && sl.sm.phase == 1) (void)sm_advance(ctx, sl, false);

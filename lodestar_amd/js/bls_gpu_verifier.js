@@ -36,6 +36,9 @@ const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:57
 const MAX_BUFFERED_SIGS = 32; // index.ts:66
 const MAX_BUFFER_WAIT_MS = 100; // index.ts:75
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // index.ts:80
+// one priority-lane package: at most this many sets (the library's latency path,
+// lb_set_latency_path's default 1024, runs calls up to that size)
+const MAX_PRIORITY_LANE_SETS = 1024;
 const BATCHABLE_MIN_PER_CHUNK = 16; // worker.ts:17
 const LB_PK_ROW_FLAG = 0x80000000;
 const LB_REQ_EMPTY_AGGREGATE = 1;
@@ -305,6 +308,9 @@ class BlsGpuVerifier {
    * @param {number} [o.prefetch] packages per GPU queued beyond its calls in flight (default 0;
    *   4 measured 2.32 vs 2.48 M sets/s in the node leg: the queue only grew)
    * @param {() => Uint8Array} [o.seedSource] 32-byte batch-randomness seed per call
+   * @param {boolean} [o.priorityLane] priority jobs and verifyOnMainThread calls go to the
+   *   device's priority lane (lb_verify_requests_priority_async: its own high-priority
+   *   stream beside the calls in flight) instead of waiting for a free slot (default true)
    */
   constructor(o = {}) {
     if (o.backends) this.backends = o.backends;
@@ -318,6 +324,8 @@ class BlsGpuVerifier {
     this.maxSetsPerDispatch = o.maxSetsPerDispatch || 65536;
     this.seedSource = o.seedSource || (() => new Uint8Array(crypto.randomBytes(32)));
     this.metrics = new PoolMetrics();
+    this.priorityLane = o.priorityLane === undefined ? true : Boolean(o.priorityLane);
+    this.prioBusy = this.backends.map(() => false);  // one priority package in flight per GPU
     this.jobs = [];
     this.buffered = null;
     this.idle = [];
@@ -359,7 +367,8 @@ class BlsGpuVerifier {
       // not block the event loop, unlike blst on the reference's main thread)
       const t0 = process.hrtime();
       try {
-        const r = await this.backends[0].verifyRequests(packRequests([sets], this.seedSource()));
+        const batch = packRequests([sets], this.seedSource());
+        const r = await this.backends[0].verifyRequests(batch, this.priorityLane ? {priority: true} : undefined);
         return this.requestVerdict(r, 0);
       } finally {
         const [s, ns] = process.hrtime(t0);
@@ -431,15 +440,22 @@ class BlsGpuVerifier {
     this.scheduleRun();
   };
 
-  prepareWork() {
+  /** @param {number} skip leading jobs left in the queue (priority jobs waiting for the lane) */
+  prepareWork(skip = 0) {
     const jobs = [];
     let total = 0;
-    while (total < this.maxSetsPerDispatch && this.jobs.length > 0) {
-      const job = this.jobs.shift();
+    while (total < this.maxSetsPerDispatch && this.jobs.length > skip) {
+      const job = this.jobs.splice(skip, 1)[0];
       jobs.push(job);
       total += job.type === "default" ? job.sets.length : 1;
     }
     return jobs;
+  }
+
+  leadingPriorityJobs() {
+    let n = 0;
+    while (n < this.jobs.length && this.jobs[n].opts.priority && this.jobs[n].type === "default") n++;
+    return n;
   }
 
   /** setTimeout(runJob, 0) as the reference does after every queue change (index.ts:386,
@@ -455,9 +471,50 @@ class BlsGpuVerifier {
     this.runJob();
   };
 
+  /** Leading priority verify jobs (up to MAX_PRIORITY_LANE_SETS sets) as one package on
+   * a GPU whose priority lane is free: they start now, beside the packages in flight,
+   * instead of waiting for a slot (the reference's queue-front insertion,
+   * index.ts:327-357,544-555, plus head-of-line isolation on the device). */
+  runPriority() {
+    const g = this.prioBusy.indexOf(false);
+    if (g < 0) return false;
+    const jobs = [];
+    let total = 0;
+    while (this.jobs.length > 0) {
+      const j = this.jobs[0];
+      if (!j.opts.priority || j.type !== "default") break;
+      if (jobs.length && total + j.sets.length > MAX_PRIORITY_LANE_SETS) break;
+      jobs.push(this.jobs.shift());
+      total += j.sets.length;
+    }
+    if (jobs.length === 0) return false;
+    this.prioBusy[g] = true;
+    this.metrics.inc(M.JOB_GROUPS_STARTED);
+    this.metrics.inc(M.JOBS_STARTED, jobs.length, {type: "default"});
+    this.metrics.inc(M.SIG_SETS_STARTED, total, {type: "default"});
+    const now = Date.now();
+    for (const j of jobs) this.metrics.observe(M.JOB_WAIT_TIME, (now - j.added) / 1000);
+    const p = this.dispatch(g, jobs, true).finally(() => {
+      this.prioBusy[g] = false;
+      this.running.delete(p);
+      if (this.jobs.length > 0) this.scheduleRun();
+    });
+    this.running.add(p);
+    return true;
+  }
+
   runJob = () => {
-    if (this.closed || this.idle.length === 0 || this.jobs.length === 0) return;
-    const jobs = this.prepareWork();
+    if (this.closed || this.jobs.length === 0) return;
+    let skip = 0;
+    if (this.priorityLane && this.leadingPriorityJobs() > 0) {
+      if (this.runPriority()) {
+        if (this.jobs.length > 0) this.scheduleRun();
+        return;
+      }
+      skip = this.leadingPriorityJobs();  // the lanes are busy: they wait for one, the rest go on
+    }
+    if (this.idle.length === 0 || this.jobs.length <= skip) return;
+    const jobs = this.prepareWork(skip);
     if (jobs.length === 0) return;
     const bi = this.idle.shift();
     const m = this.metrics;
@@ -481,7 +538,7 @@ class BlsGpuVerifier {
     return r.valid[k] === 1;
   }
 
-  async dispatch(bi, jobs) {
+  async dispatch(bi, jobs, priority = false) {
     const backend = this.backends[bi];
     const m = this.metrics;
     const dispatchNs = hrNowNs();
@@ -499,7 +556,7 @@ class BlsGpuVerifier {
         if (def.some((j) => j.sets.some((x) => x.type === "aggregate")))
           m.observe(M.PUBKEYS_AGGREGATION_MAIN_THREAD, s0 + ns0 / 1e9);
         const packedNs = hrNowNs();
-        waits.push(backend.verifyRequests(batch));
+        waits.push(priority ? backend.verifyRequests(batch, {priority: true}) : backend.verifyRequests(batch));
         if (this.trace) this.trace.push({dispatchNs, packedNs, submittedNs: hrNowNs(), inFlight: this.running.size});
       }
       if (same.length) {
@@ -514,7 +571,7 @@ class BlsGpuVerifier {
       outs = await Promise.all(waits);
     } catch (e) {
       // device failure rejects every job of the package (index.ts:503-512)
-      this.idle.push(bi);
+      if (!priority) this.idle.push(bi);
       m.set(M.WORKERS_BUSY, Math.min(this.capacity, this.tokens - this.idle.length));
       for (const job of jobs) job.reject(e);
       this.scheduleRun();
@@ -533,7 +590,7 @@ class BlsGpuVerifier {
           break;
         }
     }
-    this.idle.push(bi);
+    if (!priority) this.idle.push(bi);
     m.set(M.WORKERS_BUSY, Math.min(this.capacity, this.tokens - this.idle.length));
     let k = 0;
     let success = 0;
@@ -683,7 +740,21 @@ function slicePacked(p, lo, hi, seed) {
     sigOffsets: rebase(p.sigOffsets, a, b + 1, sa),
     seed,
   };
-  if (p.pubkeyIndices) out.pubkeyIndices = p.pubkeyIndices.subarray(ka, kb);
+  if (p.pubkeyIndices && p.pubkeys) {
+    // mixed package: keep the rows this slice names (LB_PK_ROW_FLAG), renumbered from 0
+    const idx = Uint32Array.from(p.pubkeyIndices.subarray(ka, kb));
+    const rows = [];
+    for (let q = 0; q < idx.length; q++)
+      if (idx[q] & LB_PK_ROW_FLAG) {
+        rows.push(idx[q] & ~LB_PK_ROW_FLAG);
+        idx[q] = (LB_PK_ROW_FLAG | (rows.length - 1)) >>> 0;
+      }
+    out.pubkeyIndices = idx;
+    if (rows.length) {
+      out.pubkeys = new Uint8Array(96 * rows.length);
+      rows.forEach((r, q) => out.pubkeys.set(p.pubkeys.subarray(96 * r, 96 * r + 96), 96 * q));
+    }
+  } else if (p.pubkeyIndices) out.pubkeyIndices = p.pubkeyIndices.subarray(ka, kb);
   else out.pubkeys = p.pubkeys.subarray(96 * ka, 96 * kb);
   return out;
 }
@@ -752,4 +823,5 @@ module.exports = {
   MAX_BUFFERED_SIGS,
   MAX_BUFFER_WAIT_MS,
   MAX_JOBS_CAN_ACCEPT_WORK,
+  MAX_PRIORITY_LANE_SETS,
 };

@@ -18,8 +18,10 @@
 //   deviceCount() -> number
 //   validateRequests(batch) -> {nRequests, nSets, nPubkeys, byIndex}   (marshalling dry run, no device)
 //   new Context(device, {capacity?}) (throws Error{code: "LB_ERR_NO_DEVICE", ...} without a GPU)
-//     .verifyRequests(batch) -> Promise<{valid, errors, setStatus, batchRetries, batchSigsSuccess,
-//                                        deviceMs, workerStartNs, workerEndNs}>
+//     .verifyRequests(batch, {priority?}) -> Promise<{valid, errors, setStatus, batchRetries,
+//                                        batchSigsSuccess, deviceMs, workerStartNs, workerEndNs}>
+//         (priority: the device's priority lane -- started at once, beside the calls in
+//          flight, retired as soon as it completes; lb_verify_requests_priority_async)
 //     .verifyRequestsPartial(batch) -> Promise<{id, partial: Uint8Array(576)}>  (two-phase, multi-GPU)
 //     .finish(id, mergedOk) -> Promise<result of verifyRequests>
 //     .gtCheck(Uint8Array n*576) -> Promise<boolean>
@@ -125,6 +127,7 @@ struct Task {
   std::vector<uint32_t> req_off, pk_off, sig_off, pk_idx, job_off;
   std::vector<uint8_t> pubkeys, messages, signatures, seed, batchable;
   bool has_pk_off = false, by_index = false, has_batchable = false, mixed = false;
+  bool prio = false;  // verifyRequests(batch, {priority: true}): the device's priority lane
   uint32_t n_req = 0, n_sets = 0, n_jobs = 0, pk_len = 0, n_keys = 0;
   int merged_ok = 0;
   uint64_t partial_id = 0;
@@ -236,32 +239,60 @@ void fail(Task* t, int rc, lb_ctx* ctx) {
   t->errmsg = ctx ? lb_last_error(ctx) : "no context";
 }
 
+// A queued task the worker can start now: a priority call always (its lane is
+// separate from the calls in flight), close always, anything else when a slot is free.
+bool startable(Context* c, size_t n_inflight) {
+  if (c->queue.empty()) return false;
+  const Task* f = c->queue.front();
+  return f->prio || f->kind == Kind::Close || (int)n_inflight < c->capacity;
+}
+
 // Worker thread: owns c->ctx.
 void worker_loop(Context* c) {
   std::deque<Task*> inflight;  // submitted, waiting for lb_wait
+  std::deque<Task*> prio;      // priority-lane calls in flight (retired as soon as done)
   for (;;) {
     Task* t = nullptr;
     {
       std::unique_lock<std::mutex> lk(c->mu);
-      c->cv.wait(lk, [&] { return !c->queue.empty() || !inflight.empty() || c->finalizing; });
-      if (!c->queue.empty() && ((int)inflight.size() < c->capacity || c->queue.front()->kind == Kind::Close)) {
+      c->cv.wait(lk, [&] { return !c->queue.empty() || !inflight.empty() || !prio.empty() || c->finalizing; });
+      if (startable(c, inflight.size())) {
         t = c->queue.front();
         c->queue.pop_front();
-      } else if (inflight.empty() && c->finalizing) {
+      } else if (inflight.empty() && prio.empty() && c->finalizing) {
         break;
+      }
+    }
+    if (!t && !prio.empty()) {  // a finished priority call retires ahead of everything
+      Task* w = prio.front();
+      int32_t done = 1;
+      if (c->finalizing || (lb_poll(c->ctx, w->ticket, &done) == LB_OK && done)) {
+        prio.pop_front();
+        w->t_retire = now_ns();
+        const int rc = lb_wait(c->ctx, w->ticket, &w->stats);
+        if (rc != LB_OK) fail(w, rc, c->ctx);
+        w->t_end = now_ns();
+        complete(c, w);
+        continue;
+      }
+      if (inflight.empty()) {
+        std::unique_lock<std::mutex> lk(c->mu);
+        c->cv.wait_for(lk, std::chrono::microseconds(50), [&] { return startable(c, 0) || c->finalizing; });
+        continue;
       }
     }
     if (!t) {  // retire the oldest call in flight
       Task* w = inflight.front();
       Task* owner = w->kind == Kind::Finish ? w->target : w;
-      if ((int)inflight.size() < c->capacity && !c->finalizing) {
-        // room for more calls: do not block on this one while the JS thread may queue
-        // the next package (blocking here held every new package back until the oldest
-        // call finished: ~12 of 16 calls in flight, 2.3 M sets/s through node)
+      if (!c->finalizing) {
+        // never block on it: the JS thread may queue the next package (blocking here held
+        // every new package back until the oldest call finished: ~12 of 16 calls in
+        // flight, 2.3 M sets/s through node), or a priority call that must start now
         int32_t done = 1;
         if (lb_poll(c->ctx, owner->ticket, &done) == LB_OK && !done) {
           std::unique_lock<std::mutex> lk(c->mu);
-          c->cv.wait_for(lk, std::chrono::microseconds(200), [&] { return !c->queue.empty() || c->finalizing; });
+          c->cv.wait_for(lk, std::chrono::microseconds(prio.empty() ? 200 : 50),
+                         [&] { return startable(c, inflight.size()) || c->finalizing; });
           continue;
         }
       }
@@ -289,13 +320,16 @@ void worker_loop(Context* c) {
       case Kind::Verify: {
         alloc_outputs(*t);
         lb_request_batch b = batch_of(*t);
-        const int rc = lb_verify_requests_async(c->ctx, &b, t->valid.data(), t->err.data(), t->sst.data(), &t->ticket);
+        const int rc = t->prio ? lb_verify_requests_priority_async(c->ctx, &b, t->valid.data(), t->err.data(),
+                                                                   t->sst.data(), &t->ticket)
+                               : lb_verify_requests_async(c->ctx, &b, t->valid.data(), t->err.data(),
+                                                          t->sst.data(), &t->ticket);
         t->t_submitted = now_ns();
         if (rc != LB_OK) {
           fail(t, rc, c->ctx);
           complete(c, t);
         } else {
-          inflight.push_back(t);
+          (t->prio ? prio : inflight).push_back(t);
         }
         break;
       }
@@ -393,6 +427,12 @@ void worker_loop(Context* c) {
         break;
       }
       case Kind::Close: {
+        for (Task* w : prio) {
+          const int rc = lb_wait(c->ctx, w->ticket, &w->stats);
+          if (rc != LB_OK) fail(w, rc, c->ctx);
+          complete(c, w);
+        }
+        prio.clear();
         while (!inflight.empty()) {  // never destroy the context under a call in flight
           Task* w = inflight.front();
           inflight.pop_front();
@@ -421,6 +461,10 @@ void worker_loop(Context* c) {
     }
   }
   // finalizer path (Context garbage-collected without close())
+  for (Task* w : prio) {
+    lb_wait(c->ctx, w->ticket, nullptr);
+    delete w;
+  }
   for (Task* w : inflight) {
     Task* owner = w->kind == Kind::Finish ? w->target : w;
     lb_wait(c->ctx, owner->ticket, nullptr);
@@ -554,7 +598,13 @@ napi_value submit(napi_env env, Context* c, Task* t) {
       return promise;
     }
     if (t->kind == Kind::Close) c->closing = true;
-    c->queue.push_back(t);
+    if (t->prio) {  // ahead of every queued non-priority task, behind earlier priority ones
+      auto it = c->queue.begin();
+      while (it != c->queue.end() && (*it)->prio) ++it;
+      c->queue.insert(it, t);
+    } else {
+      c->queue.push_back(t);
+    }
   }
   if (c->pending++ == 0) napi_ref_threadsafe_function(env, c->tsfn);
   c->cv.notify_one();
@@ -572,15 +622,23 @@ napi_value rejected(napi_env env, const std::string& msg) {
 }
 
 napi_value m_verify(napi_env env, napi_callback_info info, Kind kind) {
-  size_t argc = 1;
-  napi_value argv[1];
+  size_t argc = 2;
+  napi_value argv[2];
   Context* c = unwrap(env, info, &argc, argv);
   if (!c) return rejected(env, "not a Context");
   Task* t = new Task();
   t->kind = kind;
   try {
-    if (argc < 1) throw ArgError{"verifyRequests(batch)"};
+    if (argc < 1) throw ArgError{"verifyRequests(batch[, {priority}])"};
     parse_requests(env, argv[0], *t);
+    napi_value pv;
+    napi_valuetype ty = napi_undefined;
+    if (argc >= 2) napi_typeof(env, argv[1], &ty);
+    if (kind == Kind::Verify && ty == napi_object && has_prop(env, argv[1], "priority", &pv)) {
+      bool b = false;
+      napi_get_value_bool(env, pv, &b);
+      t->prio = b;
+    }
   } catch (const ArgError& e) {
     delete t;
     return rejected(env, e.msg);

@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
     "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
+    "lb_verify_requests_priority_async",
 )
 
 LB_BATCH_DEVICE = 1
@@ -149,6 +150,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_poll.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_verify_requests_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                              ctypes.POINTER(ctypes.c_uint64)]
+    lib.lb_verify_requests_priority_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
+                                                      ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_verify_requests_partial_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), u32, vp, vp, vp,
                                                      ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_partial_wait.argtypes = [vp, ctypes.c_uint64, vp]
@@ -323,9 +326,13 @@ class Device:
                             int(st.batch_sigs_success))
 
     def verify_requests_async(self, request_offsets, pubkeys, pk_offsets, messages, sig_blob, sig_offsets, seed,
-                              batchable=None, pk_indices=None, partial: bool = False) -> "PendingCall":
-        """lb_verify_requests_async (or the two-phase lb_verify_requests_partial_async):
-        enqueue on the next slot and return at once; wait_call() gives the verdicts."""
+                              batchable=None, pk_indices=None, partial: bool = False,
+                              priority: bool = False) -> "PendingCall":
+        """lb_verify_requests_async (or the two-phase lb_verify_requests_partial_async,
+        or with priority=True the priority lane, lb_verify_requests_priority_async):
+        enqueue and return at once; wait_call() gives the verdicts."""
+        if partial and priority:
+            raise ValueError("a two-phase call cannot take the priority lane")
         b, keep, n_req, n_sets = self._host_batch(request_offsets, pubkeys, pk_offsets, messages, sig_blob,
                                                   sig_offsets, seed, batchable, pk_indices)
         pc = PendingCall(0, n_req, n_sets, np.zeros(max(n_req, 1), np.uint8), np.zeros(max(n_req, 1), np.uint8),
@@ -336,9 +343,9 @@ class Device:
                                                            _ptr(pc.sst), ctypes.byref(t))
             self._check(rc, "lb_verify_requests_partial_async")
         else:
-            rc = self.lib.lb_verify_requests_async(self._h, ctypes.byref(b), _ptr(pc.valid), _ptr(pc.err),
-                                                   _ptr(pc.sst), ctypes.byref(t))
-            self._check(rc, "lb_verify_requests_async")
+            fn = self.lib.lb_verify_requests_priority_async if priority else self.lib.lb_verify_requests_async
+            rc = fn(self._h, ctypes.byref(b), _ptr(pc.valid), _ptr(pc.err), _ptr(pc.sst), ctypes.byref(t))
+            self._check(rc, "lb_verify_requests_priority_async" if priority else "lb_verify_requests_async")
         pc.ticket = int(t.value)
         return pc
 

@@ -38,11 +38,13 @@ class MockBackend {
     }
     return {valid, errors, sizes};
   }
-  async verifyRequests(b) {
+  async verifyRequests(b, opts) {
     assert(!this.closed);
     const {valid, errors, sizes} = this.verdicts(b);
     this.dispatches.push(sizes);
-    await new Promise((r) => setTimeout(r, 1));
+    const prio = Boolean(opts && opts.priority);
+    (this.log || (this.log = [])).push({sizes, prio, t: Date.now()});
+    await new Promise((r) => setTimeout(r, prio ? 1 : this.delayMs || 1));
     return {valid, errors, setStatus: new Uint8Array(0), batchRetries: 0, batchSigsSuccess: 0, deviceMs: 0};
   }
   async verifySameMessage(b) {
@@ -155,6 +157,57 @@ test("priority jobs run first", async () => {
   await Promise.all([f1, f2]);
   assert.deepStrictEqual(b.dispatches[0], [5]);
   await v.close();
+});
+
+test("priority job takes the priority lane ahead of queued packages", async () => {
+  // one slot, busy with a slow package, two more packages queued: the priority job
+  // starts at once on the lane (verifyRequests(batch, {priority: true})) and resolves
+  // before the queued packages; verifyOnMainThread takes the lane too
+  const b = new MockBackend(1);
+  b.delayMs = 40;
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed, maxSetsPerDispatch: 1});
+  const done = [];
+  const normal = [0, 1, 2].map((i) => v.verifySignatureSets(sets(3 + i)).then(() => done.push("n" + i)));
+  await new Promise((r) => setTimeout(r, 5));
+  const t0 = Date.now();
+  const p = v.verifySignatureSets(sets(7), {priority: true}).then((ok) => done.push("p") && ok);
+  const m = v.verifySignatureSets(sets(1), {verifyOnMainThread: true}).then((ok) => done.push("m") && ok);
+  assert.strictEqual(await p, true);
+  assert.strictEqual(await m, true);
+  assert(Date.now() - t0 < 30, "priority work waited for a slot");
+  await Promise.all(normal);
+  assert(done.indexOf("p") < done.indexOf("n1") && done.indexOf("m") < done.indexOf("n1"), done.join());
+  const prio = b.log.filter((x) => x.prio).map((x) => x.sizes[0]);
+  assert.deepStrictEqual(prio.sort(), [1, 7]);
+  // without the lane: the reference's queue-front order through the slots
+  const b2 = new MockBackend(1);
+  const v2 = new V.BlsGpuVerifier({backends: [b2], seedSource: seed, priorityLane: false});
+  await v2.verifySignatureSets(sets(2), {priority: true});
+  assert(b2.log.every((x) => !x.prio));
+  await v.close();
+  await v2.close();
+});
+
+test("slicePacked keeps a mixed package's rows, renumbered", () => {
+  const F = 0x80000000;
+  const rows = new Uint8Array(96 * 3);
+  for (let r = 0; r < 3; r++) rows.fill(10 + r, 96 * r, 96 * r + 96);
+  const p = {
+    requestOffsets: Uint32Array.from([0, 2, 4]),
+    pkOffsets: Uint32Array.from([0, 1, 2, 3, 4]),
+    pubkeyIndices: Uint32Array.from([5, (F | 0) >>> 0, (F | 2) >>> 0, 9]),
+    pubkeys: rows,
+    messages: new Uint8Array(128),
+    signatures: new Uint8Array(384),
+    sigOffsets: Uint32Array.from([0, 96, 192, 288, 384]),
+  };
+  const q = V.slicePacked(p, 1, 2, new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(q.pubkeyIndices), [(F | 0) >>> 0, 9]);
+  assert.strictEqual(q.pubkeys.length, 96);
+  assert.strictEqual(q.pubkeys[0], 12);
+  const q0 = V.slicePacked(p, 0, 1, new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(q0.pubkeyIndices), [5, (F | 0) >>> 0]);
+  assert.strictEqual(q0.pubkeys[0], 10);
 });
 
 test("empty aggregate rejects the job; empty sets are false", async () => {

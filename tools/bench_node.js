@@ -121,6 +121,32 @@ function median(xs) {
     };
     v.trace = null;
   }
+  // latency under load: `loadRounds` more rounds of packages queued at once (every slot
+  // busy with a 65,536-set call, more waiting in the JS queue); meanwhile one 1-set
+  // verifyOnMainThread call and one 128-set priority job at a time take the device's
+  // priority lane (BlsGpuVerifier priorityLane -> addon {priority} -> the library's
+  // priority slot on a highest-priority stream)
+  const loadRounds = Math.max(8, rounds >> 2);
+  const loadAll = [];
+  for (let r = 0; r < loadRounds; r++) for (const js of jobs) loadAll.push(v.verifySignatureSets(js));
+  let loadDone = false;
+  const loadP = Promise.all(loadAll).then((xs) => {
+    loadDone = true;
+    return xs.every((x) => x === true);
+  });
+  await new Promise((r) => setTimeout(r, 300));  // the pipe full
+  const load1 = [];
+  const load128 = [];
+  for (let r = 0; r < 11 && !loadDone; r++) {
+    let t = ms();
+    ok = ok && (await v.verifySignatureSets([set(r + 7)], {verifyOnMainThread: true})) === true;
+    load1.push(ms() - t);
+    t = ms();
+    ok = ok && (await v.verifySignatureSets(jobs[(r + 3) % jobs.length], {priority: true})) === true;
+    load128.push(ms() - t);
+    await new Promise((res) => setTimeout(res, 10));
+  }
+  ok = ok && (await loadP);
   const lat128 = [];
   const lat1 = [];
   if (process.env.LB_JS_TRACE === "1") v.trace = [];
@@ -151,6 +177,13 @@ function median(xs) {
       // the same after the throughput phase (a process that has just run 96 packages)
       p50_ms_128set_after_throughput: +median(lat128).toFixed(3),
       p50_ms_1set_after_throughput: +median(lat1).toFixed(3),
+      // while every slot is busy with a 65,536-set package (priority lane)
+      under_load: {
+        p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
+        p50_ms_128set_priority: load128.length ? +median(load128).toFixed(3) : null,
+        samples: load1.length,
+        load_packages: loadRounds,
+      },
       ...(trace ? {trace} : {}),
       ...(latTrace ? {latency_trace: latTrace} : {}),
       ...(latTraceAfter ? {latency_trace_after_throughput: latTraceAfter} : {}),
