@@ -163,156 +163,187 @@ LB_DEV void hash_to_field_fp2_2(fp2 u[2], const uint8_t msg[32]) {
   fp_from_64be_words(u[1].c1, ub + 48);
 }
 
-// Square root in Fp2 when a square root s of the norm N(a) = a0^2 + a1^2 is
-// already known: one Fp exponentiation (fp2_sqrt's second half).  a must be a
-// square; which of the two roots comes out does not matter (callers fix the sign).
-LB_DEV void fp2_sqrt_with_norm_root(fp2& r, const fp2& a, const fp& s) {
-  if (fp_is_zero(a.c1)) {  // a in Fp (probability ~2^-381 on hashed input)
-    fp2 t;
-    fp2_sqrt(t, a);
-    r = t;
+// sqrt(W / m) in Fp2 (W / m a square; m in Fp), given s with s^2 = N(W), with no
+// inversion: with t = (W0 + s) / 2 and c = (t m)^((p-3)/4), z = t c satisfies
+// z^2 = (t / m) chi(t m) and 1 / z = c m (chi = 1), so
+//   chi(t m) = 1  -> y = (z, W1 c / 2)
+//   chi(t m) = -1 -> y = (-W1 c / 2, z)     ((W0 - s) / 2 is the square then)
+// W1 = 0 (W / m in Fp, probability ~2^-381 on hashed input): sqrt(u / v) =
+// u (u v)^((p-3)/4), or i sqrt(-u / v).  Which root comes out does not matter
+// (the caller fixes the sign).  Step for step in tests/test_sswu_fraction.py.
+LB_DEV void fp2_sqrt_ratio_frac(fp2& y, const fp2& W, const fp& m, const fp& s) {
+  fp half, t, c, z, chk, a1c, na1c;
+  fp_set(half, LB_HALF);
+  if (fp_is_zero(W.c1)) {
+    fp u = W.c0;
+    fp_mul(t, u, m);
+    fp_pow_p34(c, t);
+    fp_mul(z, u, c);
+    fp_sqr(chk, z);
+    fp_mul(chk, chk, m);
+    if (fp_eq(chk, u)) {
+      y.c0 = z;
+      fp_zero(y.c1);
+    } else {
+      fp_neg(u, u);
+      fp_mul(t, u, m);
+      fp_pow_p34(c, t);
+      fp_zero(y.c0);
+      fp_mul(y.c1, u, c);
+    }
     return;
   }
-  fp half, t, c, x0, chk, a1c;
-  fp_set(half, LB_HALF);
-  fp_add(t, a.c0, s);
+  fp_add(t, W.c0, s);
   fp_mul(t, t, half);
-  fp_pow_p34(c, t);
-  fp_mul(x0, t, c);  // t^((p+1)/4)
-  fp_sqr(chk, x0);
-  fp_mul(a1c, a.c1, c);
+  fp_mul(c, t, m);
+  fp_pow_p34(c, c);
+  fp_mul(z, t, c);
+  fp_sqr(chk, z);
+  fp_mul(chk, chk, m);
+  fp_mul(a1c, W.c1, c);
   fp_mul(a1c, a1c, half);
   const bool direct = fp_eq(chk, t);
-  fp na1c;
   fp_neg(na1c, a1c);
-  r.c0 = x0;
-  r.c1 = a1c;
-  fp_cmov(r.c0, na1c, !direct);
-  fp_cmov(r.c1, x0, !direct);
+  y.c0 = z;
+  y.c1 = a1c;
+  fp_cmov(y.c0, na1c, !direct);
+  fp_cmov(y.c1, z, !direct);
 }
 
-// Simplified SWU onto E2': y^2 = x^3 + A'x + B'  (RFC 9380 §6.6.2), branch-free.
-// With x2 = Z u^2 x1, g(x2) = Z^3 u^6 g(x1), so N(g(x2)) = N(Z)^3 N(u)^6 N(g(x1))
-// and N(Z)^3 is a non-square: ONE exponentiation t = N(g(x1))^((p-3)/4) gives
-// the square test of g(x1) and a square root of whichever norm is a square
-//   sqrt N(g(x1)) = N(g(x1)) t,   sqrt N(g(x2)) = N(u)^3 N(Z)^(3(p+1)/4) N(g(x1)) t,
-// and a second one (fp2_sqrt_with_norm_root) finishes the Fp2 root.  Every lane
-// of a wave runs the same instructions (the gx1 / gx2 choice is a select).
-LB_DEV void map_to_curve_sswu(g2a& out, const fp2& u) {
-  fp2 A, B, Z, tv1, tv2, x1, x2, gx1, gx2, x, gx, y, t;
+// Simplified SWU onto E2': y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2) followed by the
+// 3-isogeny to E2, with no inversion anywhere (no binary GCD
+// in k_hash_half).  x1 = n / d is kept as a fraction,
+//   n = -B (tv2 + 1), d = A tv2   (tv2 = Z^2 u^4 + Z u^2; tv2 = 0: n = B, d = Z A),
+// g(x1) = U / V with U = n^3 + A n d^2 + B d^3, V = d^3, and U / V = W / m with
+// W = U conj(V), m = N(V) in Fp.  ONE exponentiation e = N(W)^((p-3)/4) gives the
+// square test of g(x1) and sqrt N(W) = N(W) e; for x2 = Z u^2 x1 (g(x2) = Z^3 u^6
+// g(x1), W2 = (Z u^2)^3 W) the norm root is N(u)^3 sqrt(-N(Z)^3) N(W) e, as before.
+// fp2_sqrt_ratio_frac finishes the affine y (its sign fixed against u).  The
+// isogeny is homogenised in (x_n, d): XN = xn(x) d^3, XD = xd(x) d^2, YN = yn(x) d^3,
+// YD = yd(x) d^3, so x_E = XN / (XD d), y_E = y YN / YD and the Jacobian output is
+//   Z = XD d YD,  X = XN XD d YD^2,  Y = y YN (XD d)^3 YD^2.
+LB_DEV void map_to_g2_sswu_iso(g2j& r, const fp2& u) {
+  fp2 A, B, Zc, tv1, tv2, n, d, d2, d3, U, W, t;
   fp2_set(A, LB_SSWU_A);
   fp2_set(B, LB_SSWU_B);
-  fp2_set(Z, LB_SSWU_Z);
+  fp2_set(Zc, LB_SSWU_Z);
   fp2_sqr(tv1, u);
-  fp2_mul(tv1, Z, tv1);  // Z u^2
+  fp2_mul(tv1, Zc, tv1);  // Z u^2
   fp2_sqr(tv2, tv1);
   fp2_add(tv2, tv2, tv1);  // Z^2 u^4 + Z u^2
   const bool exceptional = fp2_is_zero(tv2);
-  fp2_inv(t, tv2);  // inv(0) = 0
-  fp one;
-  fp_one(one);
-  fp_add(t.c0, t.c0, one);
-  fp2_mul_const(x1, t, LB_SSWU_MINUS_B_OVER_A);
-  fp2 bza;
-  fp2_set(bza, LB_SSWU_B_OVER_ZA);
-  fp2_cmov(x1, bza, exceptional);
-  // gx1 = x1^3 + A x1 + B, x2 = Z u^2 x1, gx2 = x2^3 + A x2 + B
-  fp2_sqr(gx1, x1);
-  fp2_add(gx1, gx1, A);
-  fp2_mul(gx1, gx1, x1);
-  fp2_add(gx1, gx1, B);
-  fp2_mul(x2, tv1, x1);
-  fp2_sqr(gx2, x2);
-  fp2_add(gx2, gx2, A);
-  fp2_mul(gx2, gx2, x2);
-  fp2_add(gx2, gx2, B);
-  // norms and the shared exponentiation
-  fp n1, e, chk, s1, s2, nu, nu3, c1;
-  fp_sqr(n1, gx1.c0);
-  fp_sqr(e, gx1.c1);
-  fp_add(n1, n1, e);
-  fp_pow_p34(e, n1);
+  fp2 one;
+  fp2_one(one);
+  fp2_add(t, tv2, one);
+  fp2_mul(n, B, t);
+  fp2_neg(n, n);
+  fp2_mul(d, A, tv2);
+  fp2 za;
+  fp2_mul(za, Zc, A);
+  fp2_cmov(n, B, exceptional);
+  fp2_cmov(d, za, exceptional);
+  fp2_sqr(d2, d);
+  fp2_mul(d3, d2, d);
+  // U = n (n^2 + A d^2) + B d^3
+  fp2_mul(t, A, d2);
+  fp2_sqr(U, n);
+  fp2_add(U, U, t);
+  fp2_mul(U, U, n);
+  fp2_mul(t, B, d3);
+  fp2_add(U, U, t);
+  fp2 vc;
+  fp2_conj(vc, d3);
+  fp2_mul(W, U, vc);
+  fp m, nW, e, chk, s1, s2, nu, c1;
+  fp_sqr(m, d3.c0);
+  fp_sqr(e, d3.c1);
+  fp_add(m, m, e);  // N(V)
+  fp_sqr(nW, W.c0);
+  fp_sqr(e, W.c1);
+  fp_add(nW, nW, e);
+  fp_pow_p34(e, nW);
   fp_sqr(chk, e);
-  fp_mul(chk, chk, n1);
-  const bool sq1 = fp_eq(chk, one) || fp_is_zero(n1);
-  fp_mul(s1, n1, e);
+  fp_mul(chk, chk, nW);
+  fp onep;
+  fp_one(onep);
+  const bool sq1 = fp_eq(chk, onep) || fp_is_zero(nW);
+  fp_mul(s1, nW, e);
   fp_sqr(nu, u.c0);
   fp_sqr(e, u.c1);
   fp_add(nu, nu, e);
-  fp_sqr(nu3, nu);
-  fp_mul(nu3, nu3, nu);
+  fp_sqr(s2, nu);
+  fp_mul(s2, s2, nu);
   fp_set(c1, LB_SSWU_NZ3_SQRT);
-  fp_mul(s2, nu3, c1);
+  fp_mul(s2, s2, c1);
   fp_mul(s2, s2, s1);
-  x = x1;
-  gx = gx1;
   fp_cmov(s2, s1, sq1);
-  fp2_cmov(x, x2, !sq1);
-  fp2_cmov(gx, gx2, !sq1);
-  fp2_sqrt_with_norm_root(y, gx, s2);
+  // x2 branch: x_n = tv1 n, W2 = tv1^3 W
+  fp2 xn_, W2;
+  fp2_mul(xn_, tv1, n);
+  fp2_sqr(t, tv1);
+  fp2_mul(t, t, tv1);
+  fp2_mul(W2, t, W);
+  fp2_cmov(xn_, n, sq1);
+  fp2_cmov(W2, W, sq1);
+  fp2 y;
+  fp2_sqrt_ratio_frac(y, W2, m, s2);
   fp2 ny;
   fp2_neg(ny, y);
   fp2_cmov(y, ny, fp2_sgn0(u) != fp2_sgn0(y));
-  out.x = x;
-  out.y = y;
-  out.inf = false;
-}
+  // isogeny, Horner in x_n with the d powers (d, d2, d3 live)
+  fp2 XN, XD, YN, YD;
+  fp2_set(XN, LB_ISO_XNUM3);
+  fp2_mul(XN, XN, xn_);
+  fp2_mul_const(t, d, LB_ISO_XNUM2);
+  fp2_add(XN, XN, t);
+  fp2_mul(XN, XN, xn_);
+  fp2_mul_const(t, d2, LB_ISO_XNUM1);
+  fp2_add(XN, XN, t);
+  fp2_mul(XN, XN, xn_);
+  fp2_mul_const(t, d3, LB_ISO_XNUM0);
+  fp2_add(XN, XN, t);
 
-// 3-isogeny E2' -> E2, output Jacobian (no inversion):
-//   x = xn/xd, y = y' yn/yd ;  Z = xd yd, X = xn xd yd^2, Y = y' yn xd^3 yd^2
-LB_DEV void iso_map_g2(g2j& r, const g2a& p) {
-  fp2 xn, xd, yn, yd, t;
-  fp2_set(xn, LB_ISO_XNUM3);
-  fp2_mul(xn, xn, p.x);
-  fp2_set(t, LB_ISO_XNUM2);
-  fp2_add(xn, xn, t);
-  fp2_mul(xn, xn, p.x);
-  fp2_set(t, LB_ISO_XNUM1);
-  fp2_add(xn, xn, t);
-  fp2_mul(xn, xn, p.x);
-  fp2_set(t, LB_ISO_XNUM0);
-  fp2_add(xn, xn, t);
+  fp2_mul_const(t, d, LB_ISO_XDEN1);
+  fp2_add(XD, xn_, t);  // monic
+  fp2_mul(XD, XD, xn_);
+  fp2_mul_const(t, d2, LB_ISO_XDEN0);
+  fp2_add(XD, XD, t);
 
-  fp2_set(t, LB_ISO_XDEN1);
-  fp2_add(xd, p.x, t);  // monic
-  fp2_mul(xd, xd, p.x);
-  fp2_set(t, LB_ISO_XDEN0);
-  fp2_add(xd, xd, t);
+  fp2_set(YN, LB_ISO_YNUM3);
+  fp2_mul(YN, YN, xn_);
+  fp2_mul_const(t, d, LB_ISO_YNUM2);
+  fp2_add(YN, YN, t);
+  fp2_mul(YN, YN, xn_);
+  fp2_mul_const(t, d2, LB_ISO_YNUM1);
+  fp2_add(YN, YN, t);
+  fp2_mul(YN, YN, xn_);
+  fp2_mul_const(t, d3, LB_ISO_YNUM0);
+  fp2_add(YN, YN, t);
 
-  fp2_set(yn, LB_ISO_YNUM3);
-  fp2_mul(yn, yn, p.x);
-  fp2_set(t, LB_ISO_YNUM2);
-  fp2_add(yn, yn, t);
-  fp2_mul(yn, yn, p.x);
-  fp2_set(t, LB_ISO_YNUM1);
-  fp2_add(yn, yn, t);
-  fp2_mul(yn, yn, p.x);
-  fp2_set(t, LB_ISO_YNUM0);
-  fp2_add(yn, yn, t);
+  fp2_mul_const(t, d, LB_ISO_YDEN2);
+  fp2_add(YD, xn_, t);  // monic
+  fp2_mul(YD, YD, xn_);
+  fp2_mul_const(t, d2, LB_ISO_YDEN1);
+  fp2_add(YD, YD, t);
+  fp2_mul(YD, YD, xn_);
+  fp2_mul_const(t, d3, LB_ISO_YDEN0);
+  fp2_add(YD, YD, t);
 
-  fp2_set(t, LB_ISO_YDEN2);
-  fp2_add(yd, p.x, t);  // monic
-  fp2_mul(yd, yd, p.x);
-  fp2_set(t, LB_ISO_YDEN1);
-  fp2_add(yd, yd, t);
-  fp2_mul(yd, yd, p.x);
-  fp2_set(t, LB_ISO_YDEN0);
-  fp2_add(yd, yd, t);
-
-  if (fp2_is_zero(xd) || fp2_is_zero(yd)) {  // kernel point -> infinity
+  if (fp2_is_zero(XD) || fp2_is_zero(YD)) {  // kernel point -> infinity
     jac_set_inf(r);
     return;
   }
-  fp2 yd2, xd2;
-  fp2_mul(r.Z, xd, yd);
-  fp2_sqr(yd2, yd);
-  fp2_mul(t, xn, xd);
-  fp2_mul(r.X, t, yd2);
-  fp2_sqr(xd2, xd);
-  fp2_mul(xd2, xd2, xd);  // xd^3
-  fp2_mul(t, p.y, yn);
-  fp2_mul(t, t, xd2);
-  fp2_mul(r.Y, t, yd2);
+  fp2 XDd, YD2;
+  fp2_mul(XDd, XD, d);
+  fp2_mul(r.Z, XDd, YD);
+  fp2_sqr(YD2, YD);
+  fp2_mul(t, XN, XDd);
+  fp2_mul(r.X, t, YD2);
+  fp2_sqr(t, XDd);
+  fp2_mul(t, t, XDd);  // (XD d)^3
+  fp2_mul(YN, YN, y);
+  fp2_mul(YN, YN, t);
+  fp2_mul(r.Y, YN, YD2);
 }
 
 // clear_cofactor (RFC 9380 G.3): (x^2 - x - 1)P + (x - 1)psi(P) + psi^2(2P), x < 0.
@@ -352,9 +383,7 @@ LB_DEV void hash_to_g2_half(g2j& r, const uint8_t msg[32], int j) {
   fp2 u;
   fp_from_64be_words(u.c0, ub + 32 * j);
   fp_from_64be_words(u.c1, ub + 32 * j + 16);
-  g2a q;
-  map_to_curve_sswu(q, u);
-  iso_map_g2(r, q);
+  map_to_g2_sswu_iso(r, u);
 }
 // Q0 + Q1 -> clear_cofactor
 LB_DEV void hash_to_g2_finish(g2j& r, const g2j& q0, const g2j& q1, g2j* stash = nullptr) {
@@ -367,12 +396,9 @@ LB_DEV void hash_to_g2_finish(g2j& r, const g2j& q0, const g2j& q1, g2j* stash =
 LB_DEV void hash_to_g2(g2j& r, const uint8_t msg[32]) {
   fp2 u[2];
   hash_to_field_fp2_2(u, msg);
-  g2a q0, q1;
-  map_to_curve_sswu(q0, u[0]);
-  map_to_curve_sswu(q1, u[1]);
   g2j j0, j1;
-  iso_map_g2(j0, q0);
-  iso_map_g2(j1, q1);
+  map_to_g2_sswu_iso(j0, u[0]);
+  map_to_g2_sswu_iso(j1, u[1]);
   jac_add(j0, j0, j1);
   clear_cofactor_g2(r, j0);
 }
