@@ -241,6 +241,9 @@ int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* batch,
                                      uint8_t* out_request_valid, uint8_t* out_request_error, uint8_t* out_set_status,
                                      uint64_t* out_ticket);
 int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576);
+/* Non-blocking: *out_ready = 1 when lb_partial_wait(ticket) would return at once
+ * (a host's resolver thread polls it, so the combine never stalls submission). */
+int lb_partial_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_ready);
 int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* out_is_one);
 int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok);
 

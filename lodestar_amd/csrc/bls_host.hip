@@ -1431,6 +1431,24 @@ int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576) {
   return LB_OK;
 }
 
+int lb_partial_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_ready) {
+  if (!ctx || !out_ready) return LB_ERR_INVALID_ARGUMENT;
+  LB_HIP(hipSetDevice(ctx->device));
+  Slot* sl = slot_of_ticket(ctx, ticket);
+  if (!sl || !sl->partial_pending) {
+    ctx->err = "ticket is not a pending two-phase call";
+    return LB_ERR_INVALID_ARGUMENT;
+  }
+  const hipError_t q = hipEventQuery(sl->partial_ev);
+  if (q == hipErrorNotReady) {
+    *out_ready = 0;
+    return LB_OK;
+  }
+  LB_HIP(q);
+  *out_ready = 1;
+  return LB_OK;
+}
+
 int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));

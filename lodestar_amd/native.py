@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
     "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
-    "lb_verify_requests_priority_async",
+    "lb_verify_requests_priority_async", "lb_partial_poll",
 )
 
 LB_BATCH_DEVICE = 1
@@ -150,6 +150,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_poll.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_verify_requests_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                              ctypes.POINTER(ctypes.c_uint64)]
+    lib.lb_partial_poll.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]
     lib.lb_verify_requests_priority_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp,
                                                       ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_verify_requests_partial_async.argtypes = [vp, ctypes.POINTER(_RequestBatch), u32, vp, vp, vp,
@@ -496,6 +497,12 @@ class Device:
         out = np.zeros(LB_GT_BYTES, np.uint8)
         self._check(self.lib.lb_partial_wait(self._h, ticket, _ptr(out)), "lb_partial_wait")
         return out.tobytes()
+
+    def partial_ready(self, ticket: int) -> bool:
+        """True when partial_wait_t(ticket) would return at once (lb_partial_poll)."""
+        r = ctypes.c_int32(0)
+        self._check(self.lib.lb_partial_poll(self._h, ticket, ctypes.byref(r)), "lb_partial_poll")
+        return bool(r.value)
 
     def finish_t(self, ticket: int, merged_ok: bool) -> None:
         self._check(self.lib.lb_verify_requests_finish(self._h, ticket, 1 if merged_ok else 0),
