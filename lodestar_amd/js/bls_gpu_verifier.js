@@ -54,6 +54,45 @@ class QueueError extends Error {
   }
 }
 
+/** The pool's job queue: push / unshift / shift in O(1) (a package takes 512 jobs from a
+ * queue that can hold ~50k under load; Array.prototype.shift on that moved the whole
+ * array per job). */
+class JobQueue {
+  constructor() {
+    this.a = [];
+    this.h = 0;
+  }
+  get length() {
+    return this.a.length - this.h;
+  }
+  at(i) {
+    return this.a[this.h + i];
+  }
+  push(x) {
+    this.a.push(x);
+  }
+  unshift(x) {
+    if (this.h > 0) this.a[--this.h] = x;
+    else this.a.unshift(x);
+  }
+  shift() {
+    if (this.h >= this.a.length) return undefined;
+    const x = this.a[this.h];
+    this.a[this.h++] = undefined;
+    if (this.h > 1024 && this.h * 2 > this.a.length) {
+      this.a = this.a.slice(this.h);
+      this.h = 0;
+    }
+    return x;
+  }
+  clear() {
+    const rest = this.a.slice(this.h);
+    this.a = [];
+    this.h = 0;
+    return rest;
+  }
+}
+
 function loadAddon() {
   return require(path.join(__dirname, "..", "napi", "lodestar_bls.node"));
 }
@@ -326,7 +365,7 @@ class BlsGpuVerifier {
     this.metrics = new PoolMetrics();
     this.priorityLane = o.priorityLane === undefined ? true : Boolean(o.priorityLane);
     this.prioBusy = this.backends.map(() => false);  // one priority package in flight per GPU
-    this.jobs = [];
+    this.jobs = new JobQueue();
     this.buffered = null;
     this.idle = [];
     // per GPU: the addon's calls in flight plus `prefetch` packages packed ahead and queued
@@ -404,8 +443,7 @@ class BlsGpuVerifier {
         job.reject(new QueueError(QueueErrorCode.QUEUE_ABORTED));
       this.buffered = null;
     }
-    for (const job of this.jobs) job.reject(new QueueError(QueueErrorCode.QUEUE_ABORTED));
-    this.jobs = [];
+    for (const job of this.jobs.clear()) job.reject(new QueueError(QueueErrorCode.QUEUE_ABORTED));
     this.closed = true;
     await Promise.all([...this.running].map((p) => p.catch(() => undefined)));
     await Promise.all(this.backends.map((b) => (b.close ? b.close() : undefined)));
@@ -444,17 +482,20 @@ class BlsGpuVerifier {
   prepareWork(skip = 0) {
     const jobs = [];
     let total = 0;
-    while (total < this.maxSetsPerDispatch && this.jobs.length > skip) {
-      const job = this.jobs.splice(skip, 1)[0];
+    const held = [];
+    for (let q = 0; q < skip; q++) held.push(this.jobs.shift());
+    while (total < this.maxSetsPerDispatch && this.jobs.length > 0) {
+      const job = this.jobs.shift();
       jobs.push(job);
       total += job.type === "default" ? job.sets.length : 1;
     }
+    for (let q = held.length - 1; q >= 0; q--) this.jobs.unshift(held[q]);
     return jobs;
   }
 
   leadingPriorityJobs() {
     let n = 0;
-    while (n < this.jobs.length && this.jobs[n].opts.priority && this.jobs[n].type === "default") n++;
+    while (n < this.jobs.length && this.jobs.at(n).opts.priority && this.jobs.at(n).type === "default") n++;
     return n;
   }
 
@@ -481,7 +522,7 @@ class BlsGpuVerifier {
     const jobs = [];
     let total = 0;
     while (this.jobs.length > 0) {
-      const j = this.jobs[0];
+      const j = this.jobs.at(0);
       if (!j.opts.priority || j.type !== "default") break;
       if (jobs.length && total + j.sets.length > MAX_PRIORITY_LANE_SETS) break;
       jobs.push(this.jobs.shift());
@@ -731,7 +772,11 @@ function slicePacked(p, lo, hi, seed) {
   const kb = p.pkOffsets[b];
   const sa = p.sigOffsets[a];
   const sb = p.sigOffsets[b];
-  const rebase = (arr, x, y, base) => Uint32Array.from(arr.subarray(x, y), (v) => v - base);
+  const rebase = (arr, x, y, base) => {
+    const o = arr.slice(x, y);
+    if (base !== 0) for (let q = 0; q < o.length; q++) o[q] -= base;
+    return o;
+  };
   const out = {
     requestOffsets: rebase(p.requestOffsets, lo, hi + 1, a),
     pkOffsets: rebase(p.pkOffsets, a, b + 1, ka),

@@ -6,8 +6,10 @@
 // worker.ts:24-30) with one call per package on a GPU.
 //
 // Threading: JS calls arrive on the main thread; their
-// inputs are copied there (the reference structured-clones them to the worker,
-// index.ts:444) and handed to ONE host submission thread per GPU, which owns
+// offsets are copied there (the reference structured-clones its requests to the
+// worker, index.ts:444), the bulk arrays of verifyRequests are read in place (kept
+// alive by references until the promise settles: the caller must not modify them
+// meanwhile), and the task goes to ONE host submission thread per GPU, which owns
 // the lb_ctx (not thread-safe) and keeps up to `capacity` calls in flight
 // (lb_verify_requests_async + lb_wait).  Completions come back to the event
 // loop through a threadsafe function; the event loop never blocks on the GPU.
@@ -109,6 +111,46 @@ bool opt_typed(napi_env env, napi_value obj, const char* name, napi_typedarray_t
   return true;
 }
 
+// A typed array read in place (no copy on the JS thread): the caller's buffer, kept
+// alive by a reference the JS thread releases when the task settles.  Used for the
+// bulk inputs of verifyRequests (messages, signatures, pubkeys, pubkeyIndices: ~8 MB
+// for a 65,536-set package, ~1 ms of main-thread memcpy); the caller must not modify
+// them until the promise settles (packRequests' arrays are fresh and private).
+template <class T>
+struct View {
+  const T* p = nullptr;
+  size_t n = 0;
+  std::vector<T> own;  // a copy instead (empty-array placeholder)
+  const T* data() const { return p ? p : own.data(); }
+  size_t size() const { return p ? n : own.size(); }
+  bool empty() const { return size() == 0; }
+};
+
+template <class T>
+void typed_view(napi_env env, napi_value v, napi_typedarray_type want, const char* name, View<T>& out,
+                std::vector<napi_ref>& refs) {
+  bool is = false;
+  napi_is_typedarray(env, v, &is);
+  if (!is) throw ArgError{std::string(name) + " must be a typed array"};
+  napi_typedarray_type t;
+  size_t len = 0;
+  void* data = nullptr;
+  napi_value ab;
+  size_t off = 0;
+  napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+  if (t != want && !(want == napi_uint8_array && t == napi_uint8_clamped_array))
+    throw ArgError{std::string(name) + (want == napi_uint8_array ? " must be a Uint8Array" : " must be a Uint32Array")};
+  napi_ref r = nullptr;
+  if (len && napi_create_reference(env, v, 1, &r) == napi_ok) {
+    refs.push_back(r);
+    out.p = static_cast<const T*>(data);
+    out.n = len;
+  } else {
+    out.p = nullptr;
+    out.own.assign(static_cast<const T*>(data), static_cast<const T*>(data) + len);
+  }
+}
+
 void check_offsets(const std::vector<uint32_t>& off, size_t n, uint32_t last, const char* name) {
   if (off.size() != n + 1) throw ArgError{std::string(name) + ": wrong length"};
   if (off[0] != 0) throw ArgError{std::string(name) + " must start at 0"};
@@ -126,6 +168,10 @@ struct Task {
   // inputs (copied on the JS thread)
   std::vector<uint32_t> req_off, pk_off, sig_off, pk_idx, job_off;
   std::vector<uint8_t> pubkeys, messages, signatures, seed, batchable;
+  // verifyRequests: the bulk inputs read in place (see View); refs released on the JS thread
+  View<uint8_t> v_pubkeys, v_messages, v_signatures;
+  View<uint32_t> v_pk_idx;
+  std::vector<napi_ref> refs;
   bool has_pk_off = false, by_index = false, has_batchable = false, mixed = false;
   bool prio = false;  // verifyRequests(batch, {priority: true}): the device's priority lane
   uint32_t n_req = 0, n_sets = 0, n_jobs = 0, pk_len = 0, n_keys = 0;
@@ -152,37 +198,50 @@ void parse_requests(napi_env env, napi_value obj, Task& t) {
   t.n_req = (uint32_t)t.req_off.size() - 1;
   t.n_sets = t.req_off.back();
   check_offsets(t.req_off, t.n_req, UINT32_MAX, "requestOffsets");
-  req_typed(env, obj, "messages", napi_uint8_array, t.messages);
-  if (t.messages.size() != (size_t)t.n_sets * 32) throw ArgError{"messages: 32 bytes per set"};
-  req_typed(env, obj, "signatures", napi_uint8_array, t.signatures);
+  napi_value mv, sv;
+  if (!has_prop(env, obj, "messages", &mv)) throw ArgError{"missing messages"};
+  typed_view(env, mv, napi_uint8_array, "messages", t.v_messages, t.refs);
+  if (t.v_messages.size() != (size_t)t.n_sets * 32) throw ArgError{"messages: 32 bytes per set"};
+  if (!has_prop(env, obj, "signatures", &sv)) throw ArgError{"missing signatures"};
+  typed_view(env, sv, napi_uint8_array, "signatures", t.v_signatures, t.refs);
   req_typed(env, obj, "sigOffsets", napi_uint32_array, t.sig_off);
-  check_offsets(t.sig_off, t.n_sets, (uint32_t)t.signatures.size(), "sigOffsets");
+  check_offsets(t.sig_off, t.n_sets, (uint32_t)t.v_signatures.size(), "sigOffsets");
   req_typed(env, obj, "seed", napi_uint8_array, t.seed);
   if (t.seed.size() != 32) throw ArgError{"seed must be 32 bytes"};
   t.has_pk_off = opt_typed(env, obj, "pkOffsets", napi_uint32_array, t.pk_off);
   if (t.has_pk_off) check_offsets(t.pk_off, t.n_sets, UINT32_MAX, "pkOffsets");
   const size_t n_pk = t.has_pk_off ? t.pk_off[t.n_sets] : t.n_sets;
-  t.by_index = opt_typed(env, obj, "pubkeyIndices", napi_uint32_array, t.pk_idx);
+  napi_value iv, kv;
+  t.by_index = has_prop(env, obj, "pubkeyIndices", &iv);
+  const bool has_keys = has_prop(env, obj, "pubkeys", &kv);
+  if (has_keys) typed_view(env, kv, napi_uint8_array, "pubkeys", t.v_pubkeys, t.refs);
   if (t.by_index) {
-    if (t.pk_idx.size() != n_pk) throw ArgError{"pubkeyIndices: one index per pubkey"};
+    typed_view(env, iv, napi_uint32_array, "pubkeyIndices", t.v_pk_idx, t.refs);
+    if (t.v_pk_idx.size() != n_pk) throw ArgError{"pubkeyIndices: one index per pubkey"};
     // mixed package: rows of `pubkeys` named by indices with LB_PK_ROW_FLAG set
     size_t rows = 0;
-    for (const uint32_t j : t.pk_idx)
-      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & ~LB_PK_ROW_FLAG) + 1 > rows) rows = (j & ~LB_PK_ROW_FLAG) + 1;
-    t.mixed = opt_typed(env, obj, "pubkeys", napi_uint8_array, t.pubkeys);
-    if (rows && (!t.mixed || t.pubkeys.size() < rows * LB_PUBKEY_BYTES))
+    const uint32_t* ix = t.v_pk_idx.data();
+    for (size_t q = 0; q < n_pk; q++)
+      if ((ix[q] & LB_PK_ROW_FLAG) && (size_t)(ix[q] & ~LB_PK_ROW_FLAG) + 1 > rows) rows = (ix[q] & ~LB_PK_ROW_FLAG) + 1;
+    t.mixed = has_keys;
+    if (rows && (!t.mixed || t.v_pubkeys.size() < rows * LB_PUBKEY_BYTES))
       throw ArgError{"pubkeyIndices name pubkey rows that `pubkeys` does not hold"};
   } else {
-    if (!opt_typed(env, obj, "pubkeys", napi_uint8_array, t.pubkeys) && n_pk)
-      throw ArgError{"missing pubkeys (or pubkeyIndices)"};
-    if (t.pubkeys.size() != n_pk * LB_PUBKEY_BYTES) throw ArgError{"pubkeys: 96 bytes per pubkey"};
+    if (!has_keys && n_pk) throw ArgError{"missing pubkeys (or pubkeyIndices)"};
+    if (t.v_pubkeys.size() != n_pk * LB_PUBKEY_BYTES) throw ArgError{"pubkeys: 96 bytes per pubkey"};
   }
   t.has_batchable = opt_typed(env, obj, "batchable", napi_uint8_array, t.batchable);
   if (t.has_batchable && t.batchable.size() != t.n_req) throw ArgError{"batchable: one flag per request"};
-  if (t.signatures.empty()) t.signatures.push_back(0);
-  if (t.messages.empty()) t.messages.push_back(0);
-  if (t.pubkeys.empty()) t.pubkeys.push_back(0);
-  if (t.pk_idx.empty()) t.pk_idx.push_back(0);
+  // (empty arrays: one placeholder byte / index, so every pointer is valid)
+  if (t.v_signatures.empty()) t.v_signatures.own.assign(1, 0);
+  if (t.v_messages.empty()) t.v_messages.own.assign(1, 0);
+  if (t.v_pubkeys.empty()) t.v_pubkeys.own.assign(1, 0);
+  if (t.v_pk_idx.empty()) t.v_pk_idx.own.assign(1, 0);
+}
+
+void release_refs(napi_env env, Task* t) {
+  for (napi_ref r : t->refs) napi_delete_reference(env, r);
+  t->refs.clear();
 }
 
 lb_request_batch batch_of(Task& t) {
@@ -191,13 +250,13 @@ lb_request_batch batch_of(Task& t) {
   b.n_sets = t.n_sets;
   b.request_offsets = t.req_off.data();
   b.request_batchable = t.has_batchable ? t.batchable.data() : nullptr;
-  b.pubkeys = (!t.by_index || t.mixed) ? t.pubkeys.data() : nullptr;
+  b.pubkeys = (!t.by_index || t.mixed) ? t.v_pubkeys.data() : nullptr;
   b.pk_offsets = t.has_pk_off ? t.pk_off.data() : nullptr;
-  b.messages = t.messages.data();
-  b.signatures = t.signatures.data();
+  b.messages = t.v_messages.data();
+  b.signatures = t.v_signatures.data();
   b.sig_offsets = t.sig_off.data();
   b.seed = t.seed.data();
-  b.pubkey_indices = t.by_index ? t.pk_idx.data() : nullptr;
+  b.pubkey_indices = t.by_index ? t.v_pk_idx.data() : nullptr;
   return b;
 }
 
@@ -308,6 +367,7 @@ void worker_loop(Context* c) {
         w->n_req = owner->n_req;
         w->n_sets = owner->n_sets;
         w->t_start = owner->t_start;
+        w->refs.swap(owner->refs);  // its inputs' references, released on the JS thread
         c->partials.erase(owner->partial_id);
         delete owner;
       }
@@ -346,6 +406,7 @@ void worker_loop(Context* c) {
         if (rc == LB_OK) rc = lb_partial_wait(c->ctx, call->ticket, t->out_bytes.data());
         if (rc != LB_OK) {
           fail(t, rc, c->ctx);
+          t->refs.swap(call->refs);
           delete call;
         } else {
           call->partial_id = t->partial_id;
@@ -446,6 +507,7 @@ void worker_loop(Context* c) {
             w->stats = owner->stats;
             w->n_req = owner->n_req;
             w->n_sets = owner->n_sets;
+            w->refs.swap(owner->refs);
             c->partials.erase(owner->partial_id);
             delete owner;
           }
@@ -527,6 +589,7 @@ void call_js(napi_env env, napi_value /*cb*/, void* context, void* data) {
     delete t;
     return;
   }
+  release_refs(env, t);
   napi_value result = nullptr;
   if (t->rc != LB_OK) {
     napi_reject_deferred(env, t->deferred, make_error(env, t->rc, t->errmsg));
@@ -594,6 +657,7 @@ napi_value submit(napi_env env, Context* c, Task* t) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->closing) {
       napi_reject_deferred(env, t->deferred, make_error(env, LB_ERR_INVALID_ARGUMENT, "QUEUE_ERROR_QUEUE_ABORTED: context closed"));
+      release_refs(env, t);
       delete t;
       return promise;
     }
@@ -640,6 +704,7 @@ napi_value m_verify(napi_env env, napi_callback_info info, Kind kind) {
       t->prio = b;
     }
   } catch (const ArgError& e) {
+    release_refs(env, t);
     delete t;
     return rejected(env, e.msg);
   }
@@ -804,7 +869,10 @@ void finalize_ctx(napi_env env, void* data, void* /*hint*/) {
       std::lock_guard<std::mutex> lk(c->mu);
       c->finalizing = true;
       c->closing = true;
-      for (Task* t : c->queue) delete t;
+      for (Task* t : c->queue) {
+        release_refs(env, t);
+        delete t;
+      }
       c->queue.clear();
     }
     c->cv.notify_one();
@@ -865,9 +933,11 @@ napi_value ValidateRequests(napi_env env, napi_callback_info info) {
     if (argc < 1) throw ArgError{"validateRequests(batch)"};
     parse_requests(env, argv[0], t);
   } catch (const ArgError& e) {
+    release_refs(env, &t);
     napi_throw_type_error(env, nullptr, e.msg.c_str());
     return nullptr;
   }
+  release_refs(env, &t);
   napi_value o;
   napi_create_object(env, &o);
   set_num(env, o, "nRequests", t.n_req);

@@ -29,7 +29,9 @@ function median(xs) {
   const msgs = rd("msgs.bin");
   const sigs = rd("sigs.bin");
   const n = msgs.length / 32;
-  const v = new V.BlsGpuVerifier({devices: [0]});
+  // LB_JS_PREFETCH: packages packed ahead per GPU (BlsGpuVerifier prefetch; default 0)
+  const prefetch = process.env.LB_JS_PREFETCH ? parseInt(process.env.LB_JS_PREFETCH, 10) : undefined;
+  const v = new V.BlsGpuVerifier({devices: [0], prefetch});
   const tableSize = await v.syncPubkeys(Array.from({length: n}, (_, i) => pks.subarray(96 * i, 96 * i + 96)), 96);
   const set = (i) => ({
     type: "single",

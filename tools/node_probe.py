@@ -26,12 +26,16 @@ def main():
         with open(os.path.join(d, name + ".bin"), "wb") as f:
             f.write(b"".join(items))
     res = {}
-    env = dict(os.environ, LB_NODE_PRE="1", LB_JS_TRACE="1", LB_HOST_TRACE="1")
-    for rounds, prof in ((96, False),):
+    # LB_PROBE_PREFETCH="0,1,2": one run per JS prefetch depth (packages packed ahead per GPU)
+    variants = [int(x) for x in os.environ.get("LB_PROBE_PREFETCH", "0").split(",")]
+    rounds_n = int(os.environ.get("LB_PROBE_ROUNDS", "96"))
+    for pf in variants:
+        env = dict(os.environ, LB_NODE_PRE="1", LB_JS_TRACE="1", LB_HOST_TRACE="1", LB_JS_PREFETCH=str(pf))
+        rounds, prof = rounds_n, False
         cmd = ["node"] + (["--cpu-prof", "--cpu-prof-dir=" + os.path.join(out, "cpuprof")] if prof else []) + \
               [os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
-        key = "rounds%d%s" % (rounds, "_prof" if prof else "")
+        key = "rounds%d_prefetch%d%s" % (rounds, pf, "_prof" if prof else "")
         with open(os.path.join(out, key + "_stderr.txt"), "w") as f:
             f.write(r.stderr)
         ph = {}
