@@ -24,7 +24,8 @@ import importlib.util
 import os
 
 from .dsl import Flag, Fp, Graph, P, select, select_n
-from .tower import (P34, Fp2, Fp6, Fp12, Jac, Ops, fp2_lex_largest, fp2_sgn0, fp_pow, jac_add, jac_add_aff,
+from .tower import (P34, Fp2, Fp6, Fp12, Jac, Ops, Proj, fp2_lex_largest, fp2_sgn0, fp_pow, jac_add, jac_add_aff,
+                    proj_add, proj_dbl, proj_eq, proj_from_jac, proj_mul_xabs,
                     jac_dbl, jac_eq, jac_inf, jsel, line_mul_line)
 
 X_ABS = 0xD201000000010000
@@ -86,8 +87,179 @@ def fp2_sqrt(a: Fp2):
 
 
 # ---------------------------------------------------------------------------
+# Square roots in Fp2 from ONE exponentiation (q = p^2 = 9 mod 16), the round
+# programs' form: depth ~log2(p) instead of the norm method's two sequential Fp
+# exponentiations (bls_field.h fp2_sqrt).  For U / V (V != 0):
+#   y0 = U V^3 (U V^7)^c1,  c1 = (q - 9) / 16   =>   y0^2 = (U / V) zeta,
+#   zeta = (U / V)^((q-1)/8) an 8th root of unity: a 4th root (1, -1, i, -i) iff
+#   U / V is a square, and then sqrt(U / V) = y0 / sqrt(zeta).
+# (U V^7)^c1 splits as w^e0 conj(w)^e1 with c1 = e1 p + e0 (w^p = conj(w)), so ONE
+# squaring chain of ~381 Fp2 squarings carries both halves (RFC 9380's
+# sqrt_ratio for q = 9 mod 16, restated).  Which root comes out does not matter:
+# every caller fixes the sign (sgn0 / lex_largest) afterwards.
+# ---------------------------------------------------------------------------
+def _f2m(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def _f2pow(a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = _f2m(r, a)
+        a = _f2m(a, a)
+        e >>= 1
+    return r
+
+
+def _f2inv(a):
+    n = pow((a[0] * a[0] + a[1] * a[1]) % P, P - 2, P)
+    return (a[0] * n % P, (-a[1]) * n % P)
+
+
+def _f2sqrt(a):
+    """a square root of a in Fp2 (generator time), or None"""
+    if a == (0, 0):
+        return (0, 0)
+    y0 = _f2m(_f2pow(a, (P * P + 7) // 16), (1, 0))
+    for eta in _ETA4:
+        y = _f2m(y0, eta)
+        if _f2m(y, y) == a:
+            return y
+    return None
+
+
+_Q = P * P
+_C1 = (_Q - 9) // 16
+_E1, _E0 = divmod(_C1, P)
+_I = (0, 1)
+_RHO = None  # a primitive 8th root of unity with rho^2 = i (found below)
+for _c in range(2, 200):
+    _r = _f2pow((_c, 1), (_Q - 1) // 8)
+    if _f2pow(_r, 4) == (P - 1, 0) and _f2m(_r, _r) == _I:
+        _RHO = _r
+        break
+assert _RHO is not None
+_ZETA4 = [(1, 0), (P - 1, 0), _I, (0, P - 1)]                      # 1, -1, i, -i
+_SQRT4 = [(1, 0), _I, _RHO, _f2pow(_RHO, 3)]                       # their square roots
+_ETA4 = [_f2inv(x) for x in _SQRT4]                                 # y = y0 eta
+_ZETA8 = [_f2pow(_RHO, k) for k in (1, 3, 5, 7)]                   # primitive 8th roots
+for _z, _sq in zip(_ZETA4, _SQRT4):
+    assert _f2m(_sq, _sq) == _z
+
+
+def fp2_pow_c1(w: Fp2) -> Fp2:
+    """w^c1 = w^e0 conj(w)^e1: one squaring chain s_i = w^(2^i); the running product
+    takes s_i, conj(s_i) or N(s_i) = s_i conj(s_i) (an Fp scalar) per bit pair."""
+    g = w.g
+    acc = None
+    s = w
+    nb = max(_E0.bit_length(), _E1.bit_length())
+    for i in range(nb):
+        a, b = (_E0 >> i) & 1, (_E1 >> i) & 1
+        if a or b:
+            if a and b:
+                n = s.norm()
+                acc = Fp2(n, g.zero()) if acc is None else acc * n
+            else:
+                m = s if a else s.conj()
+                acc = m if acc is None else acc * m
+        if i + 1 < nb:
+            s = s.sqr()
+    return acc
+
+
+def fp2_sqrt_ratio_y0(U: Fp2, V: Fp2 = None):
+    """(y0, A): y0 = U V^3 (U V^7)^c1 and A = y0^2 V (= U zeta); V None means 1"""
+    if V is None:
+        t = fp2_pow_c1(U)
+        y0 = U * t
+        return y0, y0.sqr()
+    V2 = V.sqr()
+    V3 = V2 * V
+    V4 = V2.sqr()
+    V7 = V4 * V3
+    t = fp2_pow_c1(U * V7)
+    y0 = (U * V3) * t
+    return y0, y0.sqr() * V
+
+
+def fp2_sqrt1(a: Fp2):
+    """(root, is_square) of a (the one-exponentiation method; bls_field.h fp2_sqrt's
+    contract: which root is unspecified)"""
+    y0, A = fp2_sqrt_ratio_y0(a)
+    hits = [(A - a * Fp2.const(a.g, z) if z != (1, 0) else A - a).is_zero() for z in _ZETA4]
+    root = select_n([(h, y0 * Fp2.const(a.g, eta)) for h, eta in zip(hits[1:], _ETA4[1:])], y0)
+    sq = hits[0] | hits[1] | hits[2] | hits[3]
+    return root, sq
+
+
+# ---------------------------------------------------------------------------
 # hash_to_G2 (bls_hash.h): SSWU, 3-isogeny, Q0 + Q1, clear_cofactor
 # ---------------------------------------------------------------------------
+def map_to_curve_sswu_iso(u: Fp2) -> Proj:
+    """Simplified SWU onto E2' and the 3-isogeny to E2 with ONE exponentiation and no
+    inversion (the device's map_to_g2_sswu_iso, restated for round programs).
+    x1 = n / d (n = -B (tv2 + 1), d = A tv2; tv2 = 0: n = B, d = Z A), g(x1) = U / V with
+    U = n^3 + A n d^2 + B d^3, V = d^3; y0 = U V^3 (U V^7)^c1 has y0^2 = g(x1) zeta.
+    g(x1) a square (zeta a 4th root): y = y0 / sqrt(zeta), x = x1.  Otherwise zeta is
+    a primitive 8th root and g(x2) = (Z u^2)^3 g(x1) is the square:
+    y = u^3 y0 sqrt(Z^3 / zeta), x = x2 = Z u^2 x1.  The sign of y follows sgn0(u).
+    The isogeny is homogenised in (x_n, d) and lands in homogeneous coordinates."""
+    g = u.g
+    A = c2(g, "LB_SSWU_A")
+    B = c2(g, "LB_SSWU_B")
+    Z = c2(g, "LB_SSWU_Z")
+    tv1 = Z * u.sqr()
+    tv2 = tv1.sqr() + tv1
+    exceptional = tv2.is_zero()
+    n = select(exceptional, B, -(B * (tv2 + Fp2.one(g))))
+    d = select(exceptional, Z * A, A * tv2)
+    d2 = d.sqr()
+    d3 = d2 * d
+    U = n * (n.sqr() + A * d2) + B * d3
+    y0, Aq = fp2_sqrt_ratio_y0(U, d3)
+    hit4 = [(Aq - U * Fp2.const(g, z) if z != (1, 0) else Aq - U).is_zero() for z in _ZETA4]
+    sq1 = hit4[0] | hit4[1] | hit4[2] | hit4[3]
+    Zc = C["LB_SSWU_Z"]
+    z3 = _f2m(_f2m(Zc, Zc), Zc)
+    hit8, ys8 = [], []
+    u3y0 = (u.sqr() * u) * y0
+    for zeta in _ZETA8:
+        k = _f2sqrt(_f2m(z3, _f2inv(zeta)))
+        if k is None:
+            continue
+        hit8.append((Aq - U * Fp2.const(g, zeta)).is_zero())
+        ys8.append(u3y0 * Fp2.const(g, k))
+    # g(x1) a square: hit4[0] (y0 itself) or one of hit4[1:]; else the hit8 case
+    y = select(sq1, select_n([(h, y0 * Fp2.const(g, eta)) for h, eta in zip(hit4[1:], _ETA4[1:])], y0),
+               select_n([(h, yy) for h, yy in zip(hit8[1:], ys8[1:])], ys8[0]))
+    flip = fp2_sgn0(u) ^ fp2_sgn0(y)
+    y = select(flip, -y, y)
+    xn = select(sq1, n, tv1 * n)
+    return iso_map_g2_frac(xn, d, d2, d3, y)
+
+
+def iso_map_g2_frac(xn: Fp2, d: Fp2, d2: Fp2, d3: Fp2, y: Fp2) -> Proj:
+    """the 3-isogeny at x = xn / d: XN = xn(x) d^3, XD = xd(x) d^2, YN = yn(x) d^3,
+    YD = yd(x) d^3; x_E = XN / (XD d), y_E = y YN / YD, so
+    (X : Y : Z) = (XN YD : y YN XD d : XD d YD); a kernel point -> (0 : 1 : 0)."""
+    g = xn.g
+
+    def k(nm):
+        return c2(g, nm)
+    XN = ((k("LB_ISO_XNUM3") * xn + k("LB_ISO_XNUM2") * d) * xn + k("LB_ISO_XNUM1") * d2) * xn + \
+        k("LB_ISO_XNUM0") * d3
+    XD = (xn + k("LB_ISO_XDEN1") * d) * xn + k("LB_ISO_XDEN0") * d2
+    YN = ((k("LB_ISO_YNUM3") * xn + k("LB_ISO_YNUM2") * d) * xn + k("LB_ISO_YNUM1") * d2) * xn + \
+        k("LB_ISO_YNUM0") * d3
+    YD = ((xn + k("LB_ISO_YDEN2") * d) * xn + k("LB_ISO_YDEN1") * d2) * xn + k("LB_ISO_YDEN0") * d3
+    kern = XD.is_zero() | YD.is_zero()
+    XDd = XD * d
+    inf = Proj(Fp2.zero(g), Fp2.one(g), Fp2.zero(g))
+    return select(kern, inf, Proj(XN * YD, (y * YN) * XDd, XDd * YD))
+
+
 def map_to_curve_sswu(u: Fp2):
     """Simplified SWU onto E2' (bls_hash.h map_to_curve_sswu) with no inversion on
     its path: x1 = N / D is kept as a fraction, g(x1) = U / D^3 = W / m with
@@ -137,7 +309,9 @@ def map_to_curve_sswu(u: Fp2):
     return x, y
 
 
-def iso_map_g2(x: Fp2, y: Fp2) -> Jac:
+def iso_map_g2(x: Fp2, y: Fp2) -> Proj:
+    """3-isogeny E2' -> E2 on the affine SSWU output, to homogeneous coordinates:
+    (x yn-free) X = xn yd, Y = y yn xd, Z = xd yd; a kernel point -> (0 : 1 : 0)."""
     g = x.g
 
     def k(n):
@@ -149,17 +323,17 @@ def iso_map_g2(x: Fp2, y: Fp2) -> Jac:
     yd = ((x + k("LB_ISO_YDEN2")) * x + k("LB_ISO_YDEN1")) * x + k("LB_ISO_YDEN0")
     kern = xd.is_zero() | yd.is_zero()
     Z = xd * yd
-    yd2 = yd.sqr()
-    X = (xn * xd) * yd2
-    xd3 = xd.sqr() * xd
-    Y = ((y * yn) * xd3) * yd2
-    F = Ops(g, True)
-    return jsel(kern, jac_inf(F), Jac(X, Y, Z))
+    X = xn * yd
+    Y = (y * yn) * xd
+    inf = Proj(Fp2.zero(g), Fp2.one(g), Fp2.zero(g))
+    return select(kern, inf, Proj(X, Y, Z))
 
 
-def g2_psi(p: Jac) -> Jac:
+def g2_psi(p):
+    """psi(x, y) = (conj(x) cx, conj(y) cy): the same map on Jacobian and homogeneous
+    coordinates (conj(X) cx / conj(Z)^k for either weight k)"""
     g = p.X.g
-    return Jac(p.X.conj() * c2(g, "LB_PSI_CX"), p.Y.conj() * c2(g, "LB_PSI_CY"), p.Z.conj())
+    return type(p)(p.X.conj() * c2(g, "LB_PSI_CX"), p.Y.conj() * c2(g, "LB_PSI_CY"), p.Z.conj())
 
 
 def jac_mul_xabs(F: Ops, p: Jac, p_inf: Flag = None) -> Jac:
@@ -177,42 +351,43 @@ def jac_mul_xabs(F: Ops, p: Jac, p_inf: Flag = None) -> Jac:
     return jsel(p_inf, p, acc)
 
 
-def clear_cofactor_g2(p: Jac) -> Jac:
+def clear_cofactor_g2(p: Proj) -> Proj:
+    """RFC 9380 G.3 (h_eff via psi, bls_hash.h clear_cofactor_g2) with complete
+    homogeneous additions: A = [z]P, B = psi(P) - A, D = psi^2(2P) - P - B, h = D - [z]B"""
     F = Ops(p.X.g, True)
-    A = jac_mul_xabs(F, p)
-    B = jac_add(F, g2_psi(p), A.neg())
-    t = g2_psi(g2_psi(jac_dbl(F, p)))
-    t = jac_add(F, t, p.neg())
-    D = jac_add(F, t, B.neg())
-    t = jac_mul_xabs(F, B).neg()
-    return jac_add(F, D, t)
+    A = proj_mul_xabs(F, p)
+    B = proj_add(F, g2_psi(p), A.neg())
+    t = g2_psi(g2_psi(proj_dbl(F, p)))
+    t = proj_add(F, t, p.neg())
+    D = proj_add(F, t, B.neg())
+    C = proj_mul_xabs(F, B)
+    return proj_add(F, D, C.neg())
 
 
-def hash_to_g2(u0: Fp2, u1: Fp2) -> Jac:
-    q = []
-    for u in (u0, u1):
-        x, y = map_to_curve_sswu(u)
-        q.append(iso_map_g2(x, y))
+def hash_to_g2(u0: Fp2, u1: Fp2) -> Proj:
+    q = [map_to_curve_sswu_iso(u) for u in (u0, u1)]
     F = Ops(u0.g, True)
-    return clear_cofactor_g2(jac_add(F, q[0], q[1]))
+    return clear_cofactor_g2(proj_add(F, q[0], q[1]))
 
 
 # ---------------------------------------------------------------------------
 # subgroup checks (bls_curve.h)
 # ---------------------------------------------------------------------------
-def g2_in_subgroup(p: Jac, p_inf: Flag) -> Flag:
+def g2_in_subgroup(p: Proj, p_inf: Flag) -> Flag:
+    """psi(P) == [x]P (bls_curve.h g2_in_subgroup), complete homogeneous ladder"""
     F = Ops(p.X.g, True)
-    xp = jac_mul_xabs(F, p, p_inf).neg()
-    return p_inf | jac_eq(F, g2_psi(p), xp)
+    xp = proj_mul_xabs(F, p).neg()
+    return p_inf | proj_eq(F, g2_psi(p), xp)
 
 
 def g1_in_subgroup(p: Jac, p_inf: Flag) -> Flag:
+    """phi(P) == [x^2]P... as bls_curve.h g1_in_subgroup: beta X == -[|x|][|x|]P"""
     g = p.X.g
     F = Ops(g, False)
-    t = jac_mul_xabs(F, p, p_inf)
-    t = jac_mul_xabs(F, t).neg()
-    ph = Jac(p.X * g.const(C["LB_G1_BETA"]), p.Y, p.Z)
-    return p_inf | jac_eq(F, ph, t)
+    q = proj_from_jac(p)
+    t = proj_mul_xabs(F, proj_mul_xabs(F, q)).neg()
+    ph = Proj(q.X * g.const(C["LB_G1_BETA"]), q.Y, q.Z)
+    return p_inf | proj_eq(F, ph, t)
 
 
 # ---------------------------------------------------------------------------
@@ -315,15 +490,71 @@ def g1_line_point(p: Jac):
     return (p.X * p.Z, p.Y, p.Z.sqr() * p.Z)
 
 
-def g2_homogeneous(q: Jac):
-    """(X Z, Y, Z^3) of a Jacobian G2 point (affine: Zq None)"""
+def g2_homogeneous(q):
+    """(X Z, Y, Z^3) of a Jacobian G2 point (affine: Zq None); a homogeneous one as is"""
     g = q.X.g
+    if isinstance(q, Proj):
+        return (q.X, q.Y, q.Z)
     if q.Z.c0.t == g.one().t and not q.Z.c1.t:
         return (q.X, q.Y, None)
     return (q.X * q.Z, q.Y, q.Z.sqr() * q.Z)
 
 
-def miller2(pairs) -> Fp12:
+MILLER_GROUP = 1  # (> 1: the grouped f-chain; rows-bound at 32 rows, see DESIGN.md §7)
+
+
+def miller2(pairs, group: int = MILLER_GROUP) -> Fp12:
+    """miller2's value with a shorter f-chain: the Horner recurrence f <- f^2 S_t
+    (S_t the step's two lines multiplied, line_mul_line) is regrouped by `group`
+    consecutive steps, f_end = f_start^(2^d) M with M = the group's lines combined by
+    the same Horner rule -- computed beside the chain as the T-chains deliver the
+    lines.  The chain itself is then d squarings and ONE product per group (2 rounds
+    per squaring, 2 per product) instead of a squaring and a sparse product per step;
+    squaring distributes over the product, so the value is the same Fp12 element."""
+    if group <= 1:
+        return miller2_horner(pairs)
+    g = pairs[0][0].X.g
+    Ps = [g1_line_point(p) for p, _, _ in pairs]
+    Qs = [g2_homogeneous(q) for _, q, _ in pairs]
+    Ts = [(q[0], q[1], q[2] if q[2] is not None else Fp2.one(g)) for q in Qs]
+    # events (is_dbl, x, y1, y2) in loop order
+    events = []
+    for i in range(62, -1, -1):
+        lines = []
+        for k, (_, _, void) in enumerate(pairs):
+            Ts[k], ln = miller_dbl_step(Ts[k], Ps[k])
+            lines.append(unit_line(g, void, ln))
+        events.append((True,) + line_mul_line(*lines[0], *lines[1]))
+        if (X_ABS >> i) & 1:
+            lines = []
+            for k, (_, _, void) in enumerate(pairs):
+                Ts[k], ln = miller_add_step(Ts[k], Qs[k], Ps[k])
+                lines.append(unit_line(g, void, ln))
+            events.append((False,) + line_mul_line(*lines[0], *lines[1]))
+
+    def sparse(x, y1, y2):
+        return Fp12(x, Fp6(Fp2.zero(g), y1, y2))
+    # the first event starts f (f = 1 before it: its squaring is void)
+    f = sparse(*events[0][1:]).mat()
+    rest = events[1:]
+    for s0 in range(0, len(rest), group):
+        grp = rest[s0:s0 + group]
+        M, d = None, 0
+        for is_dbl, x, y1, y2 in grp:
+            if M is None:
+                M = sparse(x, y1, y2).mat()
+            elif is_dbl:
+                M = M.sqr().mat().mul_sparse2(x, y1, y2).mat()
+            else:
+                M = M.mul_sparse2(x, y1, y2).mat()
+            d += 1 if is_dbl else 0
+        for _ in range(d):
+            f = f.sqr().mat()
+        f = (f * M).mat()
+    return f.conj()
+
+
+def miller2_horner(pairs) -> Fp12:
     """prod over two pairs (P: Jacobian G1, Q: Jacobian G2, void) of f_{|x|,Q}(P),
     conjugated (x < 0), up to factors the final exponentiation kills.  A void pair
     (an infinite point) contributes unit lines."""
@@ -406,7 +637,7 @@ def set_program(single: bool) -> Graph:
     # Signature.fromBytes(validate=true): decompression / on-curve, G2 subgroup
     sx = Fp2(v["sx0"], v["sx1"])
     rhs = sx.sqr() * sx + c2(g, "LB_B2")
-    yc, sq = fp2_sqrt(rhs)
+    yc, sq = fp2_sqrt1(rhs)
     flip = fp2_lex_largest(yc) ^ fl["sig_sign"]
     yc = select(flip, -yc, yc)
     yu = Fp2(v["sy0"], v["sy1"])
@@ -416,7 +647,7 @@ def set_program(single: bool) -> Graph:
     on_curve = (comp & sq) | (~comp & on_u)
     sig_inf = fl["sig_inf"]
     sig = Jac(sx, sy, Fp2.one(g))
-    in_group = g2_in_subgroup(sig, sig_inf)
+    in_group = g2_in_subgroup(Proj(sx, sy, Fp2.one(g)), sig_inf)
     pk = Jac(v["pkX"], v["pkY"], v["pkZ"])
     pk_inf = g.is_zero(v["pkZ"])
     g1x = g.const(C["LB_G1_X"])

@@ -276,12 +276,31 @@ def compile_graph(g: Graph, rows: int = 64) -> Program:
     rounds: List[list] = []
     rnd = [-1] * N
     pending = {n: npred[n] for n in units}
+    def est_words(n):
+        """the unit's words in its round block (fixed record + extended record)"""
+        k = g.kind[n]
+        ops = _operands(k, g.args[n])
+        nfl = len(g.args[n][0]) if k == "sel" else 0
+        if len(ops) <= 2 and nfl <= 1 and all(len(op) <= INLINE_TERMS for op in ops) and \
+                (k != "sel" or len(ops) == 2):
+            return REC_WORDS
+        return REC_WORDS + 1 + nfl + sum(1 + len(op) for op in ops)
+
     while heap:
         cur = []
         deferred = []
+        used = 4
         while heap and len(cur) < rows:
-            _, n = heapq.heappop(heap)
-            cur.append(n)
+            item = heapq.heappop(heap)
+            w = est_words(item[1])
+            if used + w + 3 > BLOCK_CAP:  # (+3: the block's alignment)
+                deferred.append(item)
+                if len(deferred) > 4 * rows:
+                    break
+                continue
+            used += w
+            cur.append(item[1])
+        assert cur, "a unit larger than a round block"
         r = len(rounds)
         for n in cur:
             rnd[n] = r

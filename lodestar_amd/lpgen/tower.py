@@ -134,10 +134,27 @@ def select2(f: Flag, a: Fp2, b: Fp2) -> Fp2:
 # Fp exponentiations (fixed exponents, square-and-multiply with a window of 3
 # like bls_field.h fp_pow_p34: unrolled into the program)
 # ---------------------------------------------------------------------------
-def fp_pow(x: Fp, e: int, window: int = 3) -> Fp:
-    """x^e for a fixed exponent e > 0: left-to-right sliding window."""
+def fp_pow(x: Fp, e: int, window: int = 0) -> Fp:
+    """x^e for a fixed exponent e > 0.
+
+    Default (window 0): right-to-left, depth-optimal for round programs.  The
+    squaring chain x, x^2, x^4, ... runs one round per bit and the running
+    product takes x^(2^i) one round after it appears, so x^e is ready one round
+    after the top squaring: ~log2(e) rounds instead of log2(e) + the window
+    products of the left-to-right method (378 + 108 for (p-3)/4), at the price
+    of popcount(e) products instead of ~e.bit_length() / 4 (units in otherwise
+    idle rows).  window > 0: left-to-right sliding window (fewest products)."""
     if e == 0:
         return x.g.one()
+    if window == 0:
+        acc = None
+        s = x
+        for i in range(e.bit_length()):
+            if (e >> i) & 1:
+                acc = s if acc is None else acc * s
+            if i + 1 < e.bit_length():
+                s = s.sqr()
+        return acc
     bits = bin(e)[2:]
     odd = {1: x}
     if window > 1:
@@ -416,6 +433,10 @@ class Ops:
     def sel(self, f, a, b):
         return select(f, a, b)
 
+    def b3(self, a):
+        """3b times a, linear: b = 4 on E1, 4 (1 + u) on E2"""
+        return a.mul_xi().scale(12) if self.ext else a.scale(12)
+
 
 class Jac:
     __slots__ = ("X", "Y", "Z")
@@ -519,3 +540,88 @@ def jac_eq(F: Ops, p: Jac, q: Jac) -> Flag:
     both = pi & qi
     neither = ~pi & ~qi
     return both | (neither & ex & ey)
+
+
+# ---------------------------------------------------------------------------
+# Homogeneous projective points (x = X / Z, y = Y / Z) with the complete formulas
+# of Renes-Costello-Batina for a = 0 (Algorithms 7 and 9 of "Complete addition
+# formulas for prime order elliptic curves", 2016).  They have no exceptional
+# case on curves without 2-torsion -- E1(Fp) and E2'(Fp2) of BLS12-381 both have
+# odd order -- and every output coordinate has degree <= 4 in the inputs, so a
+# doubling or an addition takes TWO rounds (the one-lane Jacobian dbl-2009-l
+# takes three, madd four plus the selects of its exceptional cases).  3b enters
+# linearly (Ops.b3).  The group law is the same as the one-lane code's; the
+# representatives differ, which only the affine values (and the pairing, up to
+# factors the final exponentiation kills) ever see.
+# ---------------------------------------------------------------------------
+class Proj:
+    __slots__ = ("X", "Y", "Z")
+
+    def __init__(self, X, Y, Z):
+        self.X, self.Y, self.Z = X, Y, Z
+
+    def neg(self) -> "Proj":
+        return Proj(self.X, -self.Y, self.Z)
+
+
+def proj_from_jac(p: Jac) -> Proj:
+    """(X, Y, Z) Jacobian -> (X Z, Y, Z^3); infinity (Z = 0) -> (0, Y, 0)"""
+    return Proj(p.X * p.Z, p.Y, p.Z.sqr() * p.Z)
+
+
+def proj_to_jac(p: Proj) -> Jac:
+    """(X, Y, Z) homogeneous -> (X Z, Y Z^2, Z); infinity stays Z = 0"""
+    return Jac(p.X * p.Z, p.Y * p.Z.sqr(), p.Z)
+
+
+def proj_dbl(F: Ops, p: Proj) -> Proj:
+    """X3 = 2XY(Y^2 - 9bZ^2), Y3 = (Y^2 + 9bZ^2)^2 - 108 b^2 Z^4, Z3 = 8Y^3 Z"""
+    B = p.Y.sqr()
+    C = p.Z.sqr()
+    E = F.b3(C)
+    Fq = E.scale(3)
+    X3 = ((p.X * p.Y) * (B - Fq)).scale(2)
+    Y3 = (B + Fq).sqr() - E.sqr().scale(12)
+    Z3 = (B * (p.Y * p.Z)).scale(8)
+    return Proj(X3, Y3, Z3)
+
+
+def proj_add(F: Ops, p: Proj, q: Proj) -> Proj:
+    """complete addition (RCB Algorithm 7, a = 0): two rounds of products"""
+    t0 = p.X * q.X
+    t1 = p.Y * q.Y
+    t2 = p.Z * q.Z
+    t3 = (p.X + p.Y) * (q.X + q.Y) - t0 - t1
+    t4 = (p.Y + p.Z) * (q.Y + q.Z) - t1 - t2
+    y3 = (p.X + p.Z) * (q.X + q.Z) - t0 - t2
+    t0 = t0.scale(3)
+    t2 = F.b3(t2)
+    Z3 = t1 + t2
+    t1 = t1 - t2
+    y3 = F.b3(y3)
+    X3 = t3 * t1 - t4 * y3
+    Y3 = t1 * Z3 + y3 * t0
+    Z3 = Z3 * t4 + t0 * t3
+    return Proj(X3, Y3, Z3)
+
+
+def proj_mul_xabs(F: Ops, p: Proj) -> Proj:
+    """[|x|]P: 63 doublings and 5 additions, all complete (P = O gives O)"""
+    acc = p
+    for i in range(62, -1, -1):
+        acc = proj_dbl(F, acc)
+        if (X_ABS_T >> i) & 1:
+            acc = proj_add(F, acc, p)
+    return acc
+
+
+def proj_eq(F: Ops, p: Proj, q: Proj) -> Flag:
+    """equal points (both infinity, or X1 Z2 = X2 Z1 and Y1 Z2 = Y2 Z1 with Z != 0)"""
+    pi = F.is_zero(p.Z)
+    qi = F.is_zero(q.Z)
+    ex = F.is_zero(p.X * q.Z - q.X * p.Z)
+    ey = F.is_zero(p.Y * q.Z - q.Y * p.Z)
+    return (pi & qi) | (~pi & ~qi & ex & ey)
+
+
+X_ABS_T = 0xD201000000010000

@@ -118,3 +118,40 @@ def test_batch_scalar_in_g1():
     assert O.f12_is_one(O.final_exp(O.f12_mul(fs[0], fs[1])))
     bad = run_set(False, pks[1], msgs[0], sigs[1], 0x5555)[0]
     assert not O.f12_is_one(O.final_exp(O.f12_mul(fs[0], bad)))
+
+
+@functools.lru_cache(maxsize=None)
+def sswu_prog():
+    """map_to_curve_sswu_iso alone (u in, homogeneous (X : Y : Z) out)"""
+    from lodestar_amd.lpgen.dsl import Graph
+    from lodestar_amd.lpgen.tower import Fp2
+    g = Graph("sswu")
+    u = Fp2(g.input("u0"), g.input("u1"))
+    q = bls.map_to_curve_sswu_iso(u)
+    for nm, c in (("X", q.X), ("Y", q.Y), ("Z", q.Z)):
+        g.output(nm + "0", c.c0)
+        g.output(nm + "1", c.c1)
+    return lpc.compile_graph(g, rows=32)
+
+
+def test_sswu_iso_program_vs_oracle():
+    """the one-exponentiation SSWU + 3-isogeny (both square branches, the sign fix,
+    u = 0's exceptional x1, u in Fp) == the oracle's RFC 9380 map, point for point"""
+    import random
+    from tests.lp_helper import RINV
+    rnd = random.Random(5)
+    us = [(0, 0), (1, 0), (0, 1), (P - 1, 3)] + [(rnd.randrange(P), rnd.randrange(P)) for _ in range(16)]
+    us += list(O.hash_to_field_fp2(b"\x01" * 32, 2, O.DST_POP))
+    n_sq = 0
+    for u in us:
+        outs, _ = sswu_prog().run([mont(u[0]), mont(u[1])], [])
+        v = [x * RINV % P for x in outs]
+        X, Y, Z = (v[0], v[1]), (v[2], v[3]), (v[4], v[5])
+        ref = O.iso_map_g2(O.map_to_curve_sswu(u))
+        if ref is None:
+            assert O.f2_is_zero(Z)
+            continue
+        zi = O.f2_inv(Z)
+        assert (O.f2_mul(X, zi), O.f2_mul(Y, zi)) == ref, u
+        n_sq += 1
+    assert n_sq >= 20
