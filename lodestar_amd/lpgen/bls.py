@@ -594,15 +594,20 @@ def _gam(k):
 def fp12_exp_x(a: Fp12) -> Fp12:
     """a^x (x < 0) for cyclotomic a: 63 squarings, one round each -- every
     squaring consumes the previous one's output as forms over its products and
-    the materialized value before it, materialized meanwhile (cyc_sqr's lin)."""
-    acc = a
-    acc_mat = a
-    for i in range(62, -1, -1):
-        acc = acc.cyc_sqr(acc_mat)
-        acc_mat = acc.mat()
+    the materialized value before it, materialized meanwhile (cyc_sqr's lin).
+    Right to left: the five products by a^(2^i) (the set bits of |x| below the
+    top) run beside the squaring chain instead of inside it."""
+    s = a
+    s_mat = a
+    acc = None
+    top = X_ABS.bit_length() - 1
+    for i in range(top + 1):
         if (X_ABS >> i) & 1:
-            acc = acc_mat = (acc_mat * a).mat()
-    return acc_mat.conj()
+            acc = s_mat if acc is None else (acc * s_mat).mat()
+        if i < top:
+            s = s.cyc_sqr(s_mat)
+            s_mat = s.mat()
+    return acc.conj()
 
 
 def final_exp(f: Fp12) -> Fp12:
