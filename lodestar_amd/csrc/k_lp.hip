@@ -514,9 +514,10 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
     const uint32_t step = 1u << level;
     const uint32_t left = pos & ~(2 * step - 1);
     if (left + step >= n) continue;  // no right sibling: the value passes up unchanged
+    __threadfence();  // every wave: its stores of this workgroup's value (and set status) at L2
     __syncthreads();
     if (tid == 0) {
-      __threadfence();  // release this workgroup's value (and set status)
+      __threadfence();  // release
       sh_old = atomicAdd(c.cnt + (size_t)level * c.n_sets + base + left, 1u);
       __threadfence();
     }
