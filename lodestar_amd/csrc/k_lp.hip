@@ -127,7 +127,12 @@ LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_
   if (op == LB_LP_OP_INV) {
     // one lane of the row runs the binary-GCD inversion (bls_inv.h via fp_inv, which
     // works in the R = 2^384 form: R384^2 / c); the row multiplies by R416^3 / R384^2
+    // (the row's lanes exchange limbs through LDS inside the round: the stores of the
+    // other lanes must be done before lane 0 reads them, and lane 0's before the row
+    // reads the result -- a compiler barrier plus an LDS wait on each side; the
+    // compiler alone would hoist lane 0's loads above the row's store)
     S.reg[dst * 16u + lane] = c;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) {
       fp a, r;
 #pragma unroll
@@ -137,8 +142,9 @@ LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_
       for (int j = 0; j < 12; j++) S.reg[dst * 16u + j] = r.l[j];
       S.reg[dst * 16u + 12] = 0u;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const uint32_t ri = S.reg[dst * 16u + lane];
-    v = mont_mul<13>(ri, const_limb13(INV_FIX), pj);
+    v = canon(mont_mul<13>(ri, const_limb13(INV_FIX), pj), pj);  // canonical, as the executor's
     return false;
   }
   bool f;

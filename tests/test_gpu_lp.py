@@ -31,7 +31,7 @@ def rec(vals):
 
 
 def ints(a):
-    return [sum(int(x) << (32 * j) for j, x in enumerate(r[:12])) for r in a]
+    return [sum(int(x) << (32 * j) for j, x in enumerate(r[:13])) for r in a]  # 13 limbs: R = 2^416 values
 
 
 def run_both(dev, pid, name, cases):
