@@ -400,6 +400,16 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   c.req_err = d_req_err;
   c.n_sets = n_sets;
   LB_STAGE("lp_verify", 0, k_lp_verify, n_sets, LB_LP_TPB, c);
+  if (getenv("LB_LP_DUMP")) {  // debugging aid: set 0's program inputs, flags and Miller value on stderr
+    std::vector<uint32_t> h((size_t)LB_LP_NIN * 16 + LB_LP_NFL + 12 * 16);
+    LB_HIP(hipStreamSynchronize(sl.st[0]));
+    LB_HIP(hipMemcpy(h.data(), d_in16, LB_LP_NIN * 16 * 4, hipMemcpyDeviceToHost));
+    LB_HIP(hipMemcpy(h.data() + LB_LP_NIN * 16, d_fl, LB_LP_NFL * 4, hipMemcpyDeviceToHost));
+    LB_HIP(hipMemcpy(h.data() + LB_LP_NIN * 16 + LB_LP_NFL, d_F, 12 * 16 * 4, hipMemcpyDeviceToHost));
+    fprintf(stderr, "lb_lp_dump");
+    for (uint32_t w : h) fprintf(stderr, " %08x", w);
+    fprintf(stderr, "\n");
+  }
   PipeState& ps = sl.ps;
   ps = PipeState{};
   ps.n_req = n_req;

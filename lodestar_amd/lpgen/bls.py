@@ -677,7 +677,7 @@ def set_program(single: bool) -> Graph:
     void2 = sig_inf | p2_inf
     f = miller2([(P1, H, void1), (P2, sig, void2)])
     for k, x in enumerate(f.fps()):
-        g.output("f%d" % k, x)
+        g.output("f%d" % k, x, canonical=True)  # (the next program's inputs are canonical)
     g.output_flag("on_curve", on_curve)
     g.output_flag("in_group", in_group)
     if pk_ok is not None:
@@ -690,7 +690,7 @@ def mul_program() -> Graph:
     a = Fp12.from_fps([g.input_raw("a%d" % k) for k in range(12)])
     b = Fp12.from_fps([g.input_raw("b%d" % k) for k in range(12)])
     for k, x in enumerate((a * b).fps()):
-        g.output("f%d" % k, x)
+        g.output("f%d" % k, x, canonical=True)  # (the next program's inputs are canonical)
     return g
 
 

@@ -155,3 +155,23 @@ def test_sswu_iso_program_vs_oracle():
         assert (O.f2_mul(X, zi), O.f2_mul(Y, zi)) == ref, u
         n_sq += 1
     assert n_sq >= 20
+
+
+@pytest.mark.parametrize("single", [True, False])
+def test_set_then_mul_then_final_chain(single):
+    """the programs chained as k_lp_verify runs them: set outputs -> fp12_mul -> final_exp
+    (each program's outputs are canonical, the next one's inputs assume so)"""
+    pks, msgs, sigs = sample_sets(2)
+    outs = []
+    for k in range(2):
+        fps, flags = set_inputs(pks[k], msgs[k], sigs[k], 0x1234567890ABCDEF + k)
+        o, _ = prog("single" if single else "batch").run([mont(v) for v in fps], flags)
+        assert all(v < P for v in o)
+        outs.append(o)
+    if single:
+        for o in outs:
+            assert prog("final").run(o, [])[1] == [1]
+        return
+    prod, _ = prog("mul").run(outs[0] + outs[1], [])
+    assert all(v < P for v in prod)
+    assert prog("final").run(prod, [])[1] == [1]
