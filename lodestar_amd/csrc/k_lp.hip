@@ -273,9 +273,19 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     }
     __syncthreads();
   }
+  // the chunk loaded last round (in pw) into the ring first: its loads had a whole round
+  // to arrive, and this round's loads, issued after, are not waited for (a wait placed
+  // after them would expose a global-memory round trip in every round)
   const uint32_t pending = st.issued - st.done;  // words in pw
+#pragma unroll
+  for (int k = 0; k < PFW; k++) {
+    const uint32_t i = tid + k * LB_LP_TPB;
+    if (i < pending) S.ring[(st.done + i) & RMASK] = pw[k];
+  }
+  st.done += pending;
+  asm volatile("" ::: "memory");
   uint32_t n_new = 0;
-  if (st.issued < st.sw && st.issued + LB_LP_CHUNK <= st.cons + LB_LP_RING) {
+  if (st.issued < st.sw && st.issued + LB_LP_CHUNK <= cons_n + LB_LP_RING) {
     n_new = min((uint32_t)LB_LP_CHUNK, st.sw - st.issued);
 #pragma unroll
     for (int k = 0; k < PFW; k++) {
@@ -293,12 +303,6 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     load_desc(dn, S.ring, cons_n + 4 + RECW * row);
   }
   if (row < nu) run_unit(d, S, st.cons, lane, pj);
-#pragma unroll
-  for (int k = 0; k < PFW; k++) {
-    const uint32_t i = tid + k * LB_LP_TPB;
-    if (i < pending) S.ring[(st.done + i) & RMASK] = pw[k];
-  }
-  st.done += pending;
   st.issued += n_new;
   st.cons = cons_n;
   d = dn;
