@@ -503,13 +503,14 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
   if (tid == 0) {
     uint8_t st = c.sig_st[i];
     const bool sig_inf = c.flags[(size_t)i * LP_NFL] != 0;
-    if (st == LB_ST_OK) {
-      if (!ofl[0])
+    if (st == LB_ST_OK) {  // (the infinity encoding: no curve / subgroup test applies)
+      if (sig_inf) {
+        if (single) st = LB_ST_ZERO_SIGNATURE;
+      } else if (!ofl[0]) {
         st = LB_ST_NOT_ON_CURVE;
-      else if (!ofl[1])
+      } else if (!ofl[1]) {
         st = LB_ST_NOT_IN_GROUP;
-      else if (single && sig_inf)
-        st = LB_ST_ZERO_SIGNATURE;
+      }
     }
     c.sig_st[i] = st;
     uint8_t ps = c.pk_st[i];
