@@ -171,6 +171,7 @@ struct lb_ctx {
   // lp_max_sets sets): they never queue behind the calls in flight
   Slot slots[kMaxSlots + 1];
   Slot& prio() { return slots[n_slots]; }
+  int prio_cus = 0;  // CUs the throughput slots leave to the priority lane (LB_PRIO_CUS)
   int next_slot = 0;
   uint64_t next_ticket = 1;
   // the last tickets issued to two-phase calls: lb_verify_requests_finish accepts a
@@ -1086,11 +1087,30 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_SLOT0_STREAMS")) ctx->streams_per_slot[0] = atoi(e) == 1 ? 1 : 2;
   int prio_least = 0, prio_greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  // LB_PRIO_CUS=K: the throughput slots' streams leave K CUs (the highest-numbered) to the
+  // priority lane, so a latency-path call finds a free CU under load (a running
+  // workgroup is never preempted; a priority stream alone only reorders dispatch)
+  std::vector<uint32_t> cu_mask;
+  if (const char* e = getenv("LB_PRIO_CUS")) {
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const int k = atoi(e);
+    if (k > 0 && k < cus) {
+      cu_mask.assign((size_t)(cus + 31) / 32, 0u);
+      for (int c = 0; c < cus - k; c++) cu_mask[c / 32] |= 1u << (c % 32);
+      ctx->prio_cus = k;
+    }
+  }
   for (int s = 0; ok && s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
-    for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++)
-      ok = (s == ctx->n_slots ? hipStreamCreateWithPriority(&sl.st[i], hipStreamNonBlocking, prio_greatest)
-                              : hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking)) == hipSuccess;
+    for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++) {
+      if (s == ctx->n_slots)
+        ok = hipStreamCreateWithPriority(&sl.st[i], hipStreamNonBlocking, prio_greatest) == hipSuccess;
+      else if (!cu_mask.empty())
+        ok = hipExtStreamCreateWithCUMask(&sl.st[i], (uint32_t)cu_mask.size(), cu_mask.data()) == hipSuccess;
+      else
+        ok = hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking) == hipSuccess;
+    }
     if (ctx->streams_per_slot[s] == 1) sl.st[1] = sl.st[0];
     for (int i = 0; ok && i < 8; i++) ok = hipEventCreateWithFlags(&sl.dep[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < Slot::kMaxStages; i++)

@@ -52,6 +52,7 @@ FOPS = {"and": 0, "or": 1, "xor": 2, "not": 3, "const": 4}
 KIND_OP = {"mul": OP_MUL, "lin": OP_LIN, "sel": OP_SEL, "inv": OP_INV, "canon": OP_CANON, "iszero": OP_ISZERO,
            "bit0": OP_BIT0, "gthalf": OP_GTHALF, "fop": OP_FOP}
 FREE = ("in", "const", "inflag")
+_KIND_RANK = {"mul": 0, "lin": 1, "sel": 2, "canon": 3, "iszero": 4, "bit0": 4, "gthalf": 4, "inv": 5, "fop": 6}
 INV_WEIGHT = 80        # an inversion unit (one-lane binary GCD) costs ~ this many rounds
 BLOCK_CAP = 1024       # words of one round's block (bls_lp.h LB_LP_BLOCK_CAP)
 NINV_D = (1.0 / 436277739.0) * (1.0 - 2.0 ** -40)   # bls_coop.h reduce()
@@ -301,6 +302,10 @@ def compile_graph(g: Graph, rows: int = 64) -> Program:
             used += w
             cur.append(item[1])
         assert cur, "a unit larger than a round block"
+        # rows in kind order: a wave holds 4 consecutive rows, so a round's MUL units share
+        # their waves and the rarer kinds (LIN, SEL, predicates, extended records) theirs,
+        # instead of every wave running several code paths one after the other
+        cur.sort(key=lambda m: (_KIND_RANK.get(g.kind[m], 9), est_words(m) > REC_WORDS))
         r = len(rounds)
         for n in cur:
             rnd[n] = r
