@@ -363,13 +363,18 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
   uint32_t pa[PFW], pb[PFW];
 #pragma unroll
   for (int k = 0; k < PFW; k++) pa[k] = pb[k] = 0u;
-  uint32_t r = 0;
+  // one copy of the round in the loop (the double buffer swaps by register moves, not by
+  // unrolling: the round's code is most of the kernel's, and the instruction cache is 64 KB)
 #pragma unroll 1
-  for (; r + 1 < n_rounds; r += 2) {
+  for (uint32_t r = 0; r < n_rounds; r++) {
     lp_round(S, st, d, bw, nu, pa, pb, tid, lane, row, pj, stamps, r);
-    lp_round(S, st, d, bw, nu, pb, pa, tid, lane, row, pj, stamps, r + 1);
+#pragma unroll
+    for (int k = 0; k < PFW; k++) {
+      const uint32_t t = pa[k];
+      pa[k] = pb[k];
+      pb[k] = t;
+    }
   }
-  if (r < n_rounds) lp_round(S, st, d, bw, nu, pa, pb, tid, lane, row, pj, stamps, r);
   for (uint32_t i = row; i < n_out; i += LB_LP_ROWS) out[16 * i + lane] = lane < 13 ? S.reg[outs[i] * 16u + lane] : 0u;
   for (uint32_t i = tid; i < n_outflag; i += LB_LP_TPB) out_flags[i] = S.flag[outfl[i]];
 }
@@ -483,94 +488,118 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
 
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
   __shared__ LpShared S;
-  __shared__ uint32_t sh_old, sh_bad, sh_err;
+  __shared__ uint32_t sh_old, sh_bad, sh_err, s_fl[4];
   const uint32_t i = blockIdx.x, tid = threadIdx.x;
   if (i >= c.n_sets) return;
   const uint32_t k = c.set_req[i], base = c.req_off[k], n = c.req_off[k + 1] - base;
   const bool single = n == 1;
-  uint32_t ofl[3];
-  uint32_t* Fi = c.F + (size_t)i * 12 * 16;
-  // 1. the set program
-  {
-    __shared__ uint32_t s_ofl[4];
-    lp_run(S, single ? c.prog_single : c.prog_batch, c.in16 + (size_t)i * LP_NIN * 16, 0xffffffffu, nullptr,
-           c.flags + (size_t)i * LP_NFL, Fi, s_ofl);
+  // one interpreter call site, run per phase (the set program, each product of the
+  // tree, the final exponentiation): a single inlined copy of lp_run keeps the kernel's
+  // code a third of three copies'
+  enum { SET, TREE, FINAL };
+  int phase = SET;
+  const uint32_t* prog = single ? c.prog_single : c.prog_batch;
+  const uint32_t* in_a = c.in16 + (size_t)i * LP_NIN * 16;
+  const uint32_t* in_b = nullptr;
+  const uint32_t* in_fl = c.flags + (size_t)i * LP_NFL;
+  uint32_t split = 0xffffffffu;
+  uint32_t* out = c.F + (size_t)i * 12 * 16;
+  uint32_t pos = i - base, level = 0;
+  for (;;) {
+    lp_run(S, prog, in_a, split, in_b, in_fl, out, s_fl);
     __syncthreads();
-    ofl[0] = s_ofl[0];
-    ofl[1] = s_ofl[1];
-    ofl[2] = single ? s_ofl[2] : 1u;
-  }
-  if (tid == 0) {
-    uint8_t st = c.sig_st[i];
-    const bool sig_inf = c.flags[(size_t)i * LP_NFL] != 0;
-    if (st == LB_ST_OK) {  // (the infinity encoding: no curve / subgroup test applies)
-      if (sig_inf) {
-        if (single) st = LB_ST_ZERO_SIGNATURE;
-      } else if (!ofl[0]) {
-        st = LB_ST_NOT_ON_CURVE;
-      } else if (!ofl[1]) {
-        st = LB_ST_NOT_IN_GROUP;
+    if (phase == FINAL) {
+      if (tid == 0) {
+        c.valid[k] = s_fl[0] ? 1 : 0;
+        c.req_err[k] = (sh_err & 2u) ? LB_REQ_EMPTY_AGGREGATE : (sh_err & 1u) ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
       }
+      return;
     }
-    c.sig_st[i] = st;
-    uint8_t ps = c.pk_st[i];
-    if (ps == LB_ST_OK && !ofl[2]) ps = LB_ST_NOT_IN_GROUP;
-    c.pk_st[i] = ps;
-  }
-  // 2. the request's product tree: at level l the node of the positions
-  //    [q, q + 2^(l+1)) multiplies the values at q and q + 2^l; the second of
-  //    the two workgroups to arrive does it and continues upward
-  uint32_t pos = i - base;
-  for (uint32_t level = 0; (1u << level) < n; level++) {
-    const uint32_t step = 1u << level;
-    const uint32_t left = pos & ~(2 * step - 1);
-    if (left + step >= n) continue;  // no right sibling: the value passes up unchanged
-    __threadfence();  // every wave: its stores of this workgroup's value (and set status) at L2
+    if (phase == SET && tid == 0) {
+      uint8_t st = c.sig_st[i];
+      const bool sig_inf = c.flags[(size_t)i * LP_NFL] != 0;
+      if (st == LB_ST_OK) {  // (the infinity encoding: no curve / subgroup test applies)
+        if (sig_inf) {
+          if (single) st = LB_ST_ZERO_SIGNATURE;
+        } else if (!s_fl[0]) {
+          st = LB_ST_NOT_ON_CURVE;
+        } else if (!s_fl[1]) {
+          st = LB_ST_NOT_IN_GROUP;
+        }
+      }
+      c.sig_st[i] = st;
+      uint8_t ps = c.pk_st[i];
+      if (ps == LB_ST_OK && single && !s_fl[2]) ps = LB_ST_NOT_IN_GROUP;
+      c.pk_st[i] = ps;
+    }
+    // the request's product tree: at level l the node of the positions [q, q + 2^(l+1))
+    // multiplies the values at q and q + 2^l; the second of the two workgroups to
+    // arrive does it and continues upward
+    bool more = false;
+    for (; (1u << level) < n; level++) {
+      const uint32_t step = 1u << level;
+      const uint32_t left = pos & ~(2 * step - 1);
+      if (left + step >= n) continue;  // no right sibling: the value passes up unchanged
+      __threadfence();  // every wave: its stores of this workgroup's value (and set status) at L2
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence();  // release
+        sh_old = atomicAdd(c.cnt + (size_t)level * c.n_sets + base + left, 1u);
+        __threadfence();
+      }
+      __syncthreads();
+      if (sh_old == 0) return;  // the sibling's workgroup carries on
+      __threadfence();          // acquire the sibling's value
+      prog = c.prog_mul;
+      in_a = c.F + (size_t)(base + left) * 12 * 16;
+      in_b = c.F + (size_t)(base + left + step) * 12 * 16;
+      split = 12;
+      in_fl = nullptr;
+      out = const_cast<uint32_t*>(in_a);
+      pos = left;
+      level++;
+      more = true;
+      break;
+    }
+    if (more) {
+      phase = TREE;
+      continue;
+    }
+    // root: the request's statuses, then its final exponentiation
     __syncthreads();
+    __threadfence();
     if (tid == 0) {
-      __threadfence();  // release
-      sh_old = atomicAdd(c.cnt + (size_t)level * c.n_sets + base + left, 1u);
-      __threadfence();
+      sh_bad = 0;
+      sh_err = LB_REQ_OK;
     }
     __syncthreads();
-    if (sh_old == 0) return;  // the sibling's workgroup carries on
-    __threadfence();          // acquire the sibling's value
-    uint32_t* Fl = c.F + (size_t)(base + left) * 12 * 16;
-    const uint32_t* Fr = c.F + (size_t)(base + left + step) * 12 * 16;
-    lp_run(S, c.prog_mul, Fl, 12, Fr, nullptr, Fl, nullptr);
-    pos = left;
-  }
-  // 3. root: the request's verdict
-  __syncthreads();
-  __threadfence();
-  if (tid == 0) {
-    sh_bad = 0;
-    sh_err = LB_REQ_OK;
-  }
-  __syncthreads();
-  {
-    uint32_t bad = 0, empty = 0, badpk = 0;
-    for (uint32_t j = tid; j < n; j += LB_LP_TPB) {
-      const uint8_t ss = ((volatile uint8_t*)c.sig_st)[base + j], ps = ((volatile uint8_t*)c.pk_st)[base + j];
-      bad |= (ss != LB_ST_OK || ps != LB_ST_OK) ? 1u : 0u;
-      empty |= ps == LB_ST_EMPTY_AGGREGATE ? 1u : 0u;
-      badpk |= ps == LB_ST_BAD_ENCODING ? 1u : 0u;
+    {
+      uint32_t bad = 0, empty = 0, badpk = 0;
+      for (uint32_t j = tid; j < n; j += LB_LP_TPB) {
+        const uint8_t ss = ((volatile uint8_t*)c.sig_st)[base + j], ps = ((volatile uint8_t*)c.pk_st)[base + j];
+        bad |= (ss != LB_ST_OK || ps != LB_ST_OK) ? 1u : 0u;
+        empty |= ps == LB_ST_EMPTY_AGGREGATE ? 1u : 0u;
+        badpk |= ps == LB_ST_BAD_ENCODING ? 1u : 0u;
+      }
+      if (bad) atomicOr(&sh_bad, 1u);
+      if (empty) atomicOr(&sh_err, 2u);
+      if (badpk) atomicOr(&sh_err, 1u);
     }
-    if (bad) atomicOr(&sh_bad, 1u);
-    if (empty) atomicOr(&sh_err, 2u);
-    if (badpk) atomicOr(&sh_err, 1u);
-  }
-  __syncthreads();
-  uint32_t ok = 0;
-  if (!sh_bad) {
-    __shared__ uint32_t s_one;
-    lp_run(S, c.prog_final, c.F + (size_t)base * 12 * 16, 0xffffffffu, nullptr, nullptr, nullptr, &s_one);
     __syncthreads();
-    ok = s_one;
-  }
-  if (tid == 0) {
-    c.valid[k] = ok ? 1 : 0;
-    c.req_err[k] = (sh_err & 2u) ? LB_REQ_EMPTY_AGGREGATE : (sh_err & 1u) ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+    if (sh_bad) {
+      if (tid == 0) {
+        c.valid[k] = 0;
+        c.req_err[k] = (sh_err & 2u) ? LB_REQ_EMPTY_AGGREGATE : (sh_err & 1u) ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+      }
+      return;
+    }
+    phase = FINAL;
+    prog = c.prog_final;
+    in_a = c.F + (size_t)base * 12 * 16;
+    in_b = nullptr;
+    split = 0xffffffffu;
+    in_fl = nullptr;
+    out = nullptr;
   }
 }
 
