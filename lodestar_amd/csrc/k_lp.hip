@@ -55,28 +55,27 @@ LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
   }
 }
 
-// sum_t c_t v_t + K p -> normalized limbs (partials signed 64-bit per lane)
-LB_CO uint32_t finish_form(uint64_t Pa, uint64_t Na, bool neg, bool red, uint32_t pj) {
-  uint32_t r = neg ? norm<true>((int64_t)(Pa - Na)) : norm<false>((int64_t)Pa);
-  if (red) r = reduce(r, pj);
-  return r;
-}
-
 template <int B>
 LB_CO uint32_t inline_form(const Desc& d, const uint32_t (&v)[NT], uint32_t n, uint32_t K, bool neg, bool red,
                            uint32_t pj) {
   if (n == 1 && K == 0 && (d.w[B] >> 16) == 1u) return v[0];  // a plain register
-  uint64_t Pa = (uint64_t)K * pj, Na = 0;
+  // sum_t c_t v_t with ONE product per term: U = sum (uint32)c_t * v_t wraps by 2^32 v_t
+  // for each negative c_t, so S = U - 2^32 sum_{c_t < 0} v_t; the loop stops as soon as no
+  // row of the wave has a term left (most operands have 1-4 of the 8 slots)
+  uint64_t U = (uint64_t)K * pj, V = 0;
 #pragma unroll
   for (int t = 0; t < NT; t++) {
+    if (!__builtin_amdgcn_ballot_w64((uint32_t)t < n)) break;
     if ((uint32_t)t < n) {
       const int32_t c = (int32_t)d.w[B + t] >> 16;
-      const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
-      Pa += (uint64_t)cp * v[t];
-      Na += (uint64_t)cn * v[t];
+      U += (uint64_t)(uint32_t)c * v[t];
+      V += c < 0 ? (uint64_t)v[t] : 0ull;
     }
   }
-  return finish_form(Pa, Na, neg, red, pj);
+  const int64_t S = (int64_t)(U - (V << 32));
+  uint32_t r = neg ? norm<true>(S) : norm<false>(S);
+  if (red) r = reduce(r, pj);
+  return r;
 }
 
 // ---- extended records (forms over 8 terms, multi-way selects), read from the ring
@@ -93,22 +92,25 @@ LB_CO uint32_t ext_form(const Rec& rec, int& o, const uint32_t* __restrict__ reg
   const uint32_t K = hdr >> 16;
   const int t0 = o + 1;
   o += 1 + nt;
-  uint64_t Pa = (uint64_t)K * pj, Na = 0;
-  for (int t = 0; t < nt; t += 4) {
-    uint32_t x[4], v[4];
+  // 16 terms per LDS round trip (term words, then their registers), one product per term
+  uint64_t U = (uint64_t)K * pj, V = 0;
+  for (int t = 0; t < nt; t += 16) {
+    uint32_t x[16], v[16];
 #pragma unroll
-    for (int k = 0; k < 4; k++) x[k] = t + k < nt ? rec[t0 + t + k] : 0u;
+    for (int k = 0; k < 16; k++) x[k] = t + k < nt ? rec[t0 + t + k] : 0u;
 #pragma unroll
-    for (int k = 0; k < 4; k++) v[k] = reg[(x[k] & 0xffffu) * 16u + lane];
+    for (int k = 0; k < 16; k++) v[k] = reg[(x[k] & 0xffffu) * 16u + lane];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int32_t c = (int32_t)x[k] >> 16;
-      const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
-      Pa += (uint64_t)cp * v[k];
-      Na += (uint64_t)cn * v[k];
+    for (int k = 0; k < 16; k++) {
+      const int32_t c = (int32_t)x[k] >> 16;  // (0 for the padding: no contribution)
+      U += (uint64_t)(uint32_t)c * v[k];
+      V += c < 0 ? (uint64_t)v[k] : 0ull;
     }
   }
-  return finish_form(Pa, Na, neg, red, pj);
+  const int64_t S = (int64_t)(U - (V << 32));
+  uint32_t r = neg ? norm<true>(S) : norm<false>(S);
+  if (red) r = reduce(r, pj);
+  return r;
 }
 
 LB_CO void skip_form(const Rec& rec, int& o) { o += 1 + (int)(rec[o] & 255u); }
