@@ -77,31 +77,38 @@ LB_CO uint32_t halfp_limb() { return const_limb(HALF_P_LIMB); }
 // Signed per-limb partials -> 32-bit limbs.  t: this lane's partial (lanes 13-15
 // of the row 0); the row's value sum_j t_j 2^(32 j) must be >= 0 and < 2^416.
 // NEG: some partials may be negative (a linear form with negative terms, or
-// after subtracting q p).  One DPP shift moves each partial's high word up a
-// limb, leaving per-limb carries in {-1, 0, 1}; those resolve by lookahead:
-// one pass adds the +1 carries, one subtracts the -1 carries.
+// after subtracting q p).  One DPP shift moves each partial's high word (|h| <
+// 2^31) up a limb, leaving per-limb carries c in {-1, 0, 1}; a second shift adds
+// them.  A carry ripples further only where it meets a limb 0xffffffff (+1) or 0
+// (-1): one ballot detects that (probability ~2^-32 per limb on data) and only
+// then the carries resolve by lookahead (one pass adds the +1 carries, one
+// subtracts the -1 carries) -- the common case has no scalar round trip but the
+// one branch.
 template <bool NEG>
 LB_CO uint32_t norm(int64_t t) {
   const uint32_t lo = (uint32_t)t;
-  const uint64_t h = (uint64_t)(t >> 32);
-  const uint32_t hl = dpp<DPP_ROW_SHR1>((uint32_t)h);
-  const uint32_t hh = dpp<DPP_ROW_SHR1>((uint32_t)(h >> 32));
-  const int64_t u = (int64_t)(uint64_t)lo + (int64_t)(((uint64_t)hh << 32) | hl);
-  uint32_t v = (uint32_t)u;
+  const int32_t h = (int32_t)(t >> 32);
+  const int32_t hs = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)h);
+  const int64_t u = (int64_t)(uint64_t)lo + (int64_t)hs;
+  const uint32_t v = (uint32_t)u;
   const int32_t c = (int32_t)(u >> 32);
-  const uint32_t x = lanebit((ballot(c == 1) << 1) & ~ROW_LANE0);
+  const int32_t ci = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)c);  // carry into this limb (lane 0 of a row: 0)
+  const bool ripple = (ci == 1 && v == 0xffffffffu) || (NEG && ci == -1 && v == 0u);
+  if (__builtin_expect(ballot(ripple) == 0, 1)) return v + (uint32_t)ci;
+  uint32_t r = v;
   {
-    const uint64_t g = ballot(x && v == 0xffffffffu);
-    const uint64_t p = ballot(x ? v == 0xfffffffeu : v == 0xffffffffu);
-    v = v + x + lanebit(lookahead(g, p));
+    const uint32_t x = ci == 1 ? 1u : 0u;
+    const uint64_t g = ballot(x && r == 0xffffffffu);
+    const uint64_t p = ballot(x ? r == 0xfffffffeu : r == 0xffffffffu);
+    r = r + x + lanebit(lookahead(g, p));
   }
   if (NEG) {
-    const uint32_t y = lanebit((ballot(c == -1) << 1) & ~ROW_LANE0);
-    const uint64_t g = ballot(y && v == 0u);
-    const uint64_t p = ballot(y ? v == 1u : v == 0u);
-    v = v - y - lanebit(lookahead(g, p));
+    const uint32_t y = ci == -1 ? 1u : 0u;
+    const uint64_t g = ballot(y && r == 0u);
+    const uint64_t p = ballot(y ? r == 1u : r == 0u);
+    r = r - y - lanebit(lookahead(g, p));
   }
-  return v;
+  return r;
 }
 
 template <int I, int N>

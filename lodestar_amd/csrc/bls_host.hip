@@ -2398,7 +2398,7 @@ static int lp_program_run(lb_ctx* ctx, const uint32_t* d_prog, uint32_t n, uint3
   if (n_inflag) LB_HIP(hipMemcpyAsync(d_fl, in_flags, (fl_w - 1) * 4, hipMemcpyHostToDevice, ctx->stream));
   uint32_t* d_out = ws.take<uint32_t>(out_w);
   uint32_t* d_ofl = ws.take<uint32_t>(ofl_w);
-  unsigned long long* d_st = stamps ? ws.take<unsigned long long>(n_rounds + 1) : nullptr;
+  unsigned long long* d_st = stamps ? ws.take<unsigned long long>((size_t)(n_rounds + 1) * LB_LP_STAMPS) : nullptr;
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
@@ -2412,7 +2412,8 @@ static int lp_program_run(lb_ctx* ctx, const uint32_t* d_prog, uint32_t n, uint3
   LB_HIP(hipEventRecord(e1, ctx->stream));
   LB_HIP(hipMemcpyAsync(out16, d_out, out_w * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (n_outflag) LB_HIP(hipMemcpyAsync(out_flags, d_ofl, (ofl_w - 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
-  if (stamps) LB_HIP(hipMemcpyAsync(stamps, d_st, (size_t)n_rounds * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (stamps)
+    LB_HIP(hipMemcpyAsync(stamps, d_st, (size_t)n_rounds * LB_LP_STAMPS * 8, hipMemcpyDeviceToHost, ctx->stream));
   LB_HIP(hipStreamSynchronize(ctx->stream));
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, e0, e1);
@@ -2433,7 +2434,8 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
   const uint32_t* hw = prog_words ? prog_words : lb_lp_blob + LB_LP_PROGS[prog].off;
   const uint32_t n_rounds = hw[1], n_in = hw[5], n_inflag = hw[6], n_out = hw[7], n_outflag = hw[8];
   if ((n_inflag && !in_flags) || (n_outflag && !out_flags)) return LB_ERR_INVALID_ARGUMENT;
-  const size_t io = 4 * ((size_t)n * (n_in + n_out) * 16 + (size_t)n * (n_inflag + n_outflag) + 2) + 8 * (n_rounds + 1);
+  const size_t io = 4 * ((size_t)n * (n_in + n_out) * 16 + (size_t)n * (n_inflag + n_outflag) + 2) +
+                    8 * (size_t)(n_rounds + 1) * LB_LP_STAMPS;
   LB_TRY(ensure_ws(ctx, io + (prog_words ? 4 * n_words : 0) + 16384));
   Bump ws{ctx->slots[0].d_ws, 0, ctx->slots[0].ws_cap};
   const uint32_t* d_prog;

@@ -245,11 +245,19 @@ struct Stream {
 };
 
 // one round.  d / bw / nu: this round's record (row) and block header, prefetched;
-// the next round's are loaded into them.  pi: register chunk to issue into,
-// pw: the chunk issued last round.
-LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint32_t (&pi)[PFW],
-                    uint32_t (&pw)[PFW], uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
+// the next round's are loaded into them.  pf: the chunk issued last round (stored
+// into the ring first), then the chunk this round issues -- ONE register set: with a
+// double buffer swapped at the end of the round the compiler copies the fresh loads
+// right after issuing them, which waits out a global-memory round trip every round.
+LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint32_t (&pf)[PFW],
+                    uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
+  // stamps (diagnostic): LB_LP_STAMPS s_memtime points per round, lane 0 of the workgroup
+#define LB_LP_STAMP(k)                                                              \
+  do {                                                                             \
+    if (stamps && tid == 0) stamps[r * LB_LP_STAMPS + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  LB_LP_STAMP(0);
   const uint32_t cons_n = st.cons + bw;
   // the ring must hold the next round's block: catch up synchronously when the
   // prefetch ran dry (rare: it runs far ahead)
@@ -260,7 +268,7 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
 #pragma unroll
       for (int k = 0; k < PFW; k++) {
         const uint32_t i = tid + k * LB_LP_TPB;
-        if (i < n) S.ring[(st.done + i) & RMASK] = pw[k];
+        if (i < n) S.ring[(st.done + i) & RMASK] = pf[k];
       }
       st.done += n;
     } else {
@@ -275,24 +283,26 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     }
     __syncthreads();
   }
-  // the chunk loaded last round (in pw) into the ring first: its loads had a whole round
+  // the chunk loaded last round (in pf) into the ring first: its loads had a whole round
   // to arrive, and this round's loads, issued after, are not waited for (a wait placed
   // after them would expose a global-memory round trip in every round)
-  const uint32_t pending = st.issued - st.done;  // words in pw
+  LB_LP_STAMP(1);
+  const uint32_t pending = st.issued - st.done;  // words in pf
 #pragma unroll
   for (int k = 0; k < PFW; k++) {
     const uint32_t i = tid + k * LB_LP_TPB;
-    if (i < pending) S.ring[(st.done + i) & RMASK] = pw[k];
+    if (i < pending) S.ring[(st.done + i) & RMASK] = pf[k];
   }
   st.done += pending;
   asm volatile("" ::: "memory");
+  LB_LP_STAMP(2);
   uint32_t n_new = 0;
   if (st.issued < st.sw && st.issued + LB_LP_CHUNK <= cons_n + LB_LP_RING) {
     n_new = min((uint32_t)LB_LP_CHUNK, st.sw - st.issued);
 #pragma unroll
     for (int k = 0; k < PFW; k++) {
       const uint32_t i = tid + k * LB_LP_TPB;
-      pi[k] = i < n_new ? st.sp[st.issued + i] : 0u;
+      if (i < n_new) pf[k] = st.sp[st.issued + i];
     }
   }
   // the next round's header and this row's record (consumed after the barrier)
@@ -304,14 +314,19 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     nun = h.y;
     load_desc(dn, S.ring, cons_n + 4 + RECW * row);
   }
+  LB_LP_STAMP(3);
+  if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
   if (row < nu) run_unit(d, S, st.cons, lane, pj);
+  if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + LB_LP_TPB / 64 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+  LB_LP_STAMP(4);
   st.issued += n_new;
   st.cons = cons_n;
   d = dn;
   bw = bwn;
   nu = nun;
   __syncthreads();
-  if (stamps && tid == 0) stamps[r] = __builtin_amdgcn_s_memtime();
+  LB_LP_STAMP(5);
+#undef LB_LP_STAMP
 }
 
 }  // namespace
@@ -362,21 +377,13 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
     nu = h.y;
     load_desc(d, S.ring, 4 + RECW * row);
   }
-  uint32_t pa[PFW], pb[PFW];
+  uint32_t pf[PFW];
 #pragma unroll
-  for (int k = 0; k < PFW; k++) pa[k] = pb[k] = 0u;
-  // one copy of the round in the loop (the double buffer swaps by register moves, not by
-  // unrolling: the round's code is most of the kernel's, and the instruction cache is 64 KB)
+  for (int k = 0; k < PFW; k++) pf[k] = 0u;
+  // one copy of the round in the loop (the round's code is most of the kernel's, and the
+  // instruction cache is 64 KB)
 #pragma unroll 1
-  for (uint32_t r = 0; r < n_rounds; r++) {
-    lp_round(S, st, d, bw, nu, pa, pb, tid, lane, row, pj, stamps, r);
-#pragma unroll
-    for (int k = 0; k < PFW; k++) {
-      const uint32_t t = pa[k];
-      pa[k] = pb[k];
-      pb[k] = t;
-    }
-  }
+  for (uint32_t r = 0; r < n_rounds; r++) lp_round(S, st, d, bw, nu, pf, tid, lane, row, pj, stamps, r);
   for (uint32_t i = row; i < n_out; i += LB_LP_ROWS) out[16 * i + lane] = lane < 13 ? S.reg[outs[i] * 16u + lane] : 0u;
   for (uint32_t i = tid; i < n_outflag; i += LB_LP_TPB) out_flags[i] = S.flag[outfl[i]];
 }

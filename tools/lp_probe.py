@@ -56,6 +56,55 @@ def composition(words):
     return kinds
 
 
+def unit_features(words):
+    """per round, per unit: (op, ext, nx, ny, ext_terms) from the encoded blocks"""
+    n_rounds = words[1]
+    n_const, n_in, n_inflag, n_out, n_outflag = words[4:9]
+    boff = 10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag
+    out = []
+    for r in range(n_rounds):
+        bw, nu = words[boff], words[boff + 1]
+        us = []
+        for u in range(nu):
+            w0 = words[boff + 4 + 20 * u]
+            op = w0 & 15
+            if (w0 >> 18) & 1:
+                base = boff + words[boff + 4 + 20 * u + 2]
+                e0 = words[base]
+                op, nops, nfl = e0 & 15, (e0 >> 4) & 7, (e0 >> 7) & 7
+                o = base + 1 + nfl
+                ts = []
+                for _ in range(nops):
+                    ts.append(words[o] & 255)
+                    o += 1 + (words[o] & 255)
+                us.append((op, 1, 0, 0, tuple(ts)))
+            else:
+                us.append((op, 0, (w0 >> 4) & 31, (w0 >> 9) & 31, ()))
+        out.append(us)
+        boff += bw
+    return out
+
+
+def wave_table(feats, st):
+    """mean run_unit ticks of a wave by its content: key = (kinds present, max inline terms, ext terms)"""
+    nw = (st.shape[1] - 6) // 2
+    tab = {}
+    for r, us in enumerate(feats):
+        for w in range(nw):
+            mine = us[4 * w:4 * w + 4]
+            if not mine:
+                continue
+            dt = int(st[r, 6 + nw + w]) - int(st[r, 6 + w])
+            kinds = tuple(sorted({("ext%d" % u[0]) if u[1] else ("op%d" % u[0]) for u in mine}))
+            mt = max((max(u[2], u[3]) for u in mine if not u[1]), default=0)
+            et = max((sum(u[4]) for u in mine if u[1]), default=0)
+            key = "%s|t%d|e%d" % ("+".join(kinds), mt, (et + 7) // 8 * 8)
+            e = tab.setdefault(key, [0, 0])
+            e[0] += 1
+            e[1] += dt
+    return {k: {"n": v[0], "ticks": round(v[1] / v[0])} for k, v in sorted(tab.items(), key=lambda kv: -kv[1][0])}
+
+
 def main():
     dev = Device(0)
     out = {}
@@ -98,14 +147,30 @@ def main():
             if best is None or ms < best[0]:
                 best = (ms, st.copy())
         ms, st = best
-        d = np.diff(st.astype(np.int64))
+        st = st.astype(np.int64)
+        d = np.diff(st[:, 5])
+        # in-round segments: catch-up, ring store, issue + descriptor loads, run_unit, barrier; loop gap
+        seg = np.diff(st[:, :6], axis=1)
+        gap = st[1:, 0] - st[:-1, 5]
+        seg_names = ["catchup", "ring_store", "issue", "run_unit", "barrier"]
+        out[name + "_segments"] = {
+            "mean_ticks": {n: float(seg[:, k].mean()) for k, n in enumerate(seg_names)},
+            "median_ticks": {n: float(np.median(seg[:, k])) for k, n in enumerate(seg_names)},
+            "loop_gap_mean": float(gap.mean()),
+            "by_kind_mean": {kk: {n: float(seg[[i for i, x in enumerate(kinds) if x[0] == kk], k].mean())
+                                  for k, n in enumerate(seg_names)}
+                             for kk in sorted({x[0] for x in kinds})}}
+        print(name + "_segments", json.dumps(out[name + "_segments"]), flush=True)
+        out[name + "_waves"] = wave_table(unit_features(p.words), st)
+        for k, v in list(out[name + "_waves"].items())[:40]:
+            print("  wave", name, k, v, flush=True)
         summ = {}
         for (k, nu, bw), dt in zip(kinds[1:], d):
             s = summ.setdefault(k, [0, 0])
             s[0] += 1
             s[1] += int(dt)
         out[name] = {"rounds": p.n_rounds, "ms": ms, "us_per_round": 1000 * ms / p.n_rounds,
-                     "ticks_total": int(st[-1]) - int(st[0]),
+                     "ticks_total": int(st[-1, 5]) - int(st[0, 0]),
                      "by_kind": {k: {"rounds": v[0], "ticks": v[1], "ticks_per_round": v[1] / max(v[0], 1)}
                                  for k, v in summ.items()},
                      "slowest_rounds": [(int(i) + 1, kinds[int(i) + 1][0], int(d[i])) for i in np.argsort(d)[-8:]]}
