@@ -111,6 +111,26 @@ LB_CO uint32_t norm(int64_t t) {
   return r;
 }
 
+// two normalisations (signed partials) sharing the ripple test
+LB_CO void norm2(int64_t tx, int64_t ty, uint32_t& x, uint32_t& y) {
+  const int32_t hx = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)(int32_t)(tx >> 32));
+  const int32_t hy = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)(int32_t)(ty >> 32));
+  const int64_t ux = (int64_t)(uint64_t)(uint32_t)tx + (int64_t)hx;
+  const int64_t uy = (int64_t)(uint64_t)(uint32_t)ty + (int64_t)hy;
+  const uint32_t vx = (uint32_t)ux, vy = (uint32_t)uy;
+  const int32_t cx = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)(int32_t)(ux >> 32));
+  const int32_t cy = (int32_t)dpp<DPP_ROW_SHR1>((uint32_t)(int32_t)(uy >> 32));
+  const bool ripple = (cx == 1 && vx == 0xffffffffu) || (cx == -1 && vx == 0u) || (cy == 1 && vy == 0xffffffffu) ||
+                      (cy == -1 && vy == 0u);
+  if (__builtin_expect(ballot(ripple) == 0, 1)) {
+    x = vx + (uint32_t)cx;
+    y = vy + (uint32_t)cy;
+    return;
+  }
+  x = norm<true>(tx);
+  y = norm<true>(ty);
+}
+
 template <int I, int N>
 struct MontStep {
   LB_CO static void run(uint64_t& acc, uint32_t x, uint32_t y, uint32_t pj) {

@@ -10,8 +10,8 @@
 #define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
 #define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
 #define LB_LP_MAX_FLAGS 512
-#define LB_LP_STAMPS (6 + 2 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps):
-                                              // 6 of the workgroup, run_unit start / end of every wave
+#define LB_LP_STAMPS (6 + 6 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps): 6 of
+                                              // the workgroup, run_unit start / end of every wave, 4 inside its unit
 #define LB_LP_BLOCK_CAP 1024              // words of one round's encoded block
 #define LB_LP_RING 8192                   // LDS ring of the program stream (words, power of 2)
 #define LB_LP_CHUNK 1024                  // stream words fetched per round (2 per thread)

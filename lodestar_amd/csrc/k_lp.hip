@@ -55,27 +55,34 @@ LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
   }
 }
 
-template <int B>
-LB_CO uint32_t inline_form(const Desc& d, const uint32_t (&v)[NT], uint32_t n, uint32_t K, bool neg, bool red,
-                           uint32_t pj) {
-  if (n == 1 && K == 0 && (d.w[B] >> 16) == 1u) return v[0];  // a plain register
-  // sum_t c_t v_t with ONE product per term: U = sum (uint32)c_t * v_t wraps by 2^32 v_t
-  // for each negative c_t, so S = U - 2^32 sum_{c_t < 0} v_t; the loop stops as soon as no
-  // row of the wave has a term left (most operands have 1-4 of the 8 slots)
-  uint64_t U = (uint64_t)K * pj, V = 0;
+// Both operand forms of an inline record at once (one loop over the wave's longest
+// form, the two normalisations sharing their ripple test): x = sum_t c_t vx_t + Kx p,
+// y likewise; a form's unused terms have coefficient 0.  A wave whose rows all read
+// plain registers (one term, coefficient 1, K = 0) skips the arithmetic.
+LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[NT], uint32_t n, bool redx,
+                  bool redy, uint32_t pj, uint32_t& x, uint32_t& y) {
+  const uint32_t K = d.w[1];
+  const bool plain = n <= 1 && K == 0 && (d.w[3] >> 16) <= 1u && (d.w[11] >> 16) <= 1u;
+  if (!ballot(!plain)) {  // (coefficient 0: an absent form, value 0 -- not read)
+    x = vx[0];
+    y = vy[0];
+    return;
+  }
+  uint64_t Ux = (uint64_t)(K & 0xffffu) * pj, Vx = 0, Uy = (uint64_t)(K >> 16) * pj, Vy = 0;
 #pragma unroll
   for (int t = 0; t < NT; t++) {
-    if (!__builtin_amdgcn_ballot_w64((uint32_t)t < n)) break;
-    if ((uint32_t)t < n) {
-      const int32_t c = (int32_t)d.w[B + t] >> 16;
-      U += (uint64_t)(uint32_t)c * v[t];
-      V += c < 0 ? (uint64_t)v[t] : 0ull;
-    }
+    if (!ballot((uint32_t)t < n)) break;
+    const int32_t cx = (int32_t)d.w[3 + t] >> 16, cy = (int32_t)d.w[11 + t] >> 16;
+    Ux += (uint64_t)(uint32_t)cx * vx[t];
+    Vx += cx < 0 ? (uint64_t)vx[t] : 0ull;
+    Uy += (uint64_t)(uint32_t)cy * vy[t];
+    Vy += cy < 0 ? (uint64_t)vy[t] : 0ull;
   }
-  const int64_t S = (int64_t)(U - (V << 32));
-  uint32_t r = neg ? norm<true>(S) : norm<false>(S);
-  if (red) r = reduce(r, pj);
-  return r;
+  norm2((int64_t)(Ux - (Vx << 32)), (int64_t)(Uy - (Vy << 32)), x, y);
+  if (ballot(redx || redy)) {
+    if (redx) x = reduce(x, pj);
+    if (redy) y = reduce(y, pj);
+  }
 }
 
 // ---- extended records (forms over 8 terms, multi-way selects), read from the ring
@@ -184,7 +191,13 @@ LB_CO void ext_unit(const Rec& rec, LpShared& S, uint32_t lane, uint32_t pj) {
 }
 
 // one unit from its prefetched record; every lane of the row calls it
-LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, uint32_t pj) {
+LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, uint32_t pj,
+                    unsigned long long* ustamp = nullptr) {
+  // ustamp (diagnostic): s_memtime after the register reads / x form / y form / product
+#define LB_LP_USTAMP(k)                                                       \
+  do {                                                                        \
+    if (ustamp && (threadIdx.x & 63u) == 0) ustamp[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
   const uint32_t w0 = d.w[0];
   const uint32_t op = w0 & 15u, dst = w0 >> 19;
   if (op == LB_LP_OP_FOP) {
@@ -210,30 +223,33 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
     return;
   }
   const uint32_t nx = (w0 >> 4) & 31u, ny = (w0 >> 9) & 31u;
-  const bool negx = (w0 >> 14) & 1u, negy = (w0 >> 15) & 1u, redx = (w0 >> 16) & 1u, redy = (w0 >> 17) & 1u;
-  const uint32_t Kx = d.w[1] & 0xffffu, Ky = d.w[1] >> 16;
-  // every register read of both forms (and a select's flag) in one LDS round trip
+  const bool redx = (w0 >> 16) & 1u, redy = (w0 >> 17) & 1u;
+  // every register read of both forms in one LDS round trip, unconditionally: a record's
+  // unused term words are 0 (register 0, coefficient 0), so no lane masks or branches
   uint32_t vx[NT], vy[NT];
 #pragma unroll
-  for (int t = 0; t < NT; t++) vx[t] = (uint32_t)t < nx ? S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane] : 0u;
+  for (int t = 0; t < NT; t++) vx[t] = S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane];
 #pragma unroll
-  for (int t = 0; t < NT; t++) vy[t] = (uint32_t)t < ny ? S.reg[(d.w[11 + t] & 0xffffu) * 16u + lane] : 0u;
+  for (int t = 0; t < NT; t++) vy[t] = S.reg[(d.w[11 + t] & 0xffffu) * 16u + lane];
+  if (ustamp) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    LB_LP_USTAMP(0);
+  }
+  uint32_t x, y;
+  forms2(d, vx, vy, nx > ny ? nx : ny, redx, redy, pj, x, y);
+  LB_LP_USTAMP(1);
+  LB_LP_USTAMP(2);
   uint32_t v;
-  if (op == LB_LP_OP_SEL) {
-    if (S.flag[d.w[2]])
-      v = inline_form<3>(d, vx, nx, Kx, negx, redx, pj);
-    else
-      v = inline_form<11>(d, vy, ny, Ky, negy, redy, pj);
-  } else {
-    const uint32_t x = inline_form<3>(d, vx, nx, Kx, negx, redx, pj);
-    if (op == LB_LP_OP_MUL) {
-      const uint32_t y = inline_form<11>(d, vy, ny, Ky, negy, redy, pj);
-      v = mont_mul<13>(x, y, pj);
-    } else if (single_op(op, dst, x, S, lane, pj, v)) {
-      return;
-    }
+  if (op == LB_LP_OP_MUL) {
+    v = mont_mul<13>(x, y, pj);
+    LB_LP_USTAMP(3);
+  } else if (op == LB_LP_OP_SEL) {
+    v = S.flag[d.w[2]] ? x : y;
+  } else if (single_op(op, dst, x, S, lane, pj, v)) {
+    return;
   }
   S.reg[dst * 16u + lane] = v;
+#undef LB_LP_USTAMP
 }
 
 struct Stream {
@@ -316,7 +332,9 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   }
   LB_LP_STAMP(3);
   if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
-  if (row < nu) run_unit(d, S, st.cons, lane, pj);
+  if (row < nu)
+    run_unit(d, S, st.cons, lane, pj,
+             stamps ? stamps + r * LB_LP_STAMPS + 6 + 2 * LB_LP_TPB / 64 + 4 * (tid >> 6) : nullptr);
   if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + LB_LP_TPB / 64 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
   LB_LP_STAMP(4);
   st.issued += n_new;

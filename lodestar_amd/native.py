@@ -748,7 +748,7 @@ class Device:
         if not isinstance(prog, int):
             words = np.ascontiguousarray(np.array(prog, dtype=np.uint32))
         n_rounds = int(words[1]) if words is not None else 4096
-        st = np.zeros((n_rounds, 6 + 2 * 8), np.uint64) if stamps else None  # LB_LP_STAMPS points per round
+        st = np.zeros((n_rounds, 6 + 6 * 8), np.uint64) if stamps else None  # LB_LP_STAMPS points per round
         self._check(self.lib.lb_lp_program_run(self._h, 0 if words is not None else prog, _ptr(words),
                                                0 if words is None else words.size, n, _ptr(inputs), _ptr(fl),
                                                _ptr(out), _ptr(ofl) if n_outflag else None, ctypes.byref(ms),

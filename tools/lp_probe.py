@@ -87,7 +87,7 @@ def unit_features(words):
 
 def wave_table(feats, st):
     """mean run_unit ticks of a wave by its content: key = (kinds present, max inline terms, ext terms)"""
-    nw = (st.shape[1] - 6) // 2
+    nw = (st.shape[1] - 6) // 6
     tab = {}
     for r, us in enumerate(feats):
         for w in range(nw):
@@ -95,14 +95,22 @@ def wave_table(feats, st):
             if not mine:
                 continue
             dt = int(st[r, 6 + nw + w]) - int(st[r, 6 + w])
+            u0 = 6 + 2 * nw + 4 * w
+            inner = [int(st[r, u0 + k]) - int(st[r, 6 + w]) if st[r, u0 + k] else -1 for k in range(4)]
             kinds = tuple(sorted({("ext%d" % u[0]) if u[1] else ("op%d" % u[0]) for u in mine}))
             mt = max((max(u[2], u[3]) for u in mine if not u[1]), default=0)
             et = max((sum(u[4]) for u in mine if u[1]), default=0)
             key = "%s|t%d|e%d" % ("+".join(kinds), mt, (et + 7) // 8 * 8)
-            e = tab.setdefault(key, [0, 0])
+            e = tab.setdefault(key, [0, 0, [0, 0, 0, 0], [0, 0, 0, 0]])
             e[0] += 1
             e[1] += dt
-    return {k: {"n": v[0], "ticks": round(v[1] / v[0])} for k, v in sorted(tab.items(), key=lambda kv: -kv[1][0])}
+            for k in range(4):
+                if inner[k] >= 0:
+                    e[2][k] += inner[k]
+                    e[3][k] += 1
+    return {k: {"n": v[0], "ticks": round(v[1] / v[0]),
+                "regs_x_y_prod": [round(v[2][i] / v[3][i]) if v[3][i] else None for i in range(4)]}
+            for k, v in sorted(tab.items(), key=lambda kv: -kv[1][0])}
 
 
 def main():
