@@ -37,9 +37,14 @@ LB_DEV void sha256_init(uint32_t st[8]) {
 
 // w: 16 big-endian message words of one block
 LB_NOINL void sha256_compress(uint32_t st[8], const uint32_t win[16]) {
+  // fully unrolled: the schedule's ring w[] then lives in registers (a rolled loop
+  // indexes it dynamically, i.e. in scratch memory -- a memory round trip per round,
+  // which a lone set's k_lp_prep waits out 19 times 64)
   uint32_t w[16];
+#pragma unroll
   for (int i = 0; i < 16; i++) w[i] = win[i];
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
   for (int i = 0; i < 64; i++) {
     uint32_t wi;
     if (i < 16) {

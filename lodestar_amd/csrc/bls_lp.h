@@ -12,7 +12,7 @@
 #define LB_LP_MAX_FLAGS 512
 #define LB_LP_STAMPS (6 + 6 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps): 6 of
                                               // the workgroup, run_unit start / end of every wave, 4 inside its unit
-#define LB_LP_BLOCK_CAP 1024              // words of one round's encoded block
+#define LB_LP_BLOCK_CAP 1536              // words of one round's encoded block
 #define LB_LP_RING 8192                   // LDS ring of the program stream (words, power of 2)
 #define LB_LP_CHUNK 1024                  // stream words fetched per round (2 per thread)
 #define LB_LP_HDR 10                      // header words of an encoded program
@@ -27,6 +27,7 @@
 #define LB_LP_OP_BIT0 6
 #define LB_LP_OP_GTHALF 7
 #define LB_LP_OP_FOP 8
+#define LB_LP_OP_LIN2 9  // a linear form over both term lists of the record (x + y)
 
 // programs in the embedded blob (gen_lp.py -> lp_programs.bin, bls_lp_progs.h)
 #define LB_LP_PROG_SET_SINGLE 0

@@ -36,8 +36,9 @@ static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
 static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
 constexpr uint32_t RMASK = LB_LP_RING - 1;
 constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk
-constexpr int RECW = 20;                      // fixed unit record (lpgen/compile.py)
-constexpr int NT = 8;                         // inline terms per operand
+constexpr int NT = 12;                        // inline terms per operand
+constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
+constexpr int YT = 3 + NT;                    // first y term word
 static constexpr uint32_t INV_FIX[13] = LB_LP_INV_FIX_LIMBS;
 
 struct Desc {
@@ -58,11 +59,12 @@ LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
 // Both operand forms of an inline record at once (one loop over the wave's longest
 // form, the two normalisations sharing their ripple test): x = sum_t c_t vx_t + Kx p,
 // y likewise; a form's unused terms have coefficient 0.  A wave whose rows all read
-// plain registers (one term, coefficient 1, K = 0) skips the arithmetic.
-LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[NT], uint32_t n, bool redx,
-                  bool redy, uint32_t pj, uint32_t& x, uint32_t& y) {
+// plain registers (one term, coefficient 1, K = 0) skips the arithmetic.  LIN2 rows:
+// x = the form over both term lists.
+LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[NT], uint32_t n, bool lin2,
+                  bool redx, bool redy, uint32_t pj, uint32_t& x, uint32_t& y) {
   const uint32_t K = d.w[1];
-  const bool plain = n <= 1 && K == 0 && (d.w[3] >> 16) <= 1u && (d.w[11] >> 16) <= 1u;
+  const bool plain = n <= 1 && K == 0 && (d.w[3] >> 16) <= 1u && (d.w[YT] >> 16) <= 1u;
   if (!ballot(!plain)) {  // (coefficient 0: an absent form, value 0 -- not read)
     x = vx[0];
     y = vy[0];
@@ -72,13 +74,15 @@ LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[
 #pragma unroll
   for (int t = 0; t < NT; t++) {
     if (!ballot((uint32_t)t < n)) break;
-    const int32_t cx = (int32_t)d.w[3 + t] >> 16, cy = (int32_t)d.w[11 + t] >> 16;
+    const int32_t cx = (int32_t)d.w[3 + t] >> 16, cy = (int32_t)d.w[YT + t] >> 16;
     Ux += (uint64_t)(uint32_t)cx * vx[t];
     Vx += cx < 0 ? (uint64_t)vx[t] : 0ull;
     Uy += (uint64_t)(uint32_t)cy * vy[t];
     Vy += cy < 0 ? (uint64_t)vy[t] : 0ull;
   }
-  norm2((int64_t)(Ux - (Vx << 32)), (int64_t)(Uy - (Vy << 32)), x, y);
+  int64_t Sx = (int64_t)(Ux - (Vx << 32)), Sy = (int64_t)(Uy - (Vy << 32));
+  if (lin2) Sx += Sy;
+  norm2(Sx, Sy, x, y);
   if (ballot(redx || redy)) {
     if (redx) x = reduce(x, pj);
     if (redy) y = reduce(y, pj);
@@ -226,17 +230,27 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
   const bool redx = (w0 >> 16) & 1u, redy = (w0 >> 17) & 1u;
   // every register read of both forms in one LDS round trip, unconditionally: a record's
   // unused term words are 0 (register 0, coefficient 0), so no lane masks or branches
+  // (in tiers of 4 terms, each tier behind a wave-uniform test of the wave's longest form)
+  const uint32_t n = nx > ny ? nx : ny;
   uint32_t vx[NT], vy[NT];
 #pragma unroll
-  for (int t = 0; t < NT; t++) vx[t] = S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane];
+  for (int t = 0; t < NT; t++) vx[t] = vy[t] = 0u;
 #pragma unroll
-  for (int t = 0; t < NT; t++) vy[t] = S.reg[(d.w[11 + t] & 0xffffu) * 16u + lane];
+  for (int tier = 0; tier < NT / 4; tier++) {
+    if (tier > 0 && !ballot(n > 4u * tier)) break;
+#pragma unroll
+    for (int t = 4 * tier; t < 4 * tier + 4; t++) {
+      vx[t] = S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane];
+      vy[t] = S.reg[(d.w[YT + t] & 0xffffu) * 16u + lane];
+    }
+  }
   if (ustamp) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     LB_LP_USTAMP(0);
   }
   uint32_t x, y;
-  forms2(d, vx, vy, nx > ny ? nx : ny, redx, redy, pj, x, y);
+  const bool lin2 = op == LB_LP_OP_LIN2;
+  forms2(d, vx, vy, lin2 ? NT : n, lin2, redx, redy, pj, x, y);
   LB_LP_USTAMP(1);
   LB_LP_USTAMP(2);
   uint32_t v;
@@ -245,7 +259,7 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
     LB_LP_USTAMP(3);
   } else if (op == LB_LP_OP_SEL) {
     v = S.flag[d.w[2]] ? x : y;
-  } else if (single_op(op, dst, x, S, lane, pj, v)) {
+  } else if (single_op(lin2 ? LB_LP_OP_LIN : op, dst, x, S, lane, pj, v)) {
     return;
   }
   S.reg[dst * 16u + lane] = v;

@@ -45,16 +45,18 @@ from .dsl import B383, FLAG_KINDS, LIMIT, LIN_REDUCE, P, R, Graph
 
 MAGIC = 0x4C500003
 HDR_WORDS = 10
-REC_WORDS = 20
-INLINE_TERMS = 8
-OP_MUL, OP_LIN, OP_SEL, OP_INV, OP_CANON, OP_ISZERO, OP_BIT0, OP_GTHALF, OP_FOP = range(9)
+INLINE_TERMS = 12
+REC_WORDS = 4 + 2 * INLINE_TERMS  # w0, K, aux, x terms, y terms, pad
+OP_MUL, OP_LIN, OP_SEL, OP_INV, OP_CANON, OP_ISZERO, OP_BIT0, OP_GTHALF, OP_FOP, OP_LIN2 = range(10)
+# OP_LIN2: a linear unit whose form fills both term lists of the fixed record (x: the first
+# INLINE_TERMS terms, y: the rest; value = their sum), so forms of up to 2 INLINE_TERMS terms stay inline
 FOPS = {"and": 0, "or": 1, "xor": 2, "not": 3, "const": 4}
 KIND_OP = {"mul": OP_MUL, "lin": OP_LIN, "sel": OP_SEL, "inv": OP_INV, "canon": OP_CANON, "iszero": OP_ISZERO,
            "bit0": OP_BIT0, "gthalf": OP_GTHALF, "fop": OP_FOP}
 FREE = ("in", "const", "inflag")
 _KIND_RANK = {"mul": 0, "lin": 1, "sel": 2, "canon": 3, "iszero": 4, "bit0": 4, "gthalf": 4, "inv": 5, "fop": 6}
 INV_WEIGHT = 80        # an inversion unit (one-lane binary GCD) costs ~ this many rounds
-BLOCK_CAP = 1024       # words of one round's block (bls_lp.h LB_LP_BLOCK_CAP)
+BLOCK_CAP = 1536       # words of one round's block (bls_lp.h LB_LP_BLOCK_CAP)
 NINV_D = (1.0 / 436277739.0) * (1.0 - 2.0 ** -40)   # bls_coop.h reduce()
 PINV = (-pow(P, -1, R)) % R
 LIMB_MASK = (1 << 32) - 1
@@ -178,7 +180,9 @@ class Program:
         redx, redy = (w0 >> 16) & 1, (w0 >> 17) & 1
         Kx, Ky = w[o + 1] & 0xFFFF, w[o + 1] >> 16
         xt = w[o + 3:o + 3 + nx]
-        yt = w[o + 11:o + 11 + ny]
+        yt = w[o + 3 + INLINE_TERMS:o + 3 + INLINE_TERMS + ny]
+        if op == OP_LIN2:
+            return self._single(OP_LIN, dst, self._sum(xt + yt, Kx, redx, reg))
         if op == OP_SEL:
             if flg[w[o + 2]]:
                 return (0, dst, self._sum(xt, Kx, redx, reg))
@@ -284,6 +288,8 @@ def compile_graph(g: Graph, rows: int = 64) -> Program:
         nfl = len(g.args[n][0]) if k == "sel" else 0
         if len(ops) <= 2 and nfl <= 1 and all(len(op) <= INLINE_TERMS for op in ops) and \
                 (k != "sel" or len(ops) == 2):
+            return REC_WORDS
+        if k == "lin" and len(ops) == 1 and len(ops[0]) <= 2 * INLINE_TERMS:
             return REC_WORDS
         return REC_WORDS + 1 + nfl + sum(1 + len(op) for op in ops)
 
@@ -463,6 +469,12 @@ def _encode_unit(g: Graph, n: int, reg):
     else:
         forms = [_form_info(g, a[0], 0 if k in ("inv", "canon", "iszero", "bit0", "gthalf") else None)]
         flags = []
+    if k == "lin" and INLINE_TERMS < len(forms[0][0]) <= 2 * INLINE_TERMS:
+        terms, K, red, neg = forms[0]
+        xt = _term_words(terms[:INLINE_TERMS], reg)
+        yt = _term_words(terms[INLINE_TERMS:], reg)
+        w0 = OP_LIN2 | len(xt) << 4 | len(yt) << 9 | neg << 14 | red << 16 | dst << 19
+        return [w0, K, 0] + xt + yt + [0] * (INLINE_TERMS - len(yt)) + [0]
     inline = len(forms) <= 2 and len(flags) <= 1 and all(len(f[0]) <= INLINE_TERMS for f in forms) and \
         (k != "sel" or len(forms) == 2)
     if inline:
@@ -472,7 +484,8 @@ def _encode_unit(g: Graph, n: int, reg):
         xt = _term_words(fx[0], reg)
         yt = _term_words(fy[0], reg)
         aux = reg[flags[0]] if flags else 0
-        return [w0, fx[1] | fy[1] << 16, aux] + xt + [0] * (8 - len(xt)) + yt + [0] * (8 - len(yt)) + [0]
+        return [w0, fx[1] | fy[1] << 16, aux] + xt + [0] * (INLINE_TERMS - len(xt)) + yt + \
+            [0] * (INLINE_TERMS - len(yt)) + [0]
     # extended record
     assert len(forms) < 8 and len(flags) < 8
     ex = [op | len(forms) << 4 | len(flags) << 7 | dst << 16] + [reg[f] for f in flags]

@@ -152,6 +152,9 @@ def test_verify_by_index_matches_byte_path(tdev):
 def test_verify_by_index_merged_call_with_invalid(tdev, n_req):
     """>= 8 requests take the merged check; one injected invalid set must only
     fail its own request (the merged-failure fallback)."""
+    # (the merged check is the throughput pipeline's: a call this small would otherwise take
+    # the latency path, which checks each request on its own and never retries)
+    tdev.set_latency_path(0)
     base = _requests(tdev)[:2]
     reqs = [list(base[k % 2]) for k in range(n_req)]
     r = reqs[37]
@@ -167,6 +170,13 @@ def test_verify_by_index_merged_call_with_invalid(tdev, n_req):
     res = tdev.verify_requests(req_off, None, pk_off, msgs, blob, offs, bytes(32), pk_indices=idx)
     assert res.valid.all()
     assert (res.batch_retries, res.batch_sigs_success) == (0, int(req_off[-1]))
+    # the latency path: the same verdicts, no merged batch
+    tdev.set_latency_path(1024)
+    reqs[37][3] = (ix, hashlib.sha256(b"other").digest(), s)
+    req_off, idx, pk_off, msgs, blob, offs = _pack(reqs)
+    res = tdev.verify_requests(req_off, None, pk_off, msgs, blob, offs, bytes(32), pk_indices=idx)
+    assert [bool(v) for v in res.valid] == [k != 37 for k in range(n_req)]
+    assert res.batch_retries == 0
 
 
 def test_bls_gpu_verifier_index_keys():
