@@ -1097,7 +1097,14 @@ int lb_create(int device, lb_ctx** out_ctx) {
     const int k = atoi(e);
     if (k > 0 && k < cus) {
       cu_mask.assign((size_t)(cus + 31) / 32, 0u);
-      for (int c = 0; c < cus - k; c++) cu_mask[c / 32] |= 1u << (c % 32);
+      // LB_PRIO_SPREAD=1: the K reserved CUs evenly spaced over the CU ids (with contiguous
+      // ids per XCD, K/8 per XCD: no XCD left with fewer CUs for the throughput kernels)
+      const char* sp = getenv("LB_PRIO_SPREAD");
+      const bool spread = sp && atoi(sp) == 1;
+      std::vector<char> reserved((size_t)cus, 0);
+      for (int j = 0; j < k; j++) reserved[spread ? (size_t)((int64_t)(j + 1) * cus / k - 1) : (size_t)(cus - k + j)] = 1;
+      for (int c = 0; c < cus; c++)
+        if (!reserved[c]) cu_mask[c / 32] |= 1u << (c % 32);
       ctx->prio_cus = k;
     }
   }

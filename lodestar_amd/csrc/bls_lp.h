@@ -13,8 +13,9 @@
 #define LB_LP_STAMPS (6 + 6 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps): 6 of
                                               // the workgroup, run_unit start / end of every wave, 4 inside its unit
 #define LB_LP_BLOCK_CAP 1536              // words of one round's encoded block
-#define LB_LP_RING 8192                   // LDS ring of the program stream (words, power of 2)
-#define LB_LP_CHUNK 1024                  // stream words fetched per round (2 per thread)
+#define LB_LP_RING 16384                  // LDS ring of the program stream (words, power of 2)
+#define LB_LP_CHUNK 2048                  // stream words fetched per round (4 per thread; rounds average
+                                          // ~0.9k words, the final program ~1.04k)
 #define LB_LP_HDR 10                      // header words of an encoded program
 #define LB_LP_TREE_LEVELS 20              // product-tree levels (requests up to 2^20 sets)
 

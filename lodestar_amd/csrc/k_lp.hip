@@ -36,24 +36,45 @@ static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
 static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
 constexpr uint32_t RMASK = LB_LP_RING - 1;
 constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk
-constexpr int NT = 12;                        // inline terms per operand
+constexpr int NT = 16;                        // inline terms per operand
 constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
 constexpr int YT = 3 + NT;                    // first y term word
 static constexpr uint32_t INV_FIX[13] = LB_LP_INV_FIX_LIMBS;
 
+// A row's unit record, spread over the row: lane j holds words j, 16 + j and 32 + j;
+// a word reaches the whole row by a DPP broadcast (row_newbcast).  Every lane loading
+// all 36 words instead would move 9 KB per wave and round through the LDS.
 struct Desc {
-  uint32_t w[RECW];
-};
-
-LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
-#pragma unroll
-  for (int k = 0; k < RECW / 4; k++) {
-    const uint4 v = *reinterpret_cast<const uint4*>(ring + ((base + 4 * k) & RMASK));
-    d.w[4 * k] = v.x;
-    d.w[4 * k + 1] = v.y;
-    d.w[4 * k + 2] = v.z;
-    d.w[4 * k + 3] = v.w;
+  uint32_t v[3];
+  // word k of the record (k a constant after unrolling: the switch folds to one DPP)
+  LB_CO uint32_t w(int k) const {
+    const uint32_t x = v[k >> 4];
+    switch (k & 15) {
+      case 0: return bcast<0>(x);
+      case 1: return bcast<1>(x);
+      case 2: return bcast<2>(x);
+      case 3: return bcast<3>(x);
+      case 4: return bcast<4>(x);
+      case 5: return bcast<5>(x);
+      case 6: return bcast<6>(x);
+      case 7: return bcast<7>(x);
+      case 8: return bcast<8>(x);
+      case 9: return bcast<9>(x);
+      case 10: return bcast<10>(x);
+      case 11: return bcast<11>(x);
+      case 12: return bcast<12>(x);
+      case 13: return bcast<13>(x);
+      case 14: return bcast<14>(x);
+      default: return bcast<15>(x);
+    }
   }
+};
+static_assert(RECW <= 48, "a record spans three words per lane");
+
+LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base, uint32_t lane) {
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    d.v[k] = 16u * k + lane < (uint32_t)RECW ? ring[(base + 16u * k + lane) & RMASK] : 0u;
 }
 
 // Both operand forms of an inline record at once (one loop over the wave's longest
@@ -61,10 +82,10 @@ LB_CO void load_desc(Desc& d, const uint32_t* ring, uint32_t base) {
 // y likewise; a form's unused terms have coefficient 0.  A wave whose rows all read
 // plain registers (one term, coefficient 1, K = 0) skips the arithmetic.  LIN2 rows:
 // x = the form over both term lists.
-LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[NT], uint32_t n, bool lin2,
-                  bool redx, bool redy, uint32_t pj, uint32_t& x, uint32_t& y) {
-  const uint32_t K = d.w[1];
-  const bool plain = n <= 1 && K == 0 && (d.w[3] >> 16) <= 1u && (d.w[YT] >> 16) <= 1u;
+LB_CO void forms2(uint32_t K, const uint32_t (&tx)[NT], const uint32_t (&ty)[NT], const uint32_t (&vx)[NT],
+                  const uint32_t (&vy)[NT], uint32_t n, bool lin2, bool redx, bool redy, uint32_t pj, uint32_t& x,
+                  uint32_t& y) {
+  const bool plain = n <= 1 && K == 0 && (tx[0] >> 16) <= 1u && (ty[0] >> 16) <= 1u;
   if (!ballot(!plain)) {  // (coefficient 0: an absent form, value 0 -- not read)
     x = vx[0];
     y = vy[0];
@@ -74,7 +95,7 @@ LB_CO void forms2(const Desc& d, const uint32_t (&vx)[NT], const uint32_t (&vy)[
 #pragma unroll
   for (int t = 0; t < NT; t++) {
     if (!ballot((uint32_t)t < n)) break;
-    const int32_t cx = (int32_t)d.w[3 + t] >> 16, cy = (int32_t)d.w[YT + t] >> 16;
+    const int32_t cx = (int32_t)tx[t] >> 16, cy = (int32_t)ty[t] >> 16;
     Ux += (uint64_t)(uint32_t)cx * vx[t];
     Vx += cx < 0 ? (uint64_t)vx[t] : 0ull;
     Uy += (uint64_t)(uint32_t)cy * vy[t];
@@ -202,11 +223,12 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
   do {                                                                        \
     if (ustamp && (threadIdx.x & 63u) == 0) ustamp[k] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-  const uint32_t w0 = d.w[0];
+  const uint32_t w0 = d.w(0);
   const uint32_t op = w0 & 15u, dst = w0 >> 19;
+  const uint32_t aux = d.w(2);  // (a DPP broadcast: read with the whole row active)
   if (op == LB_LP_OP_FOP) {
     if (lane == 0) {
-      const uint32_t x = d.w[2], fop = x & 7u, f1 = (x >> 3) & 0x1fffu, f2 = x >> 16;
+      const uint32_t x = aux, fop = x & 7u, f1 = (x >> 3) & 0x1fffu, f2 = x >> 16;
       uint32_t v;
       if (fop == 0)
         v = S.flag[f1] & S.flag[f2];
@@ -223,7 +245,7 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
     return;
   }
   if ((w0 >> 18) & 1u) {
-    ext_unit(Rec{S.ring, cons + d.w[2]}, S, lane, pj);
+    ext_unit(Rec{S.ring, cons + aux}, S, lane, pj);
     return;
   }
   const uint32_t nx = (w0 >> 4) & 31u, ny = (w0 >> 9) & 31u;
@@ -232,16 +254,18 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
   // unused term words are 0 (register 0, coefficient 0), so no lane masks or branches
   // (in tiers of 4 terms, each tier behind a wave-uniform test of the wave's longest form)
   const uint32_t n = nx > ny ? nx : ny;
-  uint32_t vx[NT], vy[NT];
+  uint32_t tx[NT], ty[NT], vx[NT], vy[NT];
 #pragma unroll
-  for (int t = 0; t < NT; t++) vx[t] = vy[t] = 0u;
+  for (int t = 0; t < NT; t++) tx[t] = ty[t] = vx[t] = vy[t] = 0u;
 #pragma unroll
   for (int tier = 0; tier < NT / 4; tier++) {
     if (tier > 0 && !ballot(n > 4u * tier)) break;
 #pragma unroll
     for (int t = 4 * tier; t < 4 * tier + 4; t++) {
-      vx[t] = S.reg[(d.w[3 + t] & 0xffffu) * 16u + lane];
-      vy[t] = S.reg[(d.w[YT + t] & 0xffffu) * 16u + lane];
+      tx[t] = d.w(3 + t);
+      ty[t] = d.w(YT + t);
+      vx[t] = S.reg[(tx[t] & 0xffffu) * 16u + lane];
+      vy[t] = S.reg[(ty[t] & 0xffffu) * 16u + lane];
     }
   }
   if (ustamp) {
@@ -250,7 +274,7 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
   }
   uint32_t x, y;
   const bool lin2 = op == LB_LP_OP_LIN2;
-  forms2(d, vx, vy, lin2 ? NT : n, lin2, redx, redy, pj, x, y);
+  forms2(d.w(1), tx, ty, vx, vy, lin2 ? NT : n, lin2, redx, redy, pj, x, y);
   LB_LP_USTAMP(1);
   LB_LP_USTAMP(2);
   uint32_t v;
@@ -258,7 +282,7 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
     v = mont_mul<13>(x, y, pj);
     LB_LP_USTAMP(3);
   } else if (op == LB_LP_OP_SEL) {
-    v = S.flag[d.w[2]] ? x : y;
+    v = S.flag[aux] ? x : y;
   } else if (single_op(lin2 ? LB_LP_OP_LIN : op, dst, x, S, lane, pj, v)) {
     return;
   }
@@ -342,7 +366,7 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     const uint4 h = *reinterpret_cast<const uint4*>(S.ring + (cons_n & RMASK));
     bwn = h.x;
     nun = h.y;
-    load_desc(dn, S.ring, cons_n + 4 + RECW * row);
+    load_desc(dn, S.ring, cons_n + 4 + RECW * row, lane);
   }
   LB_LP_STAMP(3);
   if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
@@ -407,7 +431,7 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
     const uint4 h = *reinterpret_cast<const uint4*>(S.ring);
     bw = h.x;
     nu = h.y;
-    load_desc(d, S.ring, 4 + RECW * row);
+    load_desc(d, S.ring, 4 + RECW * row, lane);
   }
   uint32_t pf[PFW];
 #pragma unroll

@@ -45,7 +45,7 @@ from .dsl import B383, FLAG_KINDS, LIMIT, LIN_REDUCE, P, R, Graph
 
 MAGIC = 0x4C500003
 HDR_WORDS = 10
-INLINE_TERMS = 12
+INLINE_TERMS = 16
 REC_WORDS = 4 + 2 * INLINE_TERMS  # w0, K, aux, x terms, y terms, pad
 OP_MUL, OP_LIN, OP_SEL, OP_INV, OP_CANON, OP_ISZERO, OP_BIT0, OP_GTHALF, OP_FOP, OP_LIN2 = range(10)
 # OP_LIN2: a linear unit whose form fills both term lists of the fixed record (x: the first
