@@ -216,5 +216,113 @@ LB_CO bool row_gt_half(uint32_t c) {
 // lowest bit of the row's value
 LB_CO uint32_t row_bit0(uint32_t v) { return bcast<0>(v) & 1u; }
 
+// ---- inversion (the latency path's INV unit) --------------------------------
+// y^-1 mod p for a raw y in [0, p) held by ONE row of the wave (its lanes 0-11; 0 -> 0),
+// by the binary GCD of bls_inv.h (Pornin, ePrint 2020/972, Alg. 2 with k = 31): 25
+// rounds of 31 divsteps on 64-bit approximations of (a, b), then the step matrix
+// applied to the full a, b, u, v.  Here the divsteps run on scalar registers (the
+// approximations are read out of the row: uniform values) and the matrix products
+// run across the row (one limb per lane, norm for the carries) -- a one-lane
+// inversion's 381-bit limb loops were ~90% of its ~150 us.  base: the row's first
+// lane (wave-uniform); lanes of other rows compute on zeros and keep their values.
+LB_CO uint32_t row_readlane(uint32_t v, uint32_t lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane); }
+
+// (x f + y g) / 2^31 for x, y >= 0 (< 2^381) and |f| + |g| <= 2^31: |result|, sign
+LB_CO uint32_t row_lin_shift(uint32_t x, uint32_t y, int64_t f, int64_t g, bool mine, uint32_t base, bool& neg) {
+  const uint32_t j = lane16();
+  // t + 2^413 >= 0: the bias keeps the normalised value non-negative (|t| < 2^412)
+  int64_t t = mine ? (int64_t)(uint64_t)x * f + (int64_t)(uint64_t)y * g : 0;
+  if (mine && j == 12) t += 1ll << 29;
+  uint32_t v = norm<true>(t);
+  neg = row_readlane(v, base + 12) < (1u << 29);
+  if (neg) {  // |t| = 2^413 - (t + 2^413)
+    const int64_t d = mine ? (j == 12 ? (int64_t)(1u << 29) : 0) - (int64_t)(uint64_t)v : 0;
+    v = norm<true>(d);
+  } else if (j == 12) {
+    v -= 1u << 29;
+  }
+  const uint32_t up = dpp<DPP_ROW_SHL1>(v);  // limb j + 1 (lane 15: 0)
+  return (v >> 31) | (up << 1);
+}
+
+// (u f + v g) / 2^31 mod p for u, v in [0, p), |f| + |g| <= 2^31 (canonical result).
+// |t| = |u f + v g| < 2^31 p: t + 2^414 normalises (the bias on lane 12, where u, v
+// are 0, so no lane's partial leaves int64), then the bias becomes 2^32 p (t + 2^32 p
+// > 0, = t mod p after / 2^31), then + k p with k = -t p^-1 mod 2^31 makes the sum
+// divisible by 2^31: (t + (2^32 + k) p) / 2^31 in (p, 4 p).
+LB_CO uint32_t row_lin_mod(uint32_t u, uint32_t v, int64_t f, int64_t g, bool mine, uint32_t base, uint32_t pj) {
+  const uint32_t j = lane16();
+  int64_t t = mine ? (int64_t)(uint64_t)u * f + (int64_t)(uint64_t)v * g : 0;
+  if (mine && j == 12) t += 1ll << 30;
+  const uint32_t n0 = norm<true>(t);
+  const uint32_t p_below = dpp<DPP_ROW_SHR1>(pj);  // p_{j-1}: the limbs of 2^32 p
+  const int64_t t1 = mine ? (int64_t)(uint64_t)n0 + (int64_t)(uint64_t)p_below - (j == 12 ? (1ll << 30) : 0) : 0;
+  const uint32_t n1 = norm<true>(t1);
+  const uint32_t k = (row_readlane(n1, base) * N0) & 0x7fffffffu;
+  const uint64_t t2 = mine ? (uint64_t)n1 + (uint64_t)k * pj : 0ull;
+  const uint32_t n2 = norm<false>((int64_t)t2);
+  const uint32_t up = dpp<DPP_ROW_SHL1>(n2);
+  const uint32_t w = (n2 >> 31) | (up << 1);
+  return canon(w, pj);
+}
+
+LB_CO uint32_t row_inv_raw(uint32_t y, bool mine, uint32_t base, uint32_t pj) {
+  const uint32_t j = lane16();
+  uint32_t a = mine ? y : 0u, b = mine ? pj : 0u, u = mine && j == 0 ? 1u : 0u, v = 0u;
+#pragma unroll 1
+  for (int round = 0; round < 25; round++) {
+    // n = bit length of max(a, b) (at least 64); the approximations' words, read out
+    const uint64_t nz = ballot((a | b) != 0u) >> base;
+    const uint32_t top = (nz & 0xfffull) ? 63u - (uint32_t)__builtin_clzll(nz & 0xfffull) : 0u;
+    const uint32_t wt = row_readlane(a | b, base + top);
+    int n = wt ? (int)(32 * top + 32 - __builtin_clz(wt)) : 0;
+    if (n < 64) n = 64;
+    const int s = n - 33, li = s >> 5, sh = s & 31;
+    auto approx = [&](uint32_t x) {
+      const uint32_t w0 = row_readlane(x, base + li), w1 = row_readlane(x, base + li + 1);
+      const uint32_t w2 = li + 2 < 12 ? row_readlane(x, base + li + 2) : 0u;
+      const uint64_t lo64 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+      uint64_t tp = sh ? ((lo64 >> sh) | ((uint64_t)w2 << (64 - sh))) : lo64;
+      tp &= (1ull << 33) - 1;
+      return (uint64_t)(row_readlane(x, base) & 0x7fffffffu) | (tp << 31);
+    };
+    uint64_t xa = approx(a), xb = approx(b);
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 1
+    for (int i = 0; i < 31; i++) {
+      const bool odd = (xa & 1u) != 0;
+      const bool sw = odd && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xa = odd ? (ta - tb) >> 1 : ta >> 1;
+      xb = tb;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      f1 = tf1 * 2;
+      g1 = tg1 * 2;
+    }
+    bool an, bn;
+    const uint32_t na = row_lin_shift(a, b, f0, g0, mine, base, an);
+    const uint32_t nb = row_lin_shift(a, b, f1, g1, mine, base, bn);
+    if (an) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (bn) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    const uint32_t nu = row_lin_mod(u, v, f0, g0, mine, base, pj);
+    const uint32_t nv = row_lin_mod(u, v, f1, g1, mine, base, pj);
+    if (mine) {
+      a = na;
+      b = nb;
+      u = nu;
+      v = nv;
+    }
+  }
+  return v;  // b = gcd(y, p) = 1 for y != 0, and then v = y^-1
+}
+
 }  // namespace co
 }  // namespace lb

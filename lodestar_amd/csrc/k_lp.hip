@@ -39,7 +39,7 @@ constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chu
 constexpr int NT = 16;                        // inline terms per operand
 constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
 constexpr int YT = 3 + NT;                    // first y term word
-static constexpr uint32_t INV_FIX[13] = LB_LP_INV_FIX_LIMBS;
+static constexpr uint32_t INV_FIX_RAW[13] = LB_LP_INV_FIX_RAW_LIMBS;
 
 // A row's unit record, spread over the row: lane j holds words j, 16 + j and 32 + j;
 // a word reaches the whole row by a DPP broadcast (row_newbcast).  Every lane loading
@@ -159,26 +159,16 @@ LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_
     return false;
   }
   if (op == LB_LP_OP_INV) {
-    // one lane of the row runs the binary-GCD inversion (bls_inv.h via fp_inv, which
-    // works in the R = 2^384 form: R384^2 / c); the row multiplies by R416^3 / R384^2
-    // (the row's lanes exchange limbs through LDS inside the round: the stores of the
-    // other lanes must be done before lane 0 reads them, and lane 0's before the row
-    // reads the result -- a compiler barrier plus an LDS wait on each side; the
-    // compiler alone would hoist lane 0's loads above the row's store)
-    S.reg[dst * 16u + lane] = c;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      fp a, r;
-#pragma unroll
-      for (int j = 0; j < 12; j++) a.l[j] = S.reg[dst * 16u + j];
-      fp_inv(r, a);
-#pragma unroll
-      for (int j = 0; j < 12; j++) S.reg[dst * 16u + j] = r.l[j];
-      S.reg[dst * 16u + 12] = 0u;
+    // the row-cooperative binary GCD (bls_coop.h row_inv_raw), one INV row of the wave
+    // after the other (its divsteps run on scalar registers: one row at a time)
+    uint32_t r = 0;
+    for (uint64_t m = ballot(lane == 0); m; m &= m - 1) {
+      const uint32_t base = (uint32_t)__builtin_ctzll(m);
+      const bool mine = (lane64() & ~15u) == base;
+      const uint32_t ri = row_inv_raw(c, mine, base, pj);
+      if (mine) r = ri;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint32_t ri = S.reg[dst * 16u + lane];
-    v = canon(mont_mul<13>(ri, const_limb13(INV_FIX), pj), pj);  // canonical, as the executor's
+    v = canon(mont_mul<13>(r, const_limb13(INV_FIX_RAW), pj), pj);  // canonical, as the executor's
     return false;
   }
   bool f;

@@ -17,6 +17,7 @@ using namespace lb::co;
 //       out = norm(T) (13 limbs), out2 = reduce(T)
 // op 3: out = canon(a); aux_out[item*4 + 0..2] = is_zero, gt_half(canon(from_mont... raw)), bit0
 // op 4: out = a - b (borrow lookahead), aux_out[item*4] = a >= b
+// op 5: out = a^-1 mod p (row_inv_raw; raw a < p); cyc[item] = ticks of the wave's inversions
 __global__ void k_coop(int op, uint32_t n, uint32_t k, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                        const uint32_t* __restrict__ c, const uint32_t* __restrict__ d, const int32_t* __restrict__ aux,
                        uint32_t* __restrict__ out, uint32_t* __restrict__ out2, uint32_t* __restrict__ aux_out,
@@ -68,6 +69,19 @@ __global__ void k_coop(int op, uint32_t n, uint32_t k, const uint32_t* __restric
     bool ge;
     out[o] = sub_cmp(va, b[o], ge);
     if (j == 0) aux_out[item * 4] = ge;
+  } else if (op == 5) {
+    // out = a^-1 mod p (raw a < p, 0 -> 0): every row of the wave, one after the other
+    uint32_t r = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (uint64_t m = ballot(j == 0); m; m &= m - 1) {
+      const uint32_t base = (uint32_t)__builtin_ctzll(m);
+      const bool mine = (lane64() & ~15u) == base;
+      const uint32_t ri = row_inv_raw(va, mine, base, pj);
+      if (mine) r = ri;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[o] = r;
+    if (j == 0) cyc[item] = t1 - t0;
   }
 }
 

@@ -135,3 +135,13 @@ def test_sub_cmp(lib):
     for x, y, o, f in zip(a, b, ints(out), aux_out):
         assert int(f[0]) == (x >= y)
         assert o == (x - y) % (1 << 512)
+
+
+def test_row_inversion(lib):
+    """row_inv_raw (the latency path's INV unit): random values, 0, 1, p - 1, small and
+    large powers of two; four rows of a wave invert one after the other."""
+    vals = sample(60, 21, P) + [0, 1, P - 1, 2, 1 << 380, P - 2, (1 << 255) + 7, 3]
+    out, _, _, cyc, ms = call(lib, 5, rows(vals))
+    for x, o in zip(vals, ints(out)):
+        assert o == (pow(x, -1, P) if x else 0), hex(x)
+    print(f"\nrow inversion: {float(np.median(cyc)):.0f} s_memtime ticks per wave (4 rows), {ms:.3f} ms")
