@@ -2435,7 +2435,7 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
                       float* out_ms, uint64_t* stamps) {
   if (!ctx || n == 0 || !in16 || !out16) return LB_ERR_INVALID_ARGUMENT;
   if (!prog_words && prog >= LB_LP_NPROGS) return LB_ERR_INVALID_ARGUMENT;
-  if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500003u)) return LB_ERR_INVALID_ARGUMENT;
+  if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500004u)) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(helper_slot(ctx));
   const uint32_t* hw = prog_words ? prog_words : lb_lp_blob + LB_LP_PROGS[prog].off;

@@ -35,7 +35,8 @@ struct LpShared {
 static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
 static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
 constexpr uint32_t RMASK = LB_LP_RING - 1;
-constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk
+constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk (one 16-byte load)
+static_assert(PFW == 4, "one uint4 of the stream per thread and chunk");
 constexpr int NT = 16;                        // inline terms per operand
 constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
 constexpr int YT = 3 + NT;                    // first y term word
@@ -293,7 +294,7 @@ struct Stream {
 // into the ring first), then the chunk this round issues -- ONE register set: with a
 // double buffer swapped at the end of the round the compiler copies the fresh loads
 // right after issuing them, which waits out a global-memory round trip every round.
-LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint32_t (&pf)[PFW],
+LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
                     uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
   // stamps (diagnostic): LB_LP_STAMPS s_memtime points per round, lane 0 of the workgroup
@@ -309,19 +310,13 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   while (st.done < need) {
     const uint32_t n = min((uint32_t)LB_LP_CHUNK, st.issued - st.done);
     if (n) {
-#pragma unroll
-      for (int k = 0; k < PFW; k++) {
-        const uint32_t i = tid + k * LB_LP_TPB;
-        if (i < n) S.ring[(st.done + i) & RMASK] = pf[k];
-      }
+      if (4u * tid < n) *reinterpret_cast<uint4*>(&S.ring[(st.done + 4u * tid) & RMASK]) = pf;
       st.done += n;
     } else {
       const uint32_t m = min((uint32_t)LB_LP_CHUNK, st.sw - st.done);
-#pragma unroll
-      for (int k = 0; k < PFW; k++) {
-        const uint32_t i = tid + k * LB_LP_TPB;
-        if (i < m) S.ring[(st.done + i) & RMASK] = st.sp[st.done + i];
-      }
+      if (4u * tid < m)
+        *reinterpret_cast<uint4*>(&S.ring[(st.done + 4u * tid) & RMASK]) =
+            *reinterpret_cast<const uint4*>(st.sp + st.done + 4u * tid);
       st.done += m;
       st.issued = st.done;
     }
@@ -329,25 +324,19 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   }
   // the chunk loaded last round (in pf) into the ring first: its loads had a whole round
   // to arrive, and this round's loads, issued after, are not waited for (a wait placed
-  // after them would expose a global-memory round trip in every round)
+  // after them would expose a global-memory round trip in every round).  Stream words
+  // move 4 per thread: one 16-byte global load and one ds_write_b128 (the stream starts
+  // 16-byte aligned and every block is a multiple of 4 words: lpgen/compile.py)
   LB_LP_STAMP(1);
   const uint32_t pending = st.issued - st.done;  // words in pf
-#pragma unroll
-  for (int k = 0; k < PFW; k++) {
-    const uint32_t i = tid + k * LB_LP_TPB;
-    if (i < pending) S.ring[(st.done + i) & RMASK] = pf[k];
-  }
+  if (4u * tid < pending) *reinterpret_cast<uint4*>(&S.ring[(st.done + 4u * tid) & RMASK]) = pf;
   st.done += pending;
   asm volatile("" ::: "memory");
   LB_LP_STAMP(2);
   uint32_t n_new = 0;
   if (st.issued < st.sw && st.issued + LB_LP_CHUNK <= cons_n + LB_LP_RING) {
     n_new = min((uint32_t)LB_LP_CHUNK, st.sw - st.issued);
-#pragma unroll
-    for (int k = 0; k < PFW; k++) {
-      const uint32_t i = tid + k * LB_LP_TPB;
-      if (i < n_new) pf[k] = st.sp[st.issued + i];
-    }
+    if (4u * tid < n_new) pf = *reinterpret_cast<const uint4*>(st.sp + st.issued + 4u * tid);
   }
   // the next round's header and this row's record (consumed after the barrier)
   Desc dn;
@@ -410,6 +399,7 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
   pos += n_out;
   const uint32_t* outfl = prog + pos;
   pos += n_outflag;
+  pos = (pos + 3u) & ~3u;  // (the stream starts 16-byte aligned)
   st.sp = prog + pos;
   st.cons = 0;
   st.done = st.issued = min(st.sw, (uint32_t)(LB_LP_RING - LB_LP_CHUNK));
@@ -423,9 +413,7 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
     nu = h.y;
     load_desc(d, S.ring, 4 + RECW * row, lane);
   }
-  uint32_t pf[PFW];
-#pragma unroll
-  for (int k = 0; k < PFW; k++) pf[k] = 0u;
+  uint4 pf = make_uint4(0u, 0u, 0u, 0u);
   // one copy of the round in the loop (the round's code is most of the kernel's, and the
   // instruction cache is 64 KB)
 #pragma unroll 1

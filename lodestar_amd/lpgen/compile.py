@@ -43,7 +43,7 @@ from typing import Dict, List
 
 from .dsl import B383, FLAG_KINDS, LIMIT, LIN_REDUCE, P, R, Graph
 
-MAGIC = 0x4C500003
+MAGIC = 0x4C500004
 HDR_WORDS = 10
 INLINE_TERMS = 16
 REC_WORDS = 4 + 2 * INLINE_TERMS  # w0, K, aux, x terms, y terms, pad
@@ -130,6 +130,7 @@ class Program:
         pos += n_out
         outfl = w[pos:pos + n_outflag]
         pos += n_outflag
+        pos = (pos + 3) & ~3
         assert pos + sw == len(w)
         boff = pos
         for r in range(n_rounds):
@@ -385,6 +386,7 @@ def compile_graph(g: Graph, rows: int = 64) -> Program:
     words += [reg[n] for _, n in inflag_nodes]
     words += [reg[n] for _, n in g.outs]
     words += [reg[n] for _, n in g.outflags]
+    words += [0] * (-len(words) % 4)  # the stream starts 16-byte aligned (the device loads it 16 B at a time)
     stream0 = len(words)
     max_terms = 0
     max_block = 0

@@ -38,11 +38,11 @@ def chain(kind, n, width=1):
 def composition(words):
     n_rounds = words[1]
     n_const, n_in, n_inflag, n_out, n_outflag = words[4:9]
-    boff = 10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag
+    boff = (10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag + 3) & ~3
     kinds = []
     for r in range(n_rounds):
         bw, nu = words[boff], words[boff + 1]
-        ops = {words[boff + 4 + 20 * u] & 15 for u in range(nu)}
+        ops = {words[boff + 4 + lpc.REC_WORDS * u] & 15 for u in range(nu)}
         boff += bw
         if 3 in ops:
             k = "inv"
@@ -60,16 +60,16 @@ def unit_features(words):
     """per round, per unit: (op, ext, nx, ny, ext_terms) from the encoded blocks"""
     n_rounds = words[1]
     n_const, n_in, n_inflag, n_out, n_outflag = words[4:9]
-    boff = 10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag
+    boff = (10 + 14 * n_const + n_in + n_inflag + n_out + n_outflag + 3) & ~3
     out = []
     for r in range(n_rounds):
         bw, nu = words[boff], words[boff + 1]
         us = []
         for u in range(nu):
-            w0 = words[boff + 4 + 20 * u]
+            w0 = words[boff + 4 + lpc.REC_WORDS * u]
             op = w0 & 15
             if (w0 >> 18) & 1:
-                base = boff + words[boff + 4 + 20 * u + 2]
+                base = boff + words[boff + 4 + lpc.REC_WORDS * u + 2]
                 e0 = words[base]
                 op, nops, nfl = e0 & 15, (e0 >> 4) & 7, (e0 >> 7) & 7
                 o = base + 1 + nfl
