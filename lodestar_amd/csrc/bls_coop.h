@@ -226,44 +226,66 @@ LB_CO uint32_t row_bit0(uint32_t v) { return bcast<0>(v) & 1u; }
 // inversion's 381-bit limb loops were ~90% of its ~150 us.  base: the row's first
 // lane (wave-uniform); lanes of other rows compute on zeros and keep their values.
 LB_CO uint32_t row_readlane(uint32_t v, uint32_t lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane); }
-
-// (x f + y g) / 2^31 for x, y >= 0 (< 2^381) and |f| + |g| <= 2^31: |result|, sign
-LB_CO uint32_t row_lin_shift(uint32_t x, uint32_t y, int64_t f, int64_t g, bool mine, uint32_t base, bool& neg) {
-  const uint32_t j = lane16();
-  // t + 2^413 >= 0: the bias keeps the normalised value non-negative (|t| < 2^412)
-  int64_t t = mine ? (int64_t)(uint64_t)x * f + (int64_t)(uint64_t)y * g : 0;
-  if (mine && j == 12) t += 1ll << 29;
-  uint32_t v = norm<true>(t);
-  neg = row_readlane(v, base + 12) < (1u << 29);
-  if (neg) {  // |t| = 2^413 - (t + 2^413)
-    const int64_t d = mine ? (j == 12 ? (int64_t)(1u << 29) : 0) - (int64_t)(uint64_t)v : 0;
-    v = norm<true>(d);
-  } else if (j == 12) {
-    v -= 1u << 29;
-  }
-  const uint32_t up = dpp<DPP_ROW_SHL1>(v);  // limb j + 1 (lane 15: 0)
-  return (v >> 31) | (up << 1);
+// a < b for wave-uniform 64-bit values, on the scalar unit (the borrow of a - b)
+LB_CO bool s_lt64(uint64_t a, uint64_t b) {
+  uint32_t r, t;
+  asm("s_cmp_lt_u32 %2, %4\n\ts_subb_u32 %1, %3, %5\n\ts_cselect_b32 %0, 1, 0"
+      : "=s"(r), "=&s"(t)
+      : "s"((uint32_t)a), "s"((uint32_t)(a >> 32)), "s"((uint32_t)b), "s"((uint32_t)(b >> 32))
+      : "scc");
+  return r != 0;
 }
 
-// (u f + v g) / 2^31 mod p for u, v in [0, p), |f| + |g| <= 2^31 (canonical result).
-// |t| = |u f + v g| < 2^31 p: t + 2^414 normalises (the bias on lane 12, where u, v
-// are 0, so no lane's partial leaves int64), then the bias becomes 2^32 p (t + 2^32 p
-// > 0, = t mod p after / 2^31), then + k p with k = -t p^-1 mod 2^31 makes the sum
-// divisible by 2^31: (t + (2^32 + k) p) / 2^31 in (p, 4 p).
-LB_CO uint32_t row_lin_mod(uint32_t u, uint32_t v, int64_t f, int64_t g, bool mine, uint32_t base, uint32_t pj) {
+// The two new (a, b) = (|x f0 + y g0|, |x f1 + y g1|) / 2^31 for x, y >= 0 (< 2^381)
+// and |f| + |g| <= 2^31, with their signs; both at once (shared normalisations).
+// t + 2^413 >= 0: the bias (on lane 12, where x, y are 0) keeps the normalised value
+// non-negative (|t| < 2^412); a negative t comes back as 2^413 - (t + 2^413).
+LB_CO void row_lin_shift2(uint32_t x, uint32_t y, int64_t f0, int64_t g0, int64_t f1, int64_t g1, bool mine,
+                          uint32_t base, uint32_t& ra, uint32_t& rb, bool& na, bool& nb) {
   const uint32_t j = lane16();
-  int64_t t = mine ? (int64_t)(uint64_t)u * f + (int64_t)(uint64_t)v * g : 0;
-  if (mine && j == 12) t += 1ll << 30;
-  const uint32_t n0 = norm<true>(t);
-  const uint32_t p_below = dpp<DPP_ROW_SHR1>(pj);  // p_{j-1}: the limbs of 2^32 p
-  const int64_t t1 = mine ? (int64_t)(uint64_t)n0 + (int64_t)(uint64_t)p_below - (j == 12 ? (1ll << 30) : 0) : 0;
-  const uint32_t n1 = norm<true>(t1);
-  const uint32_t k = (row_readlane(n1, base) * N0) & 0x7fffffffu;
-  const uint64_t t2 = mine ? (uint64_t)n1 + (uint64_t)k * pj : 0ull;
-  const uint32_t n2 = norm<false>((int64_t)t2);
-  const uint32_t up = dpp<DPP_ROW_SHL1>(n2);
-  const uint32_t w = (n2 >> 31) | (up << 1);
-  return canon(w, pj);
+  const int64_t bias = j == 12 ? (1ll << 29) : 0;
+  const int64_t ta = mine ? (int64_t)(uint64_t)x * f0 + (int64_t)(uint64_t)y * g0 + bias : 0;
+  const int64_t tb = mine ? (int64_t)(uint64_t)x * f1 + (int64_t)(uint64_t)y * g1 + bias : 0;
+  uint32_t va, vb;
+  norm2(ta, tb, va, vb);
+  na = row_readlane(va, base + 12) < (1u << 29);
+  nb = row_readlane(vb, base + 12) < (1u << 29);
+  if (na || nb) {
+    const int64_t da = mine ? (na ? bias - (int64_t)(uint64_t)va : (int64_t)(uint64_t)va - bias) : 0;
+    const int64_t db = mine ? (nb ? bias - (int64_t)(uint64_t)vb : (int64_t)(uint64_t)vb - bias) : 0;
+    norm2(da, db, va, vb);
+  } else if (j == 12) {
+    va -= 1u << 29;
+    vb -= 1u << 29;
+  }
+  const uint32_t ua = dpp<DPP_ROW_SHL1>(va), ub = dpp<DPP_ROW_SHL1>(vb);  // limb j + 1 (lane 15: 0)
+  ra = (va >> 31) | (ua << 1);
+  rb = (vb >> 31) | (ub << 1);
+}
+
+// The two new (u, v) = (u f0 + v g0, u f1 + v g1) / 2^31 mod p for u, v in [0, p),
+// |f| + |g| <= 2^31 (canonical results), both at once.  |t| < 2^31 p: t + 2^414
+// normalises (the bias on lane 12, where u, v are 0, so no lane's partial leaves
+// int64), then the bias becomes 2^32 p (t + 2^32 p > 0, = t mod p after / 2^31), then
+// + k p with k = -t p^-1 mod 2^31 makes the sum divisible by 2^31:
+// (t + (2^32 + k) p) / 2^31 in (p, 4 p).
+LB_CO void row_lin_mod2(uint32_t u, uint32_t v, int64_t f0, int64_t g0, int64_t f1, int64_t g1, bool mine,
+                        uint32_t base, uint32_t pj, uint32_t& ru, uint32_t& rv) {
+  const uint32_t j = lane16();
+  const int64_t bias = j == 12 ? (1ll << 30) : 0;
+  const int64_t ta = mine ? (int64_t)(uint64_t)u * f0 + (int64_t)(uint64_t)v * g0 + bias : 0;
+  const int64_t tb = mine ? (int64_t)(uint64_t)u * f1 + (int64_t)(uint64_t)v * g1 + bias : 0;
+  uint32_t na, nb;
+  norm2(ta, tb, na, nb);
+  const int64_t pb = (int64_t)(uint64_t)dpp<DPP_ROW_SHR1>(pj) - bias;  // p_{j-1}: the limbs of 2^32 p
+  norm2(mine ? (int64_t)(uint64_t)na + pb : 0, mine ? (int64_t)(uint64_t)nb + pb : 0, na, nb);
+  const uint32_t ka = (row_readlane(na, base) * N0) & 0x7fffffffu;
+  const uint32_t kb = (row_readlane(nb, base) * N0) & 0x7fffffffu;
+  norm2(mine ? (int64_t)((uint64_t)na + (uint64_t)ka * pj) : 0, mine ? (int64_t)((uint64_t)nb + (uint64_t)kb * pj) : 0,
+        na, nb);
+  const uint32_t ua = dpp<DPP_ROW_SHL1>(na), ub = dpp<DPP_ROW_SHL1>(nb);
+  ru = canon((na >> 31) | (ua << 1), pj);
+  rv = canon((nb >> 31) | (ub << 1), pj);
 }
 
 LB_CO uint32_t row_inv_raw(uint32_t y, bool mine, uint32_t base, uint32_t pj) {
@@ -291,7 +313,9 @@ LB_CO uint32_t row_inv_raw(uint32_t y, bool mine, uint32_t base, uint32_t pj) {
 #pragma unroll 1
     for (int i = 0; i < 31; i++) {
       const bool odd = (xa & 1u) != 0;
-      const bool sw = odd && xa < xb;
+      // xa < xb from 32-bit halves: scalar compares (a 64-bit compare is a VALU
+      // instruction, and its round trip to the scalar unit cost ~300 cycles per divstep)
+      const bool sw = odd && s_lt64(xa, xb);
       const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
       const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
       xa = odd ? (ta - tb) >> 1 : ta >> 1;
@@ -302,8 +326,8 @@ LB_CO uint32_t row_inv_raw(uint32_t y, bool mine, uint32_t base, uint32_t pj) {
       g1 = tg1 * 2;
     }
     bool an, bn;
-    const uint32_t na = row_lin_shift(a, b, f0, g0, mine, base, an);
-    const uint32_t nb = row_lin_shift(a, b, f1, g1, mine, base, bn);
+    uint32_t na, nb;
+    row_lin_shift2(a, b, f0, g0, f1, g1, mine, base, na, nb, an, bn);
     if (an) {
       f0 = -f0;
       g0 = -g0;
@@ -312,8 +336,8 @@ LB_CO uint32_t row_inv_raw(uint32_t y, bool mine, uint32_t base, uint32_t pj) {
       f1 = -f1;
       g1 = -g1;
     }
-    const uint32_t nu = row_lin_mod(u, v, f0, g0, mine, base, pj);
-    const uint32_t nv = row_lin_mod(u, v, f1, g1, mine, base, pj);
+    uint32_t nu, nv;
+    row_lin_mod2(u, v, f0, g0, f1, g1, mine, base, pj, nu, nv);
     if (mine) {
       a = na;
       b = nb;
