@@ -110,6 +110,9 @@ struct SmState {
 // One in-flight call: two streams (DAG), own workspace, staging and events.
 struct Slot {
   hipStream_t st[2] = {};
+  // LB_PRIO_CUS with LB_PRIO_DYN=1: the slot's streams without and with the CU mask;
+  // st[] is one pair or the other, chosen when a call is submitted (pick_streams)
+  hipStream_t st_full[2] = {}, st_mask[2] = {};
   hipEvent_t dep[8] = {};
   hipEvent_t done = nullptr;
   char* d_ws = nullptr;
@@ -172,6 +175,12 @@ struct lb_ctx {
   Slot slots[kMaxSlots + 1];
   Slot& prio() { return slots[n_slots]; }
   int prio_cus = 0;  // CUs the throughput slots leave to the priority lane (LB_PRIO_CUS)
+  // LB_PRIO_DYN=1 (with LB_PRIO_CUS): the throughput calls take the masked streams only
+  // while the priority lane has been used within the last prio_hold_ms (LB_PRIO_HOLD_MS)
+  bool prio_dyn = false;
+  int prio_dyn_slots = 0;  // slots [0, prio_dyn_slots) own masked streams (LB_PRIO_DYN_SLOTS)
+  double prio_hold_ms = 250.0;
+  std::chrono::steady_clock::time_point last_prio{};
   int next_slot = 0;
   uint64_t next_ticket = 1;
   // the last tickets issued to two-phase calls: lb_verify_requests_finish accepts a
@@ -1087,18 +1096,25 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_SLOT0_STREAMS")) ctx->streams_per_slot[0] = atoi(e) == 1 ? 1 : 2;
   int prio_least = 0, prio_greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-  // LB_PRIO_CUS=K: the throughput slots' streams leave K CUs (the highest-numbered) to the
-  // priority lane, so a latency-path call finds a free CU under load (a running
-  // workgroup is never preempted; a priority stream alone only reorders dispatch)
+  // The priority lane's CU reservation.  A running workgroup is never
+  // preempted and a priority stream only reorders dispatch, so under load a latency-path
+  // call would wait for a whole CU to drain.  LB_PRIO_CUS=K (default 64 of 256; 0 = off):
+  // masked streams that leave the K highest-numbered CUs to the priority lane.
+  // LB_PRIO_DYN (default 1): throughput calls take them only while the priority lane has
+  // been used within the last LB_PRIO_HOLD_MS (default 250), the full streams otherwise,
+  // so a GPU without priority traffic keeps every CU.  Measured (profiles/r04/prio_ab/):
+  // 1-set / 128-set p50 under 16 calls in flight 1.17x / 1.80x idle (6.3x / 4.8x without),
+  // C2 throughput unchanged.
   std::vector<uint32_t> cu_mask;
-  if (const char* e = getenv("LB_PRIO_CUS")) {
+  {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const int k = atoi(e);
+    int k = cus >= 128 ? 64 : 0;
+    if (const char* e = getenv("LB_PRIO_CUS")) k = atoi(e);
     if (k > 0 && k < cus) {
       cu_mask.assign((size_t)(cus + 31) / 32, 0u);
-      // LB_PRIO_SPREAD=1: the K reserved CUs evenly spaced over the CU ids (with contiguous
-      // ids per XCD, K/8 per XCD: no XCD left with fewer CUs for the throughput kernels)
+      // LB_PRIO_SPREAD=1: the K reserved CUs evenly spaced over the CU ids instead (measured
+      // worse: the mask bits do not map to CUs that way)
       const char* sp = getenv("LB_PRIO_SPREAD");
       const bool spread = sp && atoi(sp) == 1;
       std::vector<char> reserved((size_t)cus, 0);
@@ -1108,15 +1124,40 @@ int lb_create(int device, lb_ctx** out_ctx) {
       ctx->prio_cus = k;
     }
   }
+  if (!cu_mask.empty()) {
+    const char* dy = getenv("LB_PRIO_DYN");
+    ctx->prio_dyn = !dy || atoi(dy) != 0;
+    if (const char* h = getenv("LB_PRIO_HOLD_MS")) ctx->prio_hold_ms = atof(h);
+    // every masked stream takes a hardware queue of a pool of its own, and every queue
+    // reserves scratch (§5.1): with LB_PRIO_DYN_SLOTS=K only the first K slots get one
+    // masked stream each; while the priority lane is in use new calls go to those slots
+    // (default 4: 16 unmasked queues + 4 masked ones measured fine; 16 + 16 ran out of
+    // scratch, like 24 queues of one pool)
+    ctx->prio_dyn_slots = ctx->n_slots;
+    int v = 4;
+    if (const char* k = getenv("LB_PRIO_DYN_SLOTS")) v = atoi(k);
+    if (ctx->prio_dyn && v >= 1 && v < ctx->n_slots) ctx->prio_dyn_slots = v;
+  }
   for (int s = 0; ok && s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++) {
-      if (s == ctx->n_slots)
+      if (s == ctx->n_slots) {
         ok = hipStreamCreateWithPriority(&sl.st[i], hipStreamNonBlocking, prio_greatest) == hipSuccess;
-      else if (!cu_mask.empty())
-        ok = hipExtStreamCreateWithCUMask(&sl.st[i], (uint32_t)cu_mask.size(), cu_mask.data()) == hipSuccess;
-      else
+      } else if (!cu_mask.empty()) {
+        const bool one = ctx->prio_dyn && ctx->prio_dyn_slots < ctx->n_slots;  // one masked stream per slot
+        if (s < ctx->prio_dyn_slots && !(one && i > 0))
+          ok = hipExtStreamCreateWithCUMask(&sl.st_mask[i], (uint32_t)cu_mask.size(), cu_mask.data()) == hipSuccess;
+        else if (one && i > 0)
+          sl.st_mask[i] = sl.st_mask[0];
+        if (ok && ctx->prio_dyn) ok = hipStreamCreateWithFlags(&sl.st_full[i], hipStreamNonBlocking) == hipSuccess;
+        sl.st[i] = ctx->prio_dyn ? sl.st_full[i] : sl.st_mask[i];
+      } else {
         ok = hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking) == hipSuccess;
+      }
+    }
+    if (ctx->streams_per_slot[s] == 1) {
+      sl.st_full[1] = sl.st_full[0];
+      sl.st_mask[1] = sl.st_mask[0];
     }
     if (ctx->streams_per_slot[s] == 1) sl.st[1] = sl.st[0];
     for (int i = 0; ok && i < 8; i++) ok = hipEventCreateWithFlags(&sl.dep[i], hipEventDisableTiming) == hipSuccess;
@@ -1153,8 +1194,11 @@ int lb_destroy(lb_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   for (int s = 0; s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
-    for (int i = 0; i < ctx->streams_per_slot[s]; i++)
+    for (int i = 0; i < ctx->streams_per_slot[s]; i++) {
       if (sl.st[i]) (void)hipStreamSynchronize(sl.st[i]);
+      if (sl.st_full[i]) (void)hipStreamSynchronize(sl.st_full[i]);
+      if (sl.st_mask[i]) (void)hipStreamSynchronize(sl.st_mask[i]);
+    }
     if (sl.d_ws) (void)hipFree(sl.d_ws);
     if (sl.h_pin) (void)hipHostFree(sl.h_pin);
     for (int i = 0; i < 8; i++)
@@ -1169,8 +1213,14 @@ int lb_destroy(lb_ctx* ctx) {
     if (sl.partial_ev) (void)hipEventDestroy(sl.partial_ev);
     if (sl.h_stats) (void)hipHostFree(sl.h_stats);
     if (sl.h_partial) (void)hipHostFree(sl.h_partial);
-    for (int i = 0; i < ctx->streams_per_slot[s]; i++)
-      if (sl.st[i]) (void)hipStreamDestroy(sl.st[i]);
+    for (int i = 0; i < ctx->streams_per_slot[s]; i++) {
+      if (sl.st_mask[i] || sl.st_full[i]) {  // (st[] is one of these pairs)
+        if (sl.st_mask[i] && !(i > 0 && sl.st_mask[i] == sl.st_mask[0])) (void)hipStreamDestroy(sl.st_mask[i]);
+        if (sl.st_full[i]) (void)hipStreamDestroy(sl.st_full[i]);
+      } else if (sl.st[i]) {
+        (void)hipStreamDestroy(sl.st[i]);
+      }
+    }
   }
   if (ctx->d_table) (void)hipFree(ctx->d_table);
   if (ctx->aux_stream) {
@@ -1221,9 +1271,30 @@ int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names
   return ctx->n_stages;
 }
 
+// the priority lane used within the last prio_hold_ms (LB_PRIO_DYN)
+static bool prio_active(lb_ctx* ctx) {
+  return ctx->prio_dyn && std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                                    ctx->last_prio).count() < ctx->prio_hold_ms;
+}
+
+// A call about to run on slot sl (idle: finish_slot has retired its last call): with
+// LB_PRIO_DYN, the masked streams while the priority lane is in use, else the full ones.
+// The priority slot marks the lane in use.
+static void pick_streams(lb_ctx* ctx, Slot& sl) {
+  if (&sl == &ctx->prio()) {
+    ctx->last_prio = std::chrono::steady_clock::now();
+    return;
+  }
+  if (!ctx->prio_dyn) return;
+  const bool masked = prio_active(ctx) && sl.st_mask[0];
+  sl.st[0] = masked ? sl.st_mask[0] : sl.st_full[0];
+  sl.st[1] = masked ? sl.st_mask[1] : sl.st_full[1];
+}
+
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
                          uint8_t* d_set_status, bool partial, uint64_t* out_ticket) {
   LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
+  pick_streams(ctx, sl);
   if (!partial) borrow_idle_stream(ctx, sl);  // (a pending two-phase call never holds a lent slot)
   LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(b->n_requests, b->n_sets)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
@@ -1322,6 +1393,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
       al(sz_req) + al(sz_pko) + al(sz_pk) + al(sz_msg) + al(sz_sigo) + al(sz_sig) + al(sz_seed) + al(sz_rows);
   const size_t out_bytes = al(nr ? nr : 1) * 2 + al(ns ? ns : 1);
   LB_TRY(finish_slot(ctx, sl));
+  pick_streams(ctx, sl);
   t_finish = ms_since(t0);
   if (!partial) borrow_idle_stream(ctx, sl);
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
@@ -1409,10 +1481,13 @@ static void fill_stats(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
 // waits for the host's combined verdict (reusing it would retire that call with
 // merged_ok = 0: correct verdicts, but every request's tail re-run); only when
 // every slot holds a pending partial is the next one taken anyway.
+// While the priority lane is in use (LB_PRIO_DYN), only the slots with masked streams.
 static Slot& next_async_slot(lb_ctx* ctx) {  // internal: not part of the C ABI
-  int s = ctx->next_slot;
-  for (int k = 0; k < ctx->n_slots; k++) {
-    const int c = (ctx->next_slot + k) % ctx->n_slots;
+  const int n = prio_active(ctx) ? ctx->prio_dyn_slots : ctx->n_slots;
+  const int start = ctx->next_slot % n;
+  int s = start;
+  for (int k = 0; k < n; k++) {
+    const int c = (start + k) % n;
     if (!ctx->slots[c].partial_pending) {
       s = c;
       break;
@@ -2207,6 +2282,7 @@ int lb_verify_same_message_batch_async(lb_ctx* ctx, const lb_same_message_batch*
   LB_TRY(sm_pump(ctx));
   Slot& sl = next_async_slot(ctx);
   LB_TRY(finish_slot(ctx, sl));
+  pick_streams(ctx, sl);
   if (b->n_jobs == 0) {  // nothing to verify: a call that completes at once
     LB_TRY(begin_call(ctx, sl));
     LB_TRY(end_call_async(ctx, sl));
@@ -2231,6 +2307,7 @@ int lb_verify_same_message_batch(lb_ctx* ctx, const lb_same_message_batch* b, ui
   LB_TRY(borrow_second_stream(ctx, g));
   Slot& sl = ctx->slots[0];
   LB_TRY(finish_slot(ctx, sl));
+  pick_streams(ctx, sl);
   LB_TRY(sm_submit(ctx, sl, b, out_valid, out_job_fast));
   const uint64_t t = sl.ticket;
   LB_TRY(finish_slot(ctx, sl));
