@@ -1286,9 +1286,16 @@ static void pick_streams(lb_ctx* ctx, Slot& sl) {
     return;
   }
   if (!ctx->prio_dyn) return;
-  const bool masked = prio_active(ctx) && sl.st_mask[0];
-  sl.st[0] = masked ? sl.st_mask[0] : sl.st_full[0];
-  sl.st[1] = masked ? sl.st_mask[1] : sl.st_full[1];
+  if (prio_active(ctx)) {
+    // a slot without masked streams queues on those of slot (s mod K) -- on the GPU, not
+    // in finish_slot: the submitting thread never waits longer than the round robin makes it
+    const Slot& m = sl.st_mask[0] ? sl : ctx->slots[(&sl - ctx->slots) % ctx->prio_dyn_slots];
+    sl.st[0] = m.st_mask[0];
+    sl.st[1] = m.st_mask[1];
+  } else {
+    sl.st[0] = sl.st_full[0];
+    sl.st[1] = sl.st_full[1];
+  }
 }
 
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
@@ -1481,13 +1488,10 @@ static void fill_stats(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
 // waits for the host's combined verdict (reusing it would retire that call with
 // merged_ok = 0: correct verdicts, but every request's tail re-run); only when
 // every slot holds a pending partial is the next one taken anyway.
-// While the priority lane is in use (LB_PRIO_DYN), only the slots with masked streams.
 static Slot& next_async_slot(lb_ctx* ctx) {  // internal: not part of the C ABI
-  const int n = prio_active(ctx) ? ctx->prio_dyn_slots : ctx->n_slots;
-  const int start = ctx->next_slot % n;
-  int s = start;
-  for (int k = 0; k < n; k++) {
-    const int c = (start + k) % n;
+  int s = ctx->next_slot;
+  for (int k = 0; k < ctx->n_slots; k++) {
+    const int c = (ctx->next_slot + k) % ctx->n_slots;
     if (!ctx->slots[c].partial_pending) {
       s = c;
       break;
