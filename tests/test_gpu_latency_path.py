@@ -125,3 +125,31 @@ def test_latency_small_calls(lp_dev, tp_dev, workload):
         out[name] = (_timed(lp_dev, args, seed), _timed(tp_dev, args, seed))
     print("\nlatency p50 ms (lp, throughput):", out)
     assert out["1set"][0] < 20 and out["128set"][0] < 40
+
+
+def test_priority_lane_beside_calls_in_flight(workload):
+    """Priority calls between throughput calls in flight: while the lane is in use the
+    calls submitted meanwhile run on the CU-masked streams (slots without one queue on
+    those of the first slots, bls_host.hip pick_streams); every verdict, code and set
+    status must equal the same calls made one at a time."""
+    dev = Device(0)
+    try:
+        dev.set_latency_path(256)  # the 900-set call: the throughput pipeline; 1-request calls: the latency path
+        seed = hashlib.sha256(b"prio-inflight").digest()
+        want = dev.verify_requests(*workload, seed)
+        req_off = workload[0]
+        small = [r for r in range(len(req_off) - 1) if req_off[r + 1] - req_off[r] <= 4][:6]
+        want_small = [dev.verify_requests(*_slice(workload, r, r + 1), seed) for r in small]
+        pend = [dev.verify_requests_async(*workload, seed) for _ in range(6)]
+        for r, ws in zip(small, want_small):
+            got = dev.wait_call(dev.verify_requests_async(*_slice(workload, r, r + 1), seed, priority=True))
+            assert (list(got.valid), list(got.errors), list(got.set_status)) == \
+                (list(ws.valid), list(ws.errors), list(ws.set_status)), r
+            pend.append(dev.verify_requests_async(*workload, seed))  # submitted while the lane is in use
+        for pc in pend:
+            got = dev.wait_call(pc)
+            assert list(got.valid) == list(want.valid)
+            assert list(got.errors) == list(want.errors)
+            assert list(got.set_status) == list(want.set_status)
+    finally:
+        dev.close()
