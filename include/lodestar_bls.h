@@ -244,6 +244,9 @@ int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576);
 /* Non-blocking: *out_ready = 1 when lb_partial_wait(ticket) would return at once
  * (a host's resolver thread polls it, so the combine never stalls submission). */
 int lb_partial_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_ready);
+/* lb_gt_check touches only the context's own combine buffers and its aux stream (not
+ * the slots): one thread may run it while another submits and retires calls on the
+ * same context (bench.py's resolver thread does); two lb_gt_check at once may not. */
 int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* out_is_one);
 int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok);
 
