@@ -312,6 +312,22 @@ void worker_loop(Context* c) {
   std::deque<Task*> prio;      // priority-lane calls in flight (retired as soon as done)
   for (;;) {
     Task* t = nullptr;
+    // a finished priority call retires before anything else is started: with packages
+    // startable back to back (each ~3 ms of staging in lb_verify_requests_async), its
+    // verdict would otherwise wait behind all of them
+    if (!prio.empty()) {
+      Task* w = prio.front();
+      int32_t done = 0;
+      if (lb_poll(c->ctx, w->ticket, &done) == LB_OK && done) {
+        prio.pop_front();
+        w->t_retire = now_ns();
+        const int rc = lb_wait(c->ctx, w->ticket, &w->stats);
+        if (rc != LB_OK) fail(w, rc, c->ctx);
+        w->t_end = now_ns();
+        complete(c, w);
+        continue;
+      }
+    }
     {
       std::unique_lock<std::mutex> lk(c->mu);
       c->cv.wait(lk, [&] { return !c->queue.empty() || !inflight.empty() || !prio.empty() || c->finalizing; });
