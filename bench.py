@@ -555,6 +555,13 @@ def main():
         dist.barrier()
 
 
+# Algorithmic work priced at the lowest count the same kernel reaches (the
+# default k_step_acc takes one line at a time, 631,170 mads/set; with lines paired the same
+# accumulation needs 554,850 -- DESIGN.md §4 table), so a frac never credits redundant work
+ALGO_MIN_MADS_PER_SET = {"step_acc": 554850.0}
+ALGO_MIN_PIPELINE_SAVING = 631170.0 - 554850.0
+
+
 def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     """Dominant kernel's integer-MAD roofline (achieved = algorithmic mads of one
     launch / its HIP-event duration, one call at a time) + the pipeline's."""
@@ -578,6 +585,9 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     split = split_env != "0" and (split_env == "1" or n_req >= 64)  # default: lone calls from 64 requests
     if lone and split:
         per_set = lone["mads_per_set"]
+    executed = per_set
+    if not pairs_org and dom in ALGO_MIN_MADS_PER_SET:
+        per_set = min(per_set, ALGO_MIN_MADS_PER_SET[dom])
     mads = per_set * n
     achieved = mads / (timing[dom] * 1e-3) / 1e12
     peak = PEAK_MAD_PER_S / 1e12
@@ -587,12 +597,12 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
             "unit": "Tmad/s", "frac": round(achieved / peak, 5), "traffic": traffic,
-            "algorithmic_mads_per_launch": mads,
+            "algorithmic_mads_per_launch": mads, "executed_mads_per_set": round(executed),
             "launch_ms": round(timing[dom], 3),
             "timing": "median of %d one-at-a-time single-stream calls after the timed region (LB_DAG=0: "
                       "the kernel alone on the GPU; HIP events on its stream)" % iso_reps
                       if iso_ms else "timed region, calls overlapped"}
-    if per_set != per_set_pipe:
+    if executed != per_set_pipe:
         roof["organisation"] = ("lone call: requests split in halves, one pair per lane "
                                 "(profiles/op_counts.json lone_call_stages)")
         roof["mads_per_set_launch"] = round(per_set)
@@ -604,20 +614,23 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
         ka = {}
         for k, ms in sorted(iso_ms.items(), key=lambda x: -x[1]):
             m = stages.get(k, {}).get("mads_per_set")
+            if m and not pairs_org and k in ALGO_MIN_MADS_PER_SET:
+                m = min(m, ALGO_MIN_MADS_PER_SET[k])
             if m and ms > 0.5:
                 ka[k] = {"ms": round(ms, 3), "frac": round(m * n / (ms * 1e-3) / 1e12 / peak, 4)}
         roof["kernels_alone"] = ka
     if iso_ms and dom in stage_ms:
         # the same kernel while other calls' kernels share the CUs (timed region, two pairs per lane)
         roof["in_pipeline_launch_ms"] = round(stage_ms[dom], 3)
-        roof["in_pipeline_frac"] = round(per_set_pipe * n / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
+        roof["in_pipeline_frac"] = round(min(per_set_pipe, per_set) * n / (stage_ms[dom] * 1e-3) / 1e12 / peak, 5)
     tot_key = "pairs_mads_per_set_total" if pairs_org and "pairs_mads_per_set_total" in oc else "mads_per_set_total"
     if tot_key in oc:
         # whole pipeline: every v_mad_u64_u32 the algorithm needs per set x sets/s
-        pipe = value * oc[tot_key] / 1e12
+        tot = oc[tot_key] - (0 if pairs_org else ALGO_MIN_PIPELINE_SAVING)
+        pipe = value * tot / 1e12
         roof["pipeline_achieved"] = round(pipe, 4)
         roof["pipeline_frac"] = round(pipe / peak, 5)
-        roof["mads_per_set"] = round(oc[tot_key])
+        roof["mads_per_set"] = round(tot)
     return roof
 
 
