@@ -388,15 +388,19 @@ def main():
     # GPU (the roofline of the dominant kernel is priced on these)
     iso = {}
     if a.iso_reps > 0:
-        old_dag = os.environ.get("LB_DAG")
+        # (and no priority-lane CU reservation: a second context's CU-masked streams cost the
+        # later legs of this process a third of their throughput)
+        saved = {k: os.environ.get(k) for k in ("LB_DAG", "LB_PRIO_CUS")}
         os.environ["LB_DAG"] = "0"
+        os.environ["LB_PRIO_CUS"] = "0"
         try:
             iso_dev = Device(gpu)
         finally:
-            if old_dag is None:
-                os.environ.pop("LB_DAG", None)
-            else:
-                os.environ["LB_DAG"] = old_dag
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         for k in range(a.iso_reps + 1):  # (+1: the context's first call is a warm-up)
             iso_dev.verify_requests_device(n_req, n, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
                                            d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
