@@ -1102,8 +1102,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
   // masked streams that leave the K highest-numbered CUs to the priority lane.
   // LB_PRIO_DYN (default 1): throughput calls take them only while the priority lane has
   // been used within the last LB_PRIO_HOLD_MS (default 250), the full streams otherwise,
-  // so a GPU without priority traffic keeps every CU.  Measured (profiles/r04/prio_ab/):
-  // 1-set / 128-set p50 under 16 calls in flight 1.17x / 1.80x idle (6.3x / 4.8x without),
+  // so a GPU without priority traffic keeps every CU.  Measured (profiles/r04/prio_ab/,
+  // legs_ab/): 1-set / 128-set p50 under 16 calls in flight 1.2x / 1.9x idle (4-6x without),
   // C2 throughput unchanged.
   std::vector<uint32_t> cu_mask;
   {
@@ -1131,10 +1131,12 @@ int lb_create(int device, lb_ctx** out_ctx) {
     // every masked stream takes a hardware queue of a pool of its own, and every queue
     // reserves scratch (§5.1): with LB_PRIO_DYN_SLOTS=K only the first K slots get one
     // masked stream each; while the priority lane is in use new calls go to those slots
-    // (default 4: 16 unmasked queues + 4 masked ones measured fine; 16 + 16 ran out of
-    // scratch, like 24 queues of one pool)
+    // (default 2: 16 + 16 ran out of scratch, like 24 queues of one pool; with 4 masked
+    // queues the queues of a second context or process on the same GPU -- bench.py's
+    // single-stream timing context, its node leg -- slowed every later call by a third,
+    // with 2 they did not)
     ctx->prio_dyn_slots = ctx->n_slots;
-    int v = 4;
+    int v = 2;
     if (const char* k = getenv("LB_PRIO_DYN_SLOTS")) v = atoi(k);
     if (ctx->prio_dyn && v >= 1 && v < ctx->n_slots) ctx->prio_dyn_slots = v;
   }
