@@ -592,6 +592,8 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     executed = per_set
     if not pairs_org and dom in ALGO_MIN_MADS_PER_SET:
         per_set = min(per_set, ALGO_MIN_MADS_PER_SET[dom])
+        if os.environ.get("LB_STEP_MODE", "1") in ("0", "1"):  # paired lines (the default LDS build)
+            executed = per_set
     mads = per_set * n
     achieved = mads / (timing[dom] * 1e-3) / 1e12
     peak = PEAK_MAD_PER_S / 1e12

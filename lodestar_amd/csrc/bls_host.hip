@@ -211,10 +211,13 @@ struct lb_ctx {
   bool dag = true;
   // LB_STEP_MODE: k_step_acc variant (0 registers + paired lines, 1 accumulator in LDS,
   // 2 registers + one line at a time; k_steps.hip)
-  // defaults: one line at a time at 2 waves/SIMD, which with 2-wave k_lines_rows measured
-  // 3.48-3.54 vs 3.35-3.37 M sets/s (profiles/ab_r03/ab_r03s, three rounds each)
-  int step_mode = 2;
-  int step_waves = 2;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
+  // defaults (round 4): the accumulator in LDS at one wave per SIMD -- alone 4.64-4.70 ms per
+  // C2 launch against 6.04-6.10 for one line at a time at 2 waves/SIMD (which spilled 1,408
+  // B/lane: 18.3 GB of traffic per launch, 13.9x the algorithmic bytes; now 2.6 GB, 2.0x), the
+  // pipeline 3.55-3.62 vs 3.54-3.57 M sets/s, three interleaved runs each
+  // (profiles/r04/step_ab/).  Round 3 had measured 2/2 ahead of 2/1 (profiles/ab_r03/ab_r03s).
+  int step_mode = 1;
+  int step_waves = 1;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
   // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
   // submission; the N-API addon sets it, lb_last_stage_times is then empty)
   bool stage_events = true;
