@@ -89,6 +89,15 @@ const char* lb_last_error(const lb_ctx* ctx);
  * lb_create refuses GPU_MAX_HW_QUEUES > 16 with LB_ERR_RESOURCES: every queue reserves
  * scratch for the largest private segment at full occupancy (lb_scratch_per_queue). */
 int lb_slots(const lb_ctx* ctx);
+/* HIP hardware queues the context opens: its plain streams (pooled into at most
+ * GPU_MAX_HW_QUEUES queues), its CU-masked streams (one queue each) and its
+ * high-priority streams (priority lane, lb_gt_check's aux stream).  lb_create prices
+ * all of them against the scratch budget (LB_SCRATCH_BUDGET_GB, default that of the
+ * largest configuration seen to run: 20 queues at 3,328 private bytes per lane) and
+ * refuses a configuration above it with LB_ERR_RESOURCES. */
+int lb_hw_queues(const lb_ctx* ctx);
+/* Distinct streams the last submitted verify call runs on (2: the two-stream DAG). */
+int lb_last_call_streams(const lb_ctx* ctx);
 /* Number of visible HIP devices (0 when none). */
 int lb_device_count(void);
 /* Scratch one hardware queue reserves for the library's kernels: the largest

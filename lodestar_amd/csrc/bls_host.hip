@@ -25,6 +25,7 @@
 
 #include <chrono>
 #include <cstdlib>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -144,6 +145,28 @@ struct Slot {
   // stream of an idle slot (borrowed); that slot is lent (busy) until the call retires
   Slot* borrowed = nullptr;
   Slot* lent_to = nullptr;
+  // a synchronous call's second stream (borrow_second_stream): pick_streams keeps it
+  hipStream_t guard_st = nullptr;
+};
+
+// The context's last error message.  lb_gt_check may run on one thread while another
+// submits and retires calls (include/lodestar_bls.h), and both can fail: every write
+// and read of the message takes a lock.
+class ErrorText {
+ public:
+  ErrorText& operator=(std::string v) {
+    std::lock_guard<std::mutex> g(mu_);
+    s_ = std::move(v);
+    return *this;
+  }
+  operator std::string() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return s_;
+  }
+
+ private:
+  mutable std::mutex mu_;
+  std::string s_;
 };
 
 // Stats of a retired call, kept per ticket (lb_wait reports the stats of ITS
@@ -188,7 +211,7 @@ struct lb_ctx {
   static constexpr int kTwoPhaseRing = 256;
   uint64_t two_phase[kTwoPhaseRing] = {};
   int two_phase_pos = 0;
-  std::string err;
+  ErrorText err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
   // Miller organisation: stored lines + one wave per pair (k_lines/k_pair_wc,
   // lowest latency) up to wave_max_sets; one pair per lane (k_miller_sets)
@@ -256,6 +279,8 @@ struct lb_ctx {
   // (LB_LP_MAX, lb_set_latency_path; 0 = never)
   uint32_t* d_lp = nullptr;
   uint32_t lp_max_sets = 1024;
+  int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
+  int last_call_streams = 0;  // streams of the last submitted verify call (begin_call)
 };
 
 namespace {
@@ -413,16 +438,6 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   c.req_err = d_req_err;
   c.n_sets = n_sets;
   LB_STAGE("lp_verify", 0, k_lp_verify, n_sets, LB_LP_TPB, c);
-  if (getenv("LB_LP_DUMP")) {  // debugging aid: set 0's program inputs, flags and Miller value on stderr
-    std::vector<uint32_t> h((size_t)LB_LP_NIN * 16 + LB_LP_NFL + 12 * 16);
-    LB_HIP(hipStreamSynchronize(sl.st[0]));
-    LB_HIP(hipMemcpy(h.data(), d_in16, LB_LP_NIN * 16 * 4, hipMemcpyDeviceToHost));
-    LB_HIP(hipMemcpy(h.data() + LB_LP_NIN * 16, d_fl, LB_LP_NFL * 4, hipMemcpyDeviceToHost));
-    LB_HIP(hipMemcpy(h.data() + LB_LP_NIN * 16 + LB_LP_NFL, d_F, 12 * 16 * 4, hipMemcpyDeviceToHost));
-    fprintf(stderr, "lb_lp_dump");
-    for (uint32_t w : h) fprintf(stderr, " %08x", w);
-    fprintf(stderr, "\n");
-  }
   PipeState& ps = sl.ps;
   ps = PipeState{};
   ps.n_req = n_req;
@@ -936,6 +951,7 @@ void borrow_idle_stream(lb_ctx* ctx, Slot& sl) {
 }
 
 int begin_call(lb_ctx* ctx, Slot& sl) {
+  ctx->last_call_streams = sl.st[1] != sl.st[0] ? 2 : 1;
   sl.n_stages = 0;
   sl.partial_pending = false;
   sl.out_valid = sl.out_err = sl.out_sst = nullptr;
@@ -969,14 +985,17 @@ struct BorrowGuard {
   lb_ctx* ctx;
   bool active = false;
   ~BorrowGuard() {
-    if (active) ctx->slots[0].st[1] = ctx->slots[0].st[0];
+    if (active) {
+      ctx->slots[0].guard_st = nullptr;
+      ctx->slots[0].st[1] = ctx->slots[0].st[0];
+    }
   }
 };
 int borrow_second_stream(lb_ctx* ctx, BorrowGuard& g) {
   Slot& s0 = ctx->slots[0];
   if (ctx->dag && ctx->streams_per_slot[0] == 1 && ctx->n_slots >= 2) {
     LB_TRY(finish_slot(ctx, ctx->slots[1]));
-    s0.st[1] = ctx->slots[1].st[0];
+    s0.st[1] = s0.guard_st = ctx->slots[1].st[0];
     g.active = true;
   }
   return LB_OK;
@@ -1080,7 +1099,10 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
-  if (const char* e = getenv("LB_LP_MAX")) ctx->lp_max_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_LP_MAX")) {
+    const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
+    ctx->lp_max_sets = v <= 0 ? 0u : v < (1l << LB_LP_TREE_LEVELS) ? (uint32_t)v : (1u << LB_LP_TREE_LEVELS);
+  }
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = ctx->lines_waves_small = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
@@ -1143,6 +1165,46 @@ int lb_create(int device, lb_ctx** out_ctx) {
     if (const char* k = getenv("LB_PRIO_DYN_SLOTS")) v = atoi(k);
     if (ctx->prio_dyn && v >= 1 && v < ctx->n_slots) ctx->prio_dyn_slots = v;
   }
+  // Every hardware queue this context opens reserves scratch for the largest private
+  // segment it runs: price all of them, not only GPU_MAX_HW_QUEUES
+  // (VERDICT r4 #7).  HIP pools the plain streams of one priority into at most
+  // GPU_MAX_HW_QUEUES queues; a CU-masked stream gets a queue of its own.
+  {
+    int maxq = 4;
+    if (const char* e = getenv("GPU_MAX_HW_QUEUES")) maxq = atoi(e) > 0 ? atoi(e) : 4;
+    int plain = 0, masked = 0;
+    const bool one = ctx->prio_dyn && ctx->prio_dyn_slots < ctx->n_slots;
+    for (int s = 0; s < ctx->n_slots; s++) {
+      const int spp = ctx->streams_per_slot[s];
+      if (cu_mask.empty() || ctx->prio_dyn) plain += spp;
+      if (!cu_mask.empty() && s < ctx->prio_dyn_slots) masked += one ? 1 : spp;
+    }
+    const char* tp = getenv("LB_TAIL_PRIO");
+    const int high = 2 + (tp && atoi(tp) == 1 ? 1 : 0);  // priority lane, aux (lb_gt_check), tail stream
+    const int queues = (plain < maxq ? plain : maxq) + (high < maxq ? high : maxq) + masked;
+    uint32_t lane = 0;
+    const size_t per_q = scratch_per_queue(device, &lane);
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    // the largest configuration that ran: 16 plain + 2 masked + 2 high-priority queues at
+    // 3,328 private bytes per lane; 24 + 2 plain (r03) and 16 + 16 masked + 2 (r04) queues
+    // failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES
+    double budget = 20.0 * 3328 * 64 * 32 * cus;
+    if (const char* e = getenv("LB_SCRATCH_BUDGET_GB")) budget = atof(e) * 1e9;
+    if ((double)per_q * queues > budget) {
+      char msg[400];
+      snprintf(msg, sizeof msg,
+               "%d hardware queues (%d plain of GPU_MAX_HW_QUEUES=%d, %d CU-masked, %d high-priority) x %u private "
+               "bytes per lane x 64 x 32 x %d CUs = %.1f GB of scratch exceeds the %.1f GB budget (20 queues at "
+               "3,328 B/lane ran; 16 + 16 masked failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES)",
+               queues, plain < maxq ? plain : maxq, maxq, masked, high < maxq ? high : maxq, lane, cus,
+               per_q * (double)queues / 1e9, budget / 1e9);
+      g_create_err = msg;
+      delete ctx;
+      return LB_ERR_RESOURCES;
+    }
+    ctx->hw_queues = queues;
+  }
   for (int s = 0; ok && s <= ctx->n_slots; s++) {
     Slot& sl = ctx->slots[s];
     for (int i = 0; ok && i < ctx->streams_per_slot[s]; i++) {
@@ -1186,6 +1248,10 @@ int lb_create(int device, lb_ctx** out_ctx) {
     if (e && atoi(e) == 1)
       ok = ok && hipStreamCreateWithPriority(&ctx->tail_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
   }
+  // the latency path's round programs (2.6 MB) are uploaded here, before any call is in
+  // flight: a synchronous copy on the first latency-path call would wait for the
+  // throughput calls already running on blocking (CU-masked) streams
+  if (ok && ctx->lp_max_sets && lp_ensure(ctx) != LB_OK) ok = false;
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;
@@ -1243,7 +1309,12 @@ int lb_destroy(lb_ctx* ctx) {
   return LB_OK;
 }
 
-const char* lb_last_error(const lb_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+const char* lb_last_error(const lb_ctx* ctx) {
+  // (a copy per calling thread: valid until that thread's next lb_last_error)
+  static thread_local std::string out;
+  out = ctx ? std::string(ctx->err) : g_create_err;
+  return out.c_str();
+}
 
 int lb_scratch_per_queue(int device, uint64_t* out_bytes, uint32_t* out_lane_bytes) {
   int n = 0;
@@ -1255,6 +1326,8 @@ int lb_scratch_per_queue(int device, uint64_t* out_bytes, uint32_t* out_lane_byt
 }
 
 int lb_slots(const lb_ctx* ctx) { return ctx ? ctx->n_slots : 0; }
+int lb_hw_queues(const lb_ctx* ctx) { return ctx ? ctx->hw_queues : 0; }
+int lb_last_call_streams(const lb_ctx* ctx) { return ctx ? ctx->last_call_streams : 0; }
 
 #ifdef LB_COUNT_OPS
 // Fp products executed per stage of the last completed verify call (count build only)
@@ -1301,6 +1374,9 @@ static void pick_streams(lb_ctx* ctx, Slot& sl) {
     sl.st[0] = sl.st_full[0];
     sl.st[1] = sl.st_full[1];
   }
+  // a synchronous call's borrowed second stream (BorrowGuard) stays: the call runs as
+  // the two-stream DAG whichever stream pair slot 0 takes
+  if (sl.guard_st) sl.st[1] = sl.guard_st;
 }
 
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
@@ -1579,7 +1655,12 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
     // = 0: every request re-verified alone, so its verdicts stand): nothing to do
     for (int i = 0; ticket != 0 && i < lb_ctx::kTwoPhaseRing; i++)
       if (ctx->two_phase[i] == ticket) return LB_OK;
-    ctx->err = "ticket is not a two-phase call (or one older than the last 256)";
+    // older than every two-phase ticket the ring still holds (the ring wrapped): whether
+    // it was a two-phase call is no longer known, but any retired call's verdicts are
+    // final, so finishing it is a no-op rather than an error
+    const uint64_t oldest = ctx->two_phase[ctx->two_phase_pos];  // (0 until the ring wraps)
+    if (ticket != 0 && oldest != 0 && ticket < oldest && ticket < ctx->next_ticket) return LB_OK;
+    ctx->err = "ticket is not a two-phase call";
     return LB_ERR_INVALID_ARGUMENT;
   }
   return finish_partial(ctx, *sl, merged_ok != 0);
@@ -2546,7 +2627,9 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
 
 int lb_set_latency_path(lb_ctx* ctx, uint32_t max_sets) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
-  ctx->lp_max_sets = max_sets;
+  // (k_lp_verify's product tree has LB_LP_TREE_LEVELS levels of arrival counters: a
+  // request longer than 2^levels sets would count past them)
+  ctx->lp_max_sets = max_sets < (1u << LB_LP_TREE_LEVELS) ? max_sets : (1u << LB_LP_TREE_LEVELS);
   return LB_OK;
 }
 

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "lb_signing_roots_attestation_device", "lb_verify_requests_async", "lb_verify_requests_partial_async",
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
     "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
-    "lb_verify_requests_priority_async", "lb_partial_poll",
+    "lb_verify_requests_priority_async", "lb_partial_poll", "lb_hw_queues", "lb_last_call_streams",
 )
 
 LB_BATCH_DEVICE = 1
@@ -130,6 +130,8 @@ def load_library() -> ctypes.CDLL:
     lib.lb_last_error.argtypes = [vp]
     lib.lb_last_error.restype = ctypes.c_char_p
     lib.lb_slots.argtypes = [vp]
+    lib.lb_hw_queues.argtypes = [vp]
+    lib.lb_last_call_streams.argtypes = [vp]
     lib.lb_device_count.argtypes = []
     lib.lb_scratch_per_queue.argtypes = [i32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     lib.lb_verify_requests.argtypes = [vp, ctypes.POINTER(_RequestBatch), vp, vp, vp, ctypes.POINTER(_Stats)]
@@ -261,6 +263,14 @@ class Device:
     def slots(self) -> int:
         """Calls the library keeps in flight (lb_slots: one per HIP hardware queue)."""
         return int(self.lib.lb_slots(self._h))
+
+    def hw_queues(self) -> int:
+        """HIP hardware queues this context opens (lb_hw_queues, priced by lb_create)."""
+        return int(self.lib.lb_hw_queues(self._h))
+
+    def last_call_streams(self) -> int:
+        """Distinct streams of the last submitted verify call (2 = the two-stream DAG)."""
+        return int(self.lib.lb_last_call_streams(self._h))
 
     def close(self) -> None:
         if self._h:
