@@ -152,10 +152,15 @@ typedef struct {
    * its request LB_REQ_BAD_PUBKEY (the reference would index index2pubkey out of range).
    * Mixed packages (e.g. a capella block: validator-index keys plus the BLS-change
    * keys that are not in the table): with BOTH pubkey_indices and pubkeys given, an
-   * entry with LB_PK_ROW_FLAG set names row (entry & ~LB_PK_ROW_FLAG) of `pubkeys`. */
+   * entry with LB_PK_ROW_FLAG set names row (entry & LB_PK_ROW_MASK) of `pubkeys`;
+   * with LB_PK_ROW48_FLAG also set, that 96-byte row holds a 48-byte COMPRESSED
+   * encoding in its first 48 bytes (decompressed on the GPU: a @chainsafe/bls
+   * PublicKey serialized compressed, PublicKey.fromBytes(48 B) semantics). */
   const uint32_t* pubkey_indices;
 } lb_request_batch;
 #define LB_PK_ROW_FLAG 0x80000000u
+#define LB_PK_ROW48_FLAG 0x40000000u
+#define LB_PK_ROW_MASK 0x3fffffffu
 
 typedef struct {
   uint32_t batch_retries;      /* the DEVICE's merged check: 1 when it failed and requests were
@@ -291,7 +296,9 @@ typedef struct {
   uint32_t n_sets;
   const uint32_t* job_offsets;     /* n_jobs + 1                                    */
   const uint8_t* pubkeys;          /* n_sets x 96 (uncompressed), or NULL with ...  */
-  const uint32_t* pubkey_indices;  /* n_sets validator indices (device pubkey table) */
+  const uint32_t* pubkey_indices;  /* n_sets validator indices (device pubkey table); with
+                                      both given, a mixed package as in lb_request_batch
+                                      (LB_PK_ROW_FLAG / LB_PK_ROW48_FLAG rows of pubkeys) */
   const uint8_t* signatures;       /* concatenated signature bytes                  */
   const uint32_t* sig_offsets;     /* n_sets + 1                                    */
   const uint8_t* messages;         /* n_jobs x 32                                   */

@@ -99,6 +99,7 @@ struct SmState {
   uint8_t* h_rout = nullptr;         // pinned: phase-2 verdicts, errors (al(ns) each)
   // device-resident phase-1 data
   const uint8_t* d_pks = nullptr;    // 96-byte keys or u32 indices (by_index)
+  const uint8_t* d_rows = nullptr;   // by_index: the mixed package's key rows (or nullptr)
   const g2j* d_sig = nullptr;        // decoded signatures (validate=true done once)
   const uint8_t* d_sst = nullptr;
   const uint8_t* d_msgs = nullptr;
@@ -279,6 +280,11 @@ struct lb_ctx {
   // (LB_LP_MAX, lb_set_latency_path; 0 = never)
   uint32_t* d_lp = nullptr;
   uint32_t lp_max_sets = 1024;
+  // the merged check of a steps + MSM call as a round program (k_lp_mtail: S_all from the
+  // MSM's bit sums, Miller(-g1, S_all), final exponentiation on one workgroup) instead of
+  // msm_final + lines of S_all + the one-wave k_tail (LB_MTAIL=0: the one-wave chain)
+  bool mtail_lp = true;
+  bool gt_lp = true;  // lb_gt_check's final exponentiation as a round program (LB_GT_LP=0: one wave)
   int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
   int last_call_streams = 0;  // streams of the last submitted verify call (begin_call)
 };
@@ -541,6 +547,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // leave SIMDs free), otherwise its lines are stored right after the MSM, on
   // stream 0 beside stream 1's hash/lines (lines_all), and k_tail multiplies it in
   const bool fold = use_msm && by_lines && !split && !steps;
+  // merged check as a round program (k_lp_mtail): S_all, its Miller value and the final
+  // exponentiation from the MSM's bit sums and the level products' Horner value
+  const bool mtail = steps && use_msm && merged && ctx->mtail_lp;
+  if (mtail) LB_TRY(lp_ensure(ctx));
   // (steps + merged: the merged pair's lines come from a one-lane kernel before the
   // accumulation; as an extra workgroup of k_step_acc they measured 4.8 -> 8.2 ms: the
   // 1,025th wave waits for a SIMD of the 1,024 set waves, then runs the 3.4 ms line chain)
@@ -576,6 +586,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_rmeta = steps ? ws.take<uint32_t>(1) : nullptr;
   uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns) : nullptr;
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
+  uint32_t* d_mt_in = mtail ? ws.take<uint32_t>((size_t)LB_MTAIL_NIN * 16) : nullptr;
+  uint32_t* d_mt_out = mtail && partial ? ws.take<uint32_t>(12 * 16) : nullptr;
   const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta};
   sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
@@ -662,8 +674,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS), TPB, (const uint32_t*)d_coff,
              (const g2j*)d_mcsum, d_mbsum);
     LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_mbsum, d_mG);
-    LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
-    if (!fold)
+    if (!mtail) LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
+    if (!fold && !mtail)
       LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
                (const uint8_t*)nullptr);
   } else {
@@ -703,8 +715,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_STEP_STAGE(0, 1);
 #undef LB_STEP_STAGE
     if (merged) {
-      LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, n_sets + n_req, rows, d_req_off,
-               (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
+      // (mtail: the merged pair's Miller value comes from the round program, not as lines)
+      LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, mtail ? 0xffffffffu : n_sets + n_req,
+               rows, d_req_off, (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
       LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
     } else {
       LB_STAGE("req_horner", 0, k_req_horner, n_req, TPB, n_req, n_sets, rows, d_req_off, (const uint32_t*)d_G,
@@ -791,6 +804,16 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
                     (const uint8_t*)nullptr);
     }
     const uint32_t* merged_lines = (fold || steps) ? nullptr : (const uint32_t*)d_lines;
+    if (mtail) {
+      hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Fall, (const g2j*)d_mG, d_mt_in);
+      LB_HIP(hipGetLastError());
+      if (partial) {  // F_all * Miller(-g1, S_all) back into d_Fall, encoded by k_partial below
+        LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_PARTIAL].off,
+                    (const uint32_t*)d_mt_in, (uint8_t*)nullptr, d_mt_out);
+        hipLaunchKernelGGL(k_records_to_fp12, dim3(1), dim3(64), 0, ts, (const uint32_t*)d_mt_out, d_Fall);
+        LB_HIP(hipGetLastError());
+      }
+    }
     if (partial) {
       // two-phase call: the merged Miller product goes to the host, which
       // combines it with the other GPUs' partials; the tails wait for its verdict
@@ -805,8 +828,12 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       sl.partial_pending = true;
       return LB_OK;
     }
-    LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, merged_lines,
-                (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
+    if (mtail)
+      LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_CHECK].off,
+                  (const uint32_t*)d_mt_in, d_mflag, (uint32_t*)nullptr);
+    else
+      LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, merged_lines,
+                  (const fp12*)d_Fall, (const uint8_t*)(d_mflag + 1), d_mflag, (const uint8_t*)nullptr);
     if (ts != sl.st[0]) {
       LB_HIP(hipEventRecord(sl.dep[4], ts));
       LB_HIP(hipStreamWaitEvent(sl.st[0], sl.dep[4], 0));
@@ -825,7 +852,9 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
                            8 * 256;
-  return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096;
+  // (+ the merged check's round-program records, k_lp_mtail)
+  return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
+         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1050,6 +1079,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_pair_wc, (const void*)k_miller_sets,
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
+                           (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
                            (const void*)k_msm_buckets, (const void*)k_decode_sigs, (const void*)k_scalar_pk};
   size_t lane = 0;
   for (const void* k : kernels) {
@@ -1099,6 +1129,8 @@ int lb_create(int device, lb_ctx** out_ctx) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_MAX")) {
     const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
     ctx->lp_max_sets = v <= 0 ? 0u : v < (1l << LB_LP_TREE_LEVELS) ? (uint32_t)v : (1u << LB_LP_TREE_LEVELS);
@@ -1251,7 +1283,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
   // the latency path's round programs (2.6 MB) are uploaded here, before any call is in
   // flight: a synchronous copy on the first latency-path call would wait for the
   // throughput calls already running on blocking (CU-masked) streams
-  if (ok && ctx->lp_max_sets && lp_ensure(ctx) != LB_OK) ok = false;
+  if (ok && (ctx->lp_max_sets || ctx->mtail_lp || ctx->gt_lp) && lp_ensure(ctx) != LB_OK) ok = false;
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;
@@ -1470,7 +1502,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   if (by_index && b->pubkeys)
     for (size_t k = 0; k < n_pk; k++) {
       const uint32_t j = b->pubkey_indices[k];
-      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & ~LB_PK_ROW_FLAG) + 1 > n_rows) n_rows = (j & ~LB_PK_ROW_FLAG) + 1;
+      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & LB_PK_ROW_MASK) + 1 > n_rows) n_rows = (j & LB_PK_ROW_MASK) + 1;
     }
   const size_t sig_bytes = b->sig_offsets[ns];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1669,7 +1701,9 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
 int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* out_is_one) {
   if (!ctx || !out_is_one || (n && !partials576)) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
-  const size_t need = (size_t)n * LB_GT_BYTES + 256;
+  // (+ the combined product's 12 records for the round-program final exponentiation)
+  const size_t need = (((size_t)n * LB_GT_BYTES + 255) & ~(size_t)255) + 256 + 12 * 64;
+  if (ctx->gt_lp) LB_TRY(lp_ensure(ctx));
   if (need > ctx->aux_cap) {
     LB_HIP(hipStreamSynchronize(ctx->aux_stream));
     if (ctx->d_aux) LB_HIP(hipFree(ctx->d_aux));
@@ -1677,7 +1711,7 @@ int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* ou
     ctx->d_aux = nullptr;
     ctx->h_aux = nullptr;
     ctx->aux_cap = 0;
-    const size_t cap = need < 16 * LB_GT_BYTES + 256 ? 16 * LB_GT_BYTES + 256 : need;
+    const size_t cap = need < 16 * LB_GT_BYTES + 256 + 12 * 64 ? 16 * LB_GT_BYTES + 256 + 12 * 64 : need;
     if (hipMalloc(&ctx->d_aux, cap) != hipSuccess || hipHostMalloc(&ctx->h_aux, cap, hipHostMallocDefault) != hipSuccess) {
       ctx->err = "gt_check buffers";
       return LB_ERR_OUT_OF_MEMORY;
@@ -1690,8 +1724,20 @@ int lb_gt_check(lb_ctx* ctx, uint32_t n, const uint8_t* partials576, int32_t* ou
     memcpy(ctx->h_aux + 256, partials576, (size_t)n * LB_GT_BYTES);
     LB_HIP(hipMemcpyAsync(d_in, ctx->h_aux + 256, (size_t)n * LB_GT_BYTES, hipMemcpyHostToDevice, ctx->aux_stream));
   }
-  hipLaunchKernelGGL(k_gt_check, dim3(1), dim3(TPB), 0, ctx->aux_stream, n, (const uint8_t*)d_in, d_out);
-  LB_HIP(hipGetLastError());
+  if (ctx->gt_lp) {
+    // the product (one wave), then the final exponentiation as a round program on one
+    // workgroup (~420 rounds) instead of the one-wave chain
+    uint32_t* d_rec = reinterpret_cast<uint32_t*>(ctx->d_aux + 256 + (((size_t)n * LB_GT_BYTES + 255) & ~(size_t)255));
+    hipLaunchKernelGGL(k_gt_prod, dim3(1), dim3(TPB), 0, ctx->aux_stream, n, (const uint8_t*)d_in, d_rec, d_out);
+    LB_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_lp_final_lane, dim3(1), dim3(LB_LP_TPB), 0, ctx->aux_stream,
+                       (const uint32_t*)(ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_FINAL_LANE].off), (const uint32_t*)d_rec,
+                       d_out);
+    LB_HIP(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(k_gt_check, dim3(1), dim3(TPB), 0, ctx->aux_stream, n, (const uint8_t*)d_in, d_out);
+    LB_HIP(hipGetLastError());
+  }
   LB_HIP(hipMemcpyAsync(ctx->h_aux, d_out, 2, hipMemcpyDeviceToHost, ctx->aux_stream));
   LB_HIP(hipStreamSynchronize(ctx->aux_stream));
   if (ctx->h_aux[1]) {
@@ -2159,11 +2205,20 @@ size_t sm_phase2_bytes(uint32_t ns) {
 int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* out_valid, uint8_t* out_job_fast) {
   const uint32_t nj = b->n_jobs, ns = b->n_sets;
   const bool by_index = b->pubkey_indices != nullptr;
+  // mixed package (indices AND rows): rows of `pubkeys` named by flagged indices, as in
+  // lb_request_batch (every row < n_rows is staged)
+  size_t n_rows = 0;
+  if (by_index && b->pubkeys)
+    for (uint32_t i = 0; i < ns; i++) {
+      const uint32_t j = b->pubkey_indices[i];
+      if ((j & LB_PK_ROW_FLAG) && (size_t)(j & LB_PK_ROW_MASK) + 1 > n_rows) n_rows = (j & LB_PK_ROW_MASK) + 1;
+    }
   const size_t sz_joff = sizeof(uint32_t) * (nj + 1), sz_pk = (size_t)ns * (by_index ? 4 : 96),
                sz_sigo = sizeof(uint32_t) * (ns + 1), sz_sig = b->sig_offsets[ns], sz_msg = (size_t)nj * 32,
-               sz_seed = 32, sz_areq = sizeof(uint32_t) * (nj + 1), sz_asig = sizeof(uint32_t) * (nj + 1);
+               sz_seed = 32, sz_areq = sizeof(uint32_t) * (nj + 1), sz_asig = sizeof(uint32_t) * (nj + 1),
+               sz_rows = n_rows * 96;
   const size_t in_bytes = al256(sz_joff) + al256(sz_pk) + al256(sz_sigo) + al256(sz_sig) + al256(sz_msg) +
-                          al256(sz_seed) + al256(sz_areq) + al256(sz_asig);
+                          al256(sz_seed) + al256(sz_areq) + al256(sz_asig) + al256(sz_rows);
   const size_t ns1 = ns ? ns : 1;
   const size_t res_bytes = 4 * al256(nj), retry_bytes = 2 * al256(4 * ns1) + 2 * al256(ns1);
   const size_t extra = ns1 * (sizeof(g2j) + 1) + (size_t)nj * (sizeof(g1j) + 1 + 96 + 192 + 1 + 2) + 16 * 256;
@@ -2186,6 +2241,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   stage(b->seed, sz_seed);
   uint32_t* areq = (uint32_t*)stage(nullptr, sz_areq);
   uint32_t* asig = (uint32_t*)stage(nullptr, sz_asig);
+  if (n_rows) stage(b->pubkeys, sz_rows);
   for (uint32_t j = 0; j <= nj; j++) {
     areq[j] = j;        // every job one request of one (aggregated) set
     asig[j] = 192 * j;  // Signature.aggregate(...).toBytes(uncompressed)
@@ -2205,6 +2261,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   const uint8_t* d_seed = (const uint8_t*)dptr(sz_seed);
   const uint32_t* d_areq = (const uint32_t*)dptr(sz_areq);
   const uint32_t* d_asig = (const uint32_t*)dptr(sz_asig);
+  const uint8_t* d_rows = n_rows ? (const uint8_t*)dptr(sz_rows) : nullptr;
   g2j* d_sig = ws.take<g2j>(ns1);
   uint8_t* d_sst = ws.take<uint8_t>(ns1);
   g1j* d_jpk = ws.take<g1j>(nj);
@@ -2219,7 +2276,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   if (ns)
     LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
              d_sst);
-  const PkSource src{by_index ? nullptr : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
+  const PkSource src{by_index ? d_rows : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
                      ctx->table_n};
   const uint32_t agg_grid = nj < 16384u ? nj : 16384u;
   LB_STAGE("sm_pubkeys", 0, k_pubkeys_single, blocks_for(nj), TPB, nj, src, d_joff, d_jpk, d_jpkst);
@@ -2246,6 +2303,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   m.h_rset = (uint32_t*)(h_res + res_bytes);
   m.h_rout = (uint8_t*)(h_res + res_bytes + 2 * al256(4 * ns1));
   m.d_pks = d_pks;
+  m.d_rows = d_rows;
   m.d_sig = d_sig;
   m.d_sst = d_sst;
   m.d_msgs = d_msgs;
@@ -2331,7 +2389,7 @@ int sm_advance_launch(lb_ctx* ctx, Slot& sl, bool block) {
                          m.by_index ? (const uint32_t*)m.d_pks : (const uint32_t*)nullptr, d_rsig, d_rst, d_rmsg,
                          d_ridx, d_rreq);
       LB_HIP(hipGetLastError());
-      LB_TRY(run_pipeline(ctx, sl, nr, nr, d_rreq, m.by_index ? nullptr : m.d_pks, nullptr, d_ridx, d_rmsg, nullptr,
+      LB_TRY(run_pipeline(ctx, sl, nr, nr, d_rreq, m.by_index ? m.d_rows : m.d_pks, nullptr, d_ridx, d_rmsg, nullptr,
                           nullptr, m.d_seed, d_rvalid, d_rerr, nullptr, ws, nullptr, d_rsig, d_rst));
       LB_HIP(hipMemcpyAsync(m.h_rout, d_rvalid, nr, hipMemcpyDeviceToHost, sl.st[0]));
       LB_HIP(hipMemcpyAsync(m.h_rout + al256(ns), d_rerr, nr, hipMemcpyDeviceToHost, sl.st[0]));

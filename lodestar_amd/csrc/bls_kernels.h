@@ -90,11 +90,13 @@ struct PkSource {
 };
 // Pubkey k of the call; an index outside the table is a bad pubkey (LB_REQ_BAD_PUBKEY).
 // In a mixed package (index AND bytes given) an index with bit 31 set is row
-// (j & 0x7fffffff) of the call's 96-byte pubkeys (the host checked the rows exist).
+// (j & LB_PK_ROW_MASK) of the call's 96-byte pubkey rows (the host checked the rows
+// exist); bit 30 marks a row holding a 48-byte compressed encoding.
 LB_DEV uint8_t pk_load(g1a& p, const PkSource& s, uint32_t k) {
   if (s.index) {
     const uint32_t j = s.index[k];
-    if ((j & LB_PK_ROW_FLAG) && s.bytes) return g1_deserialize(p, s.bytes + (size_t)(j & ~LB_PK_ROW_FLAG) * 96, 96);
+    if ((j & LB_PK_ROW_FLAG) && s.bytes)
+      return g1_deserialize(p, s.bytes + (size_t)(j & LB_PK_ROW_MASK) * 96, (j & LB_PK_ROW48_FLAG) ? 48u : 96u);
     if (j >= s.table_n) {
       p.inf = true;
       return LB_ST_BAD_ENCODING;
@@ -215,6 +217,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_partial(uint32_t n_pairs, ui
                                                           const fp12* __restrict__ F_all, uint8_t* __restrict__ out576);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_check(uint32_t n, const uint8_t* __restrict__ in576,
                                                            uint8_t* __restrict__ out);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_prod(uint32_t n, const uint8_t* __restrict__ in576,
+                                                          uint32_t* __restrict__ out16, uint8_t* __restrict__ out);
 __global__ void __launch_bounds__(TPB) k_same_message_agg(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
                                                           const g2j* __restrict__ sig,
                                                           const uint8_t* __restrict__ sig_status,

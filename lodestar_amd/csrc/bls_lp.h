@@ -35,7 +35,11 @@
 #define LB_LP_PROG_SET_BATCH 1
 #define LB_LP_PROG_MUL 2
 #define LB_LP_PROG_FINAL 3
-#define LB_LP_NPROGS 4
+#define LB_LP_PROG_MTAIL_CHECK 4    // the throughput pipeline's merged check (lpgen/bls.py mtail_program)
+#define LB_LP_PROG_MTAIL_PARTIAL 5  // ... its two-phase form: the shard's partial
+#define LB_LP_PROG_FINAL_LANE 6     // final exponentiation == 1 of a one-lane Fp12 (lb_gt_check)
+#define LB_LP_NPROGS 7
+#define LB_MTAIL_NIN (12 + 6 * LB_MSM_POS)  // mtail inputs: the Horner value, the MSM's 33 bit sums
 
 namespace lb {
 // k_lp.hip: instance b (one workgroup of LB_LP_TPB threads) runs the round program at
@@ -74,4 +78,19 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
                                                  uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
                                                  uint32_t* __restrict__ set_req);
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c);
+// The throughput pipeline's merged check as a round program (one workgroup): in16 =
+// LB_MTAIL_NIN records (k_mtail_prep); mflag (check program): [0] = final_exp == 1;
+// out16 (partial program): the shard's partial, 12 records in the one-lane form.
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restrict__ prog,
+                                                        const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
+                                                        uint32_t* __restrict__ out16);
+// final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
+                                                             const uint32_t* __restrict__ in16,
+                                                             uint8_t* __restrict__ out);
+// in16 of the merged check: the Horner value F (one-lane fp12) and the MSM's bit sums G
+__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ F, const g2j* __restrict__ G,
+                                                    uint32_t* __restrict__ in16);
+// 12 records of one-lane limbs -> fp12
+__global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F);
 }  // namespace lb

@@ -646,6 +646,52 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
   }
 }
 
+// The throughput pipeline's merged check (bls_host.hip run_pipeline: steps organisation
+// with the bucket MSM): S_all from the MSM's bit sums, Miller(-g1, S_all) times the
+// Horner value of the call's level products, final exponentiation -- ~880 rounds on one
+// workgroup instead of the one-lane msm_final (1.5 ms) + lines of S_all (3.4 ms) + the
+// one-wave final exponentiation (3.1 ms) on every call's serial tail.
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restrict__ prog,
+                                                        const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
+                                                        uint32_t* __restrict__ out16) {
+  __shared__ LpShared S;
+  __shared__ uint32_t s_fl[4];
+  lp_run(S, prog, in16, 0xffffffffu, in16, nullptr, out16, s_fl);
+  __syncthreads();
+  if (mflag && threadIdx.x == 0) mflag[0] = s_fl[0] ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
+                                                             const uint32_t* __restrict__ in16,
+                                                             uint8_t* __restrict__ out) {
+  __shared__ LpShared S;
+  __shared__ uint32_t s_fl[4];
+  lp_run(S, prog, in16, 0xffffffffu, in16, nullptr, nullptr, s_fl);
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = s_fl[0] ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ F, const g2j* __restrict__ G,
+                                                    uint32_t* __restrict__ in16) {
+  const uint32_t i = threadIdx.x;
+  if (i >= LB_MTAIL_NIN) return;
+  // (fp12: 12 fp in the order c0.c0.c0 ... c1.c2.c1; g2j: X.c0, X.c1, Y.c0, Y.c1, Z.c0, Z.c1)
+  const fp v = i < 12 ? (&F->c0.c0.c0)[i] : (&G[(i - 12) / 6].X.c0)[(i - 12) % 6];
+#pragma unroll
+  for (int j = 0; j < 12; j++) in16[16 * i + j] = v.l[j];
+#pragma unroll
+  for (int j = 12; j < 16; j++) in16[16 * i + j] = 0u;
+}
+
+__global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {
+  const uint32_t i = threadIdx.x;
+  if (i >= 12) return;
+  fp v;
+#pragma unroll
+  for (int j = 0; j < 12; j++) v.l[j] = in16[16 * i + j];
+  (&F->c0.c0.c0)[i] = v;
+}
+
 // Test / stage entry: instance b runs `prog` on in[b * in_stride ...].
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_program(const uint32_t* __restrict__ prog, uint32_t n,
                                                           const uint32_t* __restrict__ in, uint32_t in_stride,

@@ -138,6 +138,39 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_check(uint32_t n, const u
   }
 }
 
+// The product of n partials (as k_gt_check) as 12 records of one-lane limbs for the
+// round-program final exponentiation (k_lp_final_lane); out[1] = 1 when a coefficient
+// is not < p (the product is then invalid).
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_gt_prod(uint32_t n, const uint8_t* __restrict__ in576,
+                                                          uint32_t* __restrict__ out16, uint8_t* __restrict__ out) {
+  __shared__ wc_smem S;
+  __shared__ uint32_t bad;
+  if (threadIdx.x == 0) bad = 0;
+  wc_init_tables(S);
+  wc_set_one(S, WC_ACC);
+  for (uint32_t i = 0; i < n; i++) {
+    if (threadIdx.x < 12) {
+      fp v;
+      if (!fp_read_masked(v, in576 + (size_t)i * 576 + 48 * threadIdx.x, false)) {
+        atomicOr(&bad, 1u);
+        fp_zero(v);
+      }
+      S.slot[WC_B][threadIdx.x] = v;
+    }
+    __syncthreads();
+    wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_B);
+  }
+  if (threadIdx.x < 12) {
+    const fp v = S.slot[WC_ACC][threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < 12; j++) out16[16 * threadIdx.x + j] = v.l[j];
+#pragma unroll
+    for (int j = 12; j < 16; j++) out16[16 * threadIdx.x + j] = 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) out[1] = bad ? 1 : 0;
+}
+
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_merge(uint32_t n_req, const g2a* __restrict__ S,
                                                         const fp12* __restrict__ F,
                                                         const uint8_t* __restrict__ req_bad,

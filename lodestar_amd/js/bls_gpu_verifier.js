@@ -24,10 +24,17 @@
  *
  * Sets: {type: "single", pubkey, signingRoot, signature} or
  *       {type: "aggregate", pubkeys, signingRoot, signature}
- * (ISignatureSet, state-transition/src/util/signatureSets.ts:5-24).  A pubkey is a
- * 96-byte uncompressed Uint8Array, an object with .toBytes() returning one, or
- * {index} -- a validator index into the device pubkey table (syncPubkeys, the
- * index2pubkey mirror of state-transition/src/cache/pubkeyCache.ts:56-77).
+ * (ISignatureSet, state-transition/src/util/signatureSets.ts:5-24).  A pubkey is:
+ *  - a @chainsafe/bls PublicKey, as every reference set builder passes one out of
+ *    index2pubkey (state-transition/src/signatureSets/indexedAttestation.ts:27,
+ *    proposer.ts:28, randao.ts:30, ...).  One mirrored by syncPubkeys (the index2pubkey
+ *    mirror of state-transition/src/cache/pubkeyCache.ts:56-77) ships as its 4-byte
+ *    validator index (an identity map, no serialization on the main thread); any other
+ *    is serialized with toBytes(PointFormat.uncompressed) as the reference does
+ *    (BN/chain/bls/multithread/index.ts:144, jobItem.ts:59);
+ *  - a Uint8Array: the 96-byte uncompressed or the 48-byte compressed encoding
+ *    (compressed keys are decompressed on the GPU: LB_PK_ROW48_FLAG rows);
+ *  - {index}: a validator index into the device pubkey table.
  */
 const crypto = require("crypto");
 const path = require("path");
@@ -41,6 +48,11 @@ const MAX_JOBS_CAN_ACCEPT_WORK = 512; // index.ts:80
 const MAX_PRIORITY_LANE_SETS = 1024;
 const BATCHABLE_MIN_PER_CHUNK = 16; // worker.ts:17
 const LB_PK_ROW_FLAG = 0x80000000;
+const LB_PK_ROW48_FLAG = 0x40000000; // the row holds a 48-byte compressed encoding
+const LB_PK_ROW_MASK = 0x3fffffff;
+// @chainsafe/bls PointFormat (the reference passes PointFormat.uncompressed to toBytes,
+// BN/chain/bls/multithread/index.ts:144 -> jobItem.ts:59,80)
+const PointFormat = {compressed: "compressed", uncompressed: "uncompressed"};
 const LB_REQ_EMPTY_AGGREGATE = 1;
 const LB_REQ_BAD_PUBKEY = 2;
 const GT_BYTES = 576;
@@ -135,22 +147,31 @@ function concat(arrays, total) {
 
 /** Requests (arrays of sets) -> the addon's batch (lb_request_batch layout).  Two passes:
  * count, then fill typed arrays allocated once (no per-set or per-key objects: a 65,536-set
- * package was ~75 ms of main-thread JS with intermediate arrays, the node leg's bound). */
-function packRequests(requests, seed) {
+ * package was ~75 ms of main-thread JS with intermediate arrays, the node leg's bound).
+ * keyMap (optional WeakMap PublicKey -> validator index, BlsGpuVerifier.syncPubkeys) turns
+ * mirrored key objects into indices; every other key is serialized once (first pass). */
+function packRequests(requests, seed, keyMap) {
   let nSets = 0;
   let nKeys = 0;
   let nIdx = 0;
+  let nComp = 0;
   let sigBytes = 0;
+  const rowKeys = []; // encodings of the keys shipped as rows, in order
+  const countKey = (pk) => {
+    if (keyIndex(pk, keyMap) >= 0) nIdx++;
+    else {
+      const b = keyBytes(pk);
+      if (b.length === 48) nComp++;
+      rowKeys.push(b);
+    }
+    nKeys++;
+  };
   for (const req of requests) {
     for (const s of req) {
       if (s.type === "aggregate") {
         const ks = s.pubkeys || [];
-        for (let q = 0; q < ks.length; q++) if (keyIndex(ks[q]) >= 0) nIdx++;
-        nKeys += ks.length;
-      } else {
-        if (keyIndex(s.pubkey) >= 0) nIdx++;
-        nKeys++;
-      }
+        for (let q = 0; q < ks.length; q++) countKey(ks[q]);
+      } else countKey(s.pubkey);
       if (!(s.signingRoot instanceof Uint8Array) || s.signingRoot.length !== 32)
         throw new TypeError("signingRoot must be 32 bytes");
       sigBytes += s.signature.length;
@@ -163,23 +184,25 @@ function packRequests(requests, seed) {
   const messages = new Uint8Array(32 * nSets);
   const signatures = new Uint8Array(sigBytes);
   // all keys by validator index; a mixed package (a capella block's BLS-change keys beside
-  // validator keys): indices plus flagged indices naming rows of the shipped 96-byte keys
-  // (LB_PK_ROW_FLAG); no index at all: the 96-byte encodings
-  const idx = nIdx > 0 ? new Uint32Array(nKeys) : null;
-  const rowsN = nIdx > 0 ? nKeys - nIdx : nKeys;
-  const rows = rowsN > 0 ? new Uint8Array(96 * rowsN) : null;
+  // validator keys, or compressed keys): indices plus flagged indices naming rows of the
+  // shipped keys (LB_PK_ROW_FLAG, LB_PK_ROW48_FLAG for a compressed row); no index and no
+  // compressed key: the 96-byte encodings
+  const mixed = nIdx > 0 || nComp > 0;
+  const idx = mixed ? new Uint32Array(nKeys) : null;
+  const rows = rowKeys.length > 0 ? new Uint8Array(96 * rowKeys.length) : null;
   let k = 0;
   let row = 0;
   let i = 0;
   let so = 0;
   const putKey = (pk) => {
-    const ix = keyIndex(pk);
+    const ix = keyIndex(pk, keyMap);
     if (ix >= 0) {
       idx[k++] = ix;
       return;
     }
-    rows.set(keyBytes(pk), 96 * row);
-    if (idx) idx[k] = (LB_PK_ROW_FLAG | row) >>> 0;
+    const b = rowKeys[row];
+    rows.set(b, 96 * row);
+    if (idx) idx[k] = (LB_PK_ROW_FLAG | (b.length === 48 ? LB_PK_ROW48_FLAG : 0) | row) >>> 0;
     k++;
     row++;
   };
@@ -206,56 +229,75 @@ function packRequests(requests, seed) {
   return batch;
 }
 
-/** A key's validator index, or -1 for a key given by its bytes (a 96-byte uncompressed encoding,
- * or an object with toBytes()). */
-function keyIndex(pk) {
-  if (pk && typeof pk.index === "number" && !(pk instanceof Uint8Array)) return pk.index;
+/** A key's validator index, or -1 for a key shipped by its bytes (a 96- or 48-byte
+ * encoding, or a PublicKey object that syncPubkeys has not mirrored). */
+function keyIndex(pk, keyMap) {
   if (pk instanceof Uint8Array) {
-    if (pk.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
+    if (pk.length !== 96 && pk.length !== 48) throw new TypeError("pubkey: 96-byte uncompressed or 48-byte compressed encoding");
     return -1;
   }
-  if (pk && typeof pk.toBytes === "function") return -1;
-  throw new TypeError("pubkey: Uint8Array(96), {index} or an object with toBytes()");
+  if (pk && typeof pk === "object") {
+    if (keyMap) {
+      const ix = keyMap.get(pk);
+      if (ix !== undefined) return ix;
+    }
+    if (typeof pk.index === "number") return pk.index;
+    if (typeof pk.toBytes === "function") return -1;
+  }
+  throw new TypeError("pubkey: a PublicKey (toBytes(format)), Uint8Array(96 | 48) or {index}");
 }
 
+/** The encoding of a key shipped by its bytes: a PublicKey serialized as the reference does,
+ * toBytes(PointFormat.uncompressed) (index.ts:144, jobItem.ts:59); an implementation that
+ * returns its compressed form instead is taken as such (decompressed on the GPU). */
 function keyBytes(pk) {
-  const b = pk instanceof Uint8Array ? pk : pk.toBytes(false);
-  if (!(b instanceof Uint8Array) || b.length !== 96) throw new TypeError("pubkey: 96-byte uncompressed encoding");
+  const b = pk instanceof Uint8Array ? pk : pk.toBytes(PointFormat.uncompressed);
+  if (!(b instanceof Uint8Array) || (b.length !== 96 && b.length !== 48))
+    throw new TypeError("pubkey: toBytes() must return a 96-byte uncompressed or 48-byte compressed encoding");
   return b;
 }
 
-/** Same-message jobs -> the addon's lb_same_message_batch layout. */
-function packSameMessage(jobs, seed) {
+/** Same-message jobs -> the addon's lb_same_message_batch layout (keys as packRequests:
+ * mirrored key objects by index; the rest by their encodings). */
+function packSameMessage(jobs, seed, keyMap) {
   let nSets = 0;
   let nIdx = 0;
+  let nComp = 0;
   let sigBytes = 0;
+  const rowKeys = [];
   for (const job of jobs) {
     for (const s of job.sets) {
-      if (keyIndex(s.publicKey) >= 0) nIdx++;
+      if (keyIndex(s.publicKey, keyMap) >= 0) nIdx++;
+      else {
+        const b = keyBytes(s.publicKey);
+        if (b.length === 48) nComp++;
+        rowKeys.push(b);
+      }
       sigBytes += s.signature.length;
       nSets++;
     }
   }
-  const byIndex = nSets > 0 && nIdx === nSets;
+  // every key by index, every key by its 96 bytes, or a mixed package (flagged rows)
+  const mixed = nIdx > 0 || nComp > 0;
   const jobOff = new Uint32Array(jobs.length + 1);
   const sigOff = new Uint32Array(nSets + 1);
   const signatures = new Uint8Array(sigBytes);
   const messages = new Uint8Array(32 * jobs.length);
-  const idx = byIndex ? new Uint32Array(nSets) : null;
-  const pks = byIndex ? null : new Uint8Array(96 * nSets);
+  const idx = mixed ? new Uint32Array(nSets) : null;
+  const pks = rowKeys.length > 0 ? new Uint8Array(96 * rowKeys.length) : null;
   let i = 0;
   let so = 0;
+  let row = 0;
   for (let j = 0; j < jobs.length; j++) {
     messages.set(jobs[j].message, 32 * j);
     for (const s of jobs[j].sets) {
-      if (byIndex) idx[i] = keyIndex(s.publicKey);
+      const ix = keyIndex(s.publicKey, keyMap);
+      if (ix >= 0) idx[i] = ix;
       else {
-        const pk = s.publicKey;
-        // (a key by index alone in a package with byte keys: its bytes are needed)
-        const b = pk instanceof Uint8Array || typeof pk.toBytes === "function" ? keyBytes(pk) : pk.bytes;
-        if (!(b instanceof Uint8Array) || b.length !== 96)
-          throw new TypeError("same-message package mixing index-only and byte pubkeys");
-        pks.set(b, 96 * i);
+        const b = rowKeys[row];
+        pks.set(b, 96 * row);
+        if (idx) idx[i] = (LB_PK_ROW_FLAG | (b.length === 48 ? LB_PK_ROW48_FLAG : 0) | row) >>> 0;
+        row++;
       }
       signatures.set(s.signature, so);
       so += s.signature.length;
@@ -265,8 +307,8 @@ function packSameMessage(jobs, seed) {
     jobOff[j + 1] = i;
   }
   const batch = {jobOffsets: jobOff, signatures, sigOffsets: sigOff, messages, seed};
-  if (byIndex) batch.pubkeyIndices = idx;
-  else batch.pubkeys = pks;
+  if (idx) batch.pubkeyIndices = idx;
+  if (pks) batch.pubkeys = pks;
   return batch;
 }
 
@@ -332,6 +374,24 @@ const M = {
   SINGLE_THREAD_TIME_PER_SIGSET: "lodestar_bls_single_thread_time_per_sigset_seconds",
 };
 
+/** Append keys to every backend's pubkey table; PublicKey objects are serialized with
+ * toBytes(format) and mapped to their table index in keyMap.  Returns the table size. */
+async function syncKeyTables(backends, keyMap, keys, pkLen) {
+  if (pkLen !== 48 && pkLen !== 96) throw new TypeError("syncPubkeys: pkLen 48 or 96");
+  const fmt = pkLen === 96 ? PointFormat.uncompressed : PointFormat.compressed;
+  const enc = keys.map((k) => (k instanceof Uint8Array ? k : k.toBytes(fmt)));
+  for (const b of enc)
+    if (!(b instanceof Uint8Array) || b.length !== pkLen) throw new TypeError(`syncPubkeys: ${pkLen}-byte keys`);
+  const blob = concat(enc, keys.length * pkLen);
+  const sizes = await Promise.all(backends.map((b) => b.syncPubkeys(blob, pkLen)));
+  if (new Set(sizes).size !== 1) throw new Error(`pubkey tables out of sync: ${sizes}`);
+  const base = sizes[0] - keys.length;
+  keys.forEach((k, i) => {
+    if (!(k instanceof Uint8Array) && k && typeof k === "object") keyMap.set(k, base + i);
+  });
+  return sizes[0];
+}
+
 function hrNowNs() {
   const [s, ns] = process.hrtime();
   return s * 1e9 + ns;
@@ -381,18 +441,40 @@ class BlsGpuVerifier {
     this.tokens = this.idle.length;
     this.running = new Set();
     this.closed = false;
+    // PublicKey object -> validator index in the GPUs' pubkey tables (syncPubkeys): sets
+    // built from index2pubkey ship 4-byte indices, never serialized keys
+    this.keyMap = new WeakMap();
+    this.tableSize = 0;
+    this.mirror = null;  // syncIndex2pubkey: {base, n} of the index2pubkey mirror in the tables
   }
 
   canAcceptWork() {
     return this.idle.length > 0 && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
   }
 
-  /** index2pubkey mirror on every GPU (pubkeyCache.ts:56-77): keys 48-byte compressed. */
+  /** Append keys to the pubkey table of every GPU (the index2pubkey mirror,
+   * pubkeyCache.ts:56-77) and return the table size.  keys: @chainsafe/bls PublicKey
+   * objects (serialized once here with toBytes(format); each object then maps to its
+   * table index, so sets built from it ship the index) or pkLen-byte encodings
+   * (48 compressed, as the state holds them, or 96 uncompressed). */
   async syncPubkeys(keys, pkLen = 48) {
-    const blob = concat(keys, keys.length * pkLen);
-    const sizes = await Promise.all(this.backends.map((b) => b.syncPubkeys(blob, pkLen)));
-    if (new Set(sizes).size !== 1) throw new Error(`pubkey tables out of sync: ${sizes}`);
-    return sizes[0];
+    this.tableSize = await syncKeyTables(this.backends, this.keyMap, keys, pkLen);
+    return this.tableSize;
+  }
+
+  /** pubkeyCache.syncPubkeys (pubkeyCache.ts:56-77) for the GPUs: mirror the entries of
+   * index2pubkey (PublicKey objects) not mirrored yet -- index2pubkey[i] maps to table
+   * entry base + i, where base is the table size at the first call -- and return the
+   * number of entries mirrored.  Call it wherever the node calls syncPubkeys. */
+  async syncIndex2pubkey(index2pubkey) {
+    if (!this.mirror) this.mirror = {base: this.tableSize, n: 0};
+    const m = this.mirror;
+    if (this.tableSize !== m.base + m.n) throw new Error("the pubkey table grew outside syncIndex2pubkey");
+    if (index2pubkey.length > m.n) {
+      await this.syncPubkeys(index2pubkey.slice(m.n), 48);
+      m.n = index2pubkey.length;
+    }
+    return m.n;
   }
 
   async verifySignatureSets(sets, opts = {}) {
@@ -406,7 +488,7 @@ class BlsGpuVerifier {
       // not block the event loop, unlike blst on the reference's main thread)
       const t0 = process.hrtime();
       try {
-        const batch = packRequests([sets], this.seedSource());
+        const batch = packRequests([sets], this.seedSource(), this.keyMap);
         const r = await this.backends[0].verifyRequests(batch, this.priorityLane ? {priority: true} : undefined);
         return this.requestVerdict(r, 0);
       } finally {
@@ -592,7 +674,7 @@ class BlsGpuVerifier {
         // the main thread's share of pubkey aggregation (jobItem.ts:55-63 / utils.ts:12):
         // packing the keys; the sum itself runs on the GPU
         const t0 = process.hrtime();
-        const batch = packRequests(def.map((j) => j.sets), this.seedSource());
+        const batch = packRequests(def.map((j) => j.sets), this.seedSource(), this.keyMap);
         const [s0, ns0] = process.hrtime(t0);
         if (def.some((j) => j.sets.some((x) => x.type === "aggregate")))
           m.observe(M.PUBKEYS_AGGREGATION_MAIN_THREAD, s0 + ns0 / 1e9);
@@ -604,7 +686,7 @@ class BlsGpuVerifier {
         // jobItem.ts:72-74 times Signature.fromBytes on the main thread; here the bytes are
         // only packed (every signature is decoded once, on the GPU)
         const t0 = process.hrtime();
-        const batch = packSameMessage(same, this.seedSource());
+        const batch = packSameMessage(same, this.seedSource(), this.keyMap);
         const [s0, ns0] = process.hrtime(t0);
         m.observe(M.SIG_DESERIALIZATION_MAIN_THREAD, s0 + ns0 / 1e9);
         waits.push(backend.verifySameMessage(batch));
@@ -697,6 +779,17 @@ class BlsGpuSingleThreadVerifier {
     this.backend = o.backend || new (loadAddon().Context)(o.device || 0);
     this.seedSource = o.seedSource || (() => new Uint8Array(crypto.randomBytes(32)));
     this.metrics = o.metrics || new PoolMetrics();
+    this.keyMap = new WeakMap();
+    this.tableSize = 0;
+    this.mirror = null;
+  }
+  /** as BlsGpuVerifier.syncPubkeys / syncIndex2pubkey, on this verifier's one GPU */
+  async syncPubkeys(keys, pkLen = 48) {
+    this.tableSize = await syncKeyTables([this.backend], this.keyMap, keys, pkLen);
+    return this.tableSize;
+  }
+  async syncIndex2pubkey(index2pubkey) {
+    return BlsGpuVerifier.prototype.syncIndex2pubkey.call(this, index2pubkey);
   }
   /** singleThread.ts:27-35 times the verification (mainThreadDurationInThreadPool); the
    * single-thread histograms of lodestar.ts:498-508 get the same duration, and per set. */
@@ -709,7 +802,7 @@ class BlsGpuSingleThreadVerifier {
   }
   async verifySignatureSets(sets) {
     const t0 = process.hrtime();
-    const r = await this.backend.verifyRequests(packRequests([sets], this.seedSource()));
+    const r = await this.backend.verifyRequests(packRequests([sets], this.seedSource(), this.keyMap));
     if (r.errors[0] === LB_REQ_EMPTY_AGGREGATE) throw new Error("EMPTY_AGGREGATE_ARRAY");
     if (r.errors[0] === LB_REQ_BAD_PUBKEY) throw new Error("invalid pubkey encoding");
     this.observe(t0, sets.length); // counted only for runs without an exception, as the reference
@@ -718,7 +811,7 @@ class BlsGpuSingleThreadVerifier {
   async verifySignatureSetsSameMessage(sets, message) {
     if (sets.length === 0) throw new Error("EMPTY_AGGREGATE_ARRAY"); // PublicKey.aggregate([]) throws (singleThread.ts:43)
     const t0 = process.hrtime();
-    const r = await this.backend.verifySameMessage(packSameMessage([{sets, message}], this.seedSource()));
+    const r = await this.backend.verifySameMessage(packSameMessage([{sets, message}], this.seedSource(), this.keyMap));
     this.observe(t0, sets.length);
     return Array.from(r.valid.subarray(0, sets.length), (v) => v === 1);
   }
@@ -791,8 +884,8 @@ function slicePacked(p, lo, hi, seed) {
     const rows = [];
     for (let q = 0; q < idx.length; q++)
       if (idx[q] & LB_PK_ROW_FLAG) {
-        rows.push(idx[q] & ~LB_PK_ROW_FLAG);
-        idx[q] = (LB_PK_ROW_FLAG | (rows.length - 1)) >>> 0;
+        rows.push(idx[q] & LB_PK_ROW_MASK);
+        idx[q] = (LB_PK_ROW_FLAG | (idx[q] & LB_PK_ROW48_FLAG) | (rows.length - 1)) >>> 0;
       }
     out.pubkeyIndices = idx;
     if (rows.length) {
@@ -869,4 +962,7 @@ module.exports = {
   MAX_BUFFER_WAIT_MS,
   MAX_JOBS_CAN_ACCEPT_WORK,
   MAX_PRIORITY_LANE_SETS,
+  PointFormat,
+  LB_PK_ROW_FLAG,
+  LB_PK_ROW48_FLAG,
 };

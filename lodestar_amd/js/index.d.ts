@@ -1,13 +1,22 @@
 // Type declarations for lodestar_amd/js/bls_gpu_verifier.js: the GPU verifier as a
-// Lodestar IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:4-75), so a
+// Lodestar IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:4-68), so a
 // TypeScript beacon node can construct it where chain.ts:206-208 picks the bls pool.
 // Signature sets follow @lodestar/state-transition's ISignatureSet
 // (packages/state-transition/src/util/signatureSets.ts:5-24); a pubkey may be given by
 // validator index ({index}) once syncPubkeys() has mirrored index2pubkey on the GPUs.
 
-/** A public key: its validator index in the GPUs' mirror of index2pubkey, its 96-byte
- * uncompressed encoding, or a @chainsafe/bls PublicKey (anything with toBytes(false)). */
-export type GpuPublicKey = {index: number} | Uint8Array | {toBytes(compressed?: boolean): Uint8Array};
+/** @chainsafe/bls PointFormat (the reference serializes with PointFormat.uncompressed,
+ * BN/chain/bls/multithread/index.ts:144 -> jobItem.ts:59). */
+export type PointFormat = "compressed" | "uncompressed";
+export const PointFormat: {compressed: "compressed"; uncompressed: "uncompressed"};
+/** The shape of a @chainsafe/bls PublicKey this verifier needs: toBytes(format) returns the
+ * compressed 48-byte encoding unless format is "uncompressed" (96 bytes). */
+export type PublicKeyLike = {toBytes(format?: PointFormat): Uint8Array};
+/** A public key: a @chainsafe/bls PublicKey (as index2pubkey holds them; shipped as its
+ * validator index once syncPubkeys/syncIndex2pubkey mirrored it, else serialized with
+ * toBytes("uncompressed")), its 96-byte uncompressed or 48-byte compressed encoding, or
+ * {index}: a validator index into the GPUs' pubkey tables. */
+export type GpuPublicKey = PublicKeyLike | Uint8Array | {index: number};
 
 /** signatureSets.ts:5-24 */
 export type SingleSignatureSet = {
@@ -118,8 +127,12 @@ export class BlsGpuVerifier implements IBlsVerifier {
   constructor(opts?: BlsGpuVerifierOpts);
   readonly capacity: number;
   readonly metrics: PoolMetrics;
-  /** index2pubkey mirror on every GPU (pubkeyCache.ts:56-77); returns the table size */
-  syncPubkeys(keys: Uint8Array[], pkLen?: 48 | 96): Promise<number>;
+  /** Append keys to every GPU's pubkey table (pubkeyCache.ts:56-77); PublicKey objects are
+   * serialized once here and then ship as their table index.  Returns the table size. */
+  syncPubkeys(keys: (Uint8Array | PublicKeyLike)[], pkLen?: 48 | 96): Promise<number>;
+  /** pubkeyCache.syncPubkeys for the GPUs: mirror index2pubkey's new entries (incremental);
+   * returns the number of entries mirrored. */
+  syncIndex2pubkey(index2pubkey: PublicKeyLike[]): Promise<number>;
   verifySignatureSets(sets: ISignatureSet[], opts?: VerifySignatureOpts): Promise<boolean>;
   verifySignatureSetsSameMessage(
     sets: {publicKey: GpuPublicKey; signature: Uint8Array}[],
@@ -133,6 +146,8 @@ export class BlsGpuVerifier implements IBlsVerifier {
 /** BlsSingleThreadVerifier (chain/bls/singleThread.ts:10-89) on one GPU. */
 export class BlsGpuSingleThreadVerifier implements IBlsVerifier {
   constructor(opts?: {backend?: GpuBackend; device?: number; seedSource?: () => Uint8Array; metrics?: PoolMetrics});
+  syncPubkeys(keys: (Uint8Array | PublicKeyLike)[], pkLen?: 48 | 96): Promise<number>;
+  syncIndex2pubkey(index2pubkey: PublicKeyLike[]): Promise<number>;
   verifySignatureSets(sets: ISignatureSet[]): Promise<boolean>;
   verifySignatureSetsSameMessage(
     sets: {publicKey: GpuPublicKey; signature: Uint8Array}[],
@@ -163,10 +178,15 @@ export function workerBatchStats(
   batchable: boolean[],
   valid: boolean[]
 ): {retries: number; sigsOk: number};
-export function packRequests(requests: ISignatureSet[][], seed: Uint8Array): PackedRequests;
+export function packRequests(
+  requests: ISignatureSet[][],
+  seed: Uint8Array,
+  keyMap?: WeakMap<object, number>
+): PackedRequests;
 export function packSameMessage(
   jobs: {sets: {publicKey: GpuPublicKey; signature: Uint8Array}[]; message: Uint8Array}[],
-  seed: Uint8Array
+  seed: Uint8Array,
+  keyMap?: WeakMap<object, number>
 ): SameMessageBatch;
 export function shardRequests(sizes: number[], nShards: number): [number, number][];
 export function slicePacked(p: PackedRequests, lo: number, hi: number, seed: Uint8Array): PackedRequests;
@@ -191,3 +211,6 @@ export const MAX_BUFFERED_SIGS: 32;
 export const MAX_BUFFER_WAIT_MS: 100;
 export const MAX_JOBS_CAN_ACCEPT_WORK: 512;
 export const MAX_PRIORITY_LANE_SETS: 1024;
+/** lb_request_batch / lb_same_message_batch pubkeyIndices flags (include/lodestar_bls.h) */
+export const LB_PK_ROW_FLAG: 0x80000000;
+export const LB_PK_ROW48_FLAG: 0x40000000;

@@ -17,6 +17,14 @@ agree point for point:
 * ``mul_program``: the product of two Miller values (the request's product
   tree across its sets' workgroups).
 * ``final_program``: final exponentiation == 1 (the request's verdict).
+* ``mtail_program(partial)``: the throughput pipeline's merged check of a whole
+  call (the worker's merged batch, BN/chain/bls/multithread/worker.ts:41-96):
+  S_all = sum_p 2^p G_p from the bucket MSM's 33 bit sums (k_msm.hip), the
+  Miller value of (-g1, S_all), times the call's level-product Horner value,
+  then the final exponentiation == 1 -- or, for a two-phase (multi-GPU) call,
+  the product itself as the shard's partial.
+* ``final_lane_program``: final exponentiation == 1 of a one-lane Fp12 (the
+  host combine of the shards' partials, lb_gt_check).
 """
 from __future__ import annotations
 
@@ -25,7 +33,7 @@ import os
 
 from .dsl import Flag, Fp, Graph, P, select, select_n
 from .tower import (P34, Fp2, Fp6, Fp12, Jac, Ops, Proj, fp2_lex_largest, fp2_sgn0, fp_pow, jac_add, jac_add_aff,
-                    proj_add, proj_dbl, proj_eq, proj_from_jac, proj_mul_xabs,
+                    proj_add, proj_dbl, proj_eq, proj_from_jac, proj_mul_xabs, R384_RAW,
                     jac_dbl, jac_eq, jac_inf, jsel, line_mul_line)
 
 X_ABS = 0xD201000000010000
@@ -697,5 +705,79 @@ def mul_program() -> Graph:
 def final_program() -> Graph:
     g = Graph("final_exp")
     f = Fp12.from_fps([g.input_raw("f%d" % k) for k in range(12)])
+    g.output_flag("is_one", final_exp(f).is_one())
+    return g
+
+
+# ---------------------------------------------------------------------------
+# the throughput pipeline's merged check (bls_host.hip run_pipeline, steps + MSM)
+# ---------------------------------------------------------------------------
+MSM_POS = 33  # k_msm.hip LB_MSM_POS: bit positions of the MSM's reduction
+
+
+def miller1(q: Proj, void: Flag) -> Fp12:
+    """Miller value of the one pair (-g1, Q), Q homogeneous (conj(f_{|x|,Q}(-g1)), x < 0),
+    up to factors the final exponentiation kills; void (Q = O): 1.  -g1 is a constant
+    affine point, so its line coordinates enter as constants."""
+    g = q.X.g
+    P1 = g1_line_point(Jac(g.const(C["LB_G1_X"]), g.const(C["LB_G1_NEG_Y"]), g.one()))
+    Q = g2_homogeneous(q)
+    T = Q
+    f = None
+    for i in range(62, -1, -1):
+        T, ln = miller_dbl_step(T, P1)
+        l0, l1, l4 = unit_line(g, void, ln)
+        if f is None:
+            f = Fp12(Fp6(l0, l1, Fp2.zero(g)), Fp6(Fp2.zero(g), l4, Fp2.zero(g)))
+        else:
+            f = f.sqr().mat().mul_line(l0, l1, l4).mat()
+        if (X_ABS >> i) & 1:
+            T, ln = miller_add_step(T, Q, P1)
+            f = f.mul_line(*unit_line(g, void, ln)).mat()
+    return f.conj()
+
+
+def msm_sum(pts) -> Proj:
+    """sum_p 2^p G_p (Horner from the top position), complete homogeneous formulas"""
+    F = Ops(pts[0].X.g, True)
+    acc = pts[-1]
+    for p in range(len(pts) - 2, -1, -1):
+        acc = proj_add(F, proj_dbl(F, acc), pts[p])
+    return acc
+
+
+MTAIL_INPUTS = ["h%d" % k for k in range(12)] + ["G%d_%s" % (p, c) for p in range(MSM_POS)
+                                                 for c in ("X0", "X1", "Y0", "Y1", "Z0", "Z1")]
+
+
+def mtail_program(partial: bool) -> Graph:
+    """inputs: the call's Horner value conj(prod_l P_l^(2^(62-l))) over its good requests'
+    lane values (k_horner_all) and the MSM's 33 bit sums G_p (Jacobian G2, one-lane
+    Montgomery form); S_all = sum 2^p G_p; f = Horner value * Miller(-g1, S_all).
+    check: output flag is_one = (final_exp(f) == 1).  partial: f as 12 canonical Fp in
+    the one-lane form (R = 2^384), the shard's 576-byte partial before encoding."""
+    g = Graph("mtail_partial" if partial else "mtail_check")
+    v = [g.input(n) for n in MTAIL_INPUTS]
+    h = Fp12.from_fps(v[:12])
+    pts = []
+    zero, one = Fp2.zero(g), Fp2.one(g)
+    for p in range(MSM_POS):
+        X, Y, Z = (Fp2(v[12 + 6 * p + 2 * c], v[12 + 6 * p + 2 * c + 1]) for c in range(3))
+        pts.append(select(Z.is_zero(), Proj(zero, one, zero), proj_from_jac(Jac(X, Y, Z))))
+    S = msm_sum(pts)
+    f = (h * miller1(S, S.Z.is_zero())).mat()
+    if partial:
+        r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+        for k, x in enumerate(f.fps()):
+            g.output("f%d" % k, x * r384, canonical=True)
+    else:
+        g.output_flag("is_one", final_exp(f).is_one())
+    return g
+
+
+def final_lane_program() -> Graph:
+    """final exponentiation == 1 of a one-lane Fp12 (canonical, R = 2^384)"""
+    g = Graph("final_exp_lane")
+    f = Fp12.from_fps([g.input("f%d" % k) for k in range(12)])
     g.output_flag("is_one", final_exp(f).is_one())
     return g

@@ -625,3 +625,6 @@ def proj_eq(F: Ops, p: Proj, q: Proj) -> Flag:
 
 
 X_ABS_T = 0xD201000000010000
+# 2^384 mod p as a raw register: x * R384_RAW / 2^416 takes this domain's x back to the
+# one-lane code's Montgomery form (R = 2^384)
+R384_RAW = (1 << 384) % 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB

@@ -222,7 +222,7 @@ void parse_requests(napi_env env, napi_value obj, Task& t) {
     size_t rows = 0;
     const uint32_t* ix = t.v_pk_idx.data();
     for (size_t q = 0; q < n_pk; q++)
-      if ((ix[q] & LB_PK_ROW_FLAG) && (size_t)(ix[q] & ~LB_PK_ROW_FLAG) + 1 > rows) rows = (ix[q] & ~LB_PK_ROW_FLAG) + 1;
+      if ((ix[q] & LB_PK_ROW_FLAG) && (size_t)(ix[q] & LB_PK_ROW_MASK) + 1 > rows) rows = (ix[q] & LB_PK_ROW_MASK) + 1;
     t.mixed = has_keys;
     if (rows && (!t.mixed || t.v_pubkeys.size() < rows * LB_PUBKEY_BYTES))
       throw ArgError{"pubkeyIndices name pubkey rows that `pubkeys` does not hold"};
@@ -450,7 +450,7 @@ void worker_loop(Context* c) {
         b.n_jobs = t->n_jobs;
         b.n_sets = t->n_sets;
         b.job_offsets = t->job_off.data();
-        b.pubkeys = t->by_index ? nullptr : t->pubkeys.data();
+        b.pubkeys = (t->by_index && !t->mixed) ? nullptr : t->pubkeys.data();
         b.pubkey_indices = t->by_index ? t->pk_idx.data() : nullptr;
         b.signatures = t->signatures.data();
         b.sig_offsets = t->sig_off.data();
@@ -789,6 +789,13 @@ napi_value VerifySameMessage(napi_env env, napi_callback_info info) {
     t->by_index = opt_typed(env, o, "pubkeyIndices", napi_uint32_array, t->pk_idx);
     if (t->by_index) {
       if (t->pk_idx.size() != t->n_sets) throw ArgError{"pubkeyIndices: one per set"};
+      // mixed package: rows of `pubkeys` named by indices with LB_PK_ROW_FLAG set
+      size_t rows = 0;
+      for (uint32_t j : t->pk_idx)
+        if ((j & LB_PK_ROW_FLAG) && (size_t)(j & LB_PK_ROW_MASK) + 1 > rows) rows = (j & LB_PK_ROW_MASK) + 1;
+      t->mixed = opt_typed(env, o, "pubkeys", napi_uint8_array, t->pubkeys);
+      if (rows && (!t->mixed || t->pubkeys.size() < rows * LB_PUBKEY_BYTES))
+        throw ArgError{"pubkeyIndices name pubkey rows that `pubkeys` does not hold"};
     } else {
       if (!opt_typed(env, o, "pubkeys", napi_uint8_array, t->pubkeys) && t->n_sets)
         throw ArgError{"missing pubkeys (or pubkeyIndices)"};

@@ -46,6 +46,8 @@ EXPORTED_SYMBOLS = (
 LB_BATCH_DEVICE = 1
 LB_GT_BYTES = 576
 LB_PK_ROW_FLAG = 0x80000000  # mixed packages: an index naming a row of the call's 96-byte pubkeys
+LB_PK_ROW48_FLAG = 0x40000000  # ... whose row holds a 48-byte compressed encoding
+LB_PK_ROW_MASK = 0x3FFFFFFF
 
 
 class LodestarBlsError(RuntimeError):
@@ -384,9 +386,10 @@ class Device:
         self._check(self.lib.lb_gt_check(self._h, len(partials), _ptr(blob), ctypes.byref(out)), "lb_gt_check")
         return bool(out.value)
 
-    def _same_message_batch(self, jobs, seed: bytes, by_index: bool):
+    def _same_message_batch(self, jobs, seed: bytes, by_index: bool, rows=None):
         """The lb_same_message_batch of a package, its output arrays and the
-        input arrays the library reads (kept alive until the call retires)."""
+        input arrays the library reads (kept alive until the call retires).  rows (with
+        by_index): a mixed package's 96-byte key rows, named by LB_PK_ROW_FLAG indices."""
         nj = len(jobs)
         job_off = np.zeros(nj + 1, np.uint32)
         for j, (pks, sigs, msg) in enumerate(jobs):
@@ -401,7 +404,7 @@ class Device:
         if by_index:
             idx = (np.concatenate([np.asarray(pks, dtype=np.uint32).reshape(-1) for pks, _, _ in jobs])
                    if ns else np.zeros(1, np.uint32))
-            pk = None
+            pk = _u8(rows) if rows is not None else None
         else:
             pk = _u8(b"".join(bytes(k) for pks, _, _ in jobs for k in pks) or b"\0")
             idx = None
@@ -421,7 +424,8 @@ class Device:
         return res, fast[:nj].astype(bool).tolist(), (int(st.batch_retries), int(st.batch_sigs_success))
 
     def verify_same_message_batch(self, jobs: Sequence[Tuple[Sequence, Sequence[bytes], bytes]], seed: bytes,
-                                  by_index: bool = False) -> Tuple[List[List[bool]], List[bool], Tuple[int, int]]:
+                                  by_index: bool = False,
+                                  rows=None) -> Tuple[List[List[bool]], List[bool], Tuple[int, int]]:
         """jobs: (pubkeys, signatures, message) per same-message job; pubkeys are
         96-byte encodings, or validator indices when by_index.  Returns per-set
         verdicts per job, the per-job fast-path flags and (retried jobs, sets
@@ -429,7 +433,7 @@ class Device:
         nj = len(jobs)
         if nj == 0:
             return [], [], (0, 0)
-        b, out, fast, job_off, keep = self._same_message_batch(jobs, seed, by_index)
+        b, out, fast, job_off, keep = self._same_message_batch(jobs, seed, by_index, rows)
         st = _Stats()
         rc = self.lib.lb_verify_same_message_batch(self._h, ctypes.byref(b), _ptr(out), _ptr(fast), ctypes.byref(st))
         self._check(rc, "lb_verify_same_message_batch")

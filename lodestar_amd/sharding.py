@@ -85,11 +85,13 @@ class PackedRequests:
         idx, pks = None, None
         if self.idx is not None and self.pks is not None:
             # mixed: keep the rows this slice names, renumbered from 0
-            from .native import LB_PK_ROW_FLAG
+            from .native import LB_PK_ROW48_FLAG, LB_PK_ROW_FLAG, LB_PK_ROW_MASK
             idx = self.idx[ka:kb].astype(np.uint32)
             flagged = (idx & LB_PK_ROW_FLAG) != 0
-            rows = (idx[flagged] & ~np.uint32(LB_PK_ROW_FLAG)).astype(np.int64)
-            idx[flagged] = np.uint32(LB_PK_ROW_FLAG) | np.arange(len(rows), dtype=np.uint32)
+            rows = (idx[flagged] & np.uint32(LB_PK_ROW_MASK)).astype(np.int64)
+            # (a compressed row keeps its LB_PK_ROW48_FLAG)
+            idx[flagged] = (np.uint32(LB_PK_ROW_FLAG) | (idx[flagged] & np.uint32(LB_PK_ROW48_FLAG)) |
+                            np.arange(len(rows), dtype=np.uint32))
             pks = self.pks.reshape(-1, 96)[rows].reshape(-1) if len(rows) else np.zeros(1, np.uint8)
         elif self.idx is not None:
             idx = self.idx[ka:kb]

@@ -308,6 +308,127 @@ test("single-thread verifier", async () => {
   assert(v.canAcceptWork());
 });
 
+// A @chainsafe/bls PublicKey as the reference's set builders hand it over
+// (index2pubkey[i], state-transition/src/signatureSets/indexedAttestation.ts:27):
+// toBytes(format) returns the COMPRESSED encoding unless format is "uncompressed"
+// (PointFormat, the reference passes PointFormat.uncompressed, index.ts:144).
+class MockPublicKey {
+  constructor(b, ignoreFormat = false) {
+    this.unc = new Uint8Array(96).fill(b);
+    this.unc[0] = b & 0x1f;
+    this.comp = new Uint8Array(48).fill(b);
+    this.comp[0] = 0x80 | (b & 0x1f);
+    this.ignoreFormat = ignoreFormat;
+    this.formats = [];
+  }
+  toBytes(format) {
+    this.formats.push(format);
+    return format === "uncompressed" && !this.ignoreFormat ? this.unc : this.comp;
+  }
+}
+
+test("PublicKey objects (unmapped) are serialized once with PointFormat.uncompressed", () => {
+  const ks = [1, 2, 3, 4].map((b) => new MockPublicKey(b));
+  const s1 = {type: "single", pubkey: ks[0], signingRoot: new Uint8Array(32), signature: GOOD};
+  const s2 = {type: "aggregate", pubkeys: [ks[1], ks[2], ks[3]], signingRoot: new Uint8Array(32), signature: GOOD};
+  const b = V.packRequests([[s1, s2]], new Uint8Array(32), new WeakMap());
+  assert.strictEqual(b.pubkeyIndices, undefined);
+  assert.deepStrictEqual(Array.from(b.pkOffsets), [0, 1, 4]);
+  assert.strictEqual(b.pubkeys.length, 4 * 96);
+  ks.forEach((k, i) => {
+    assert.deepStrictEqual(k.formats, ["uncompressed"]);
+    assert.deepStrictEqual(Array.from(b.pubkeys.subarray(96 * i, 96 * i + 96)), Array.from(k.unc));
+  });
+  // the old boolean form would have produced the compressed 48 bytes and thrown
+  assert.strictEqual(new MockPublicKey(7).toBytes(false).length, 48);
+});
+
+test("compressed keys (48-byte bytes, or toBytes ignoring the format) ship as flagged rows", () => {
+  const F = 0x80000000;
+  const F48 = 0x40000000;
+  const raw48 = new MockPublicKey(5).comp;
+  const obj48 = new MockPublicKey(6, true);
+  const unc = new MockPublicKey(7);
+  const sets_ = [
+    {type: "single", pubkey: raw48, signingRoot: new Uint8Array(32), signature: GOOD},
+    {type: "aggregate", pubkeys: [obj48, unc, {index: 9}], signingRoot: new Uint8Array(32), signature: GOOD},
+  ];
+  const b = V.packRequests([sets_], new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(b.pubkeyIndices), [(F | F48 | 0) >>> 0, (F | F48 | 1) >>> 0, (F | 2) >>> 0, 9]);
+  assert.deepStrictEqual(Array.from(b.pubkeys.subarray(0, 48)), Array.from(raw48));
+  assert.deepStrictEqual(Array.from(b.pubkeys.subarray(96, 144)), Array.from(obj48.comp));
+  assert.deepStrictEqual(Array.from(b.pubkeys.subarray(192, 288)), Array.from(unc.unc));
+  // slicing keeps the compressed flag while renumbering rows
+  const q = V.slicePacked({...b, requestOffsets: Uint32Array.from([0, 1, 2])}, 1, 2, new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(q.pubkeyIndices), [(F | F48 | 0) >>> 0, (F | 1) >>> 0, 9]);
+  // same-message packages: the same mixed layout
+  const sm = V.packSameMessage([{sets: [{publicKey: raw48, signature: GOOD}, {publicKey: unc, signature: GOOD}],
+    message: new Uint8Array(32)}], new Uint8Array(32));
+  assert.deepStrictEqual(Array.from(sm.pubkeyIndices), [(F | F48 | 0) >>> 0, (F | 1) >>> 0]);
+  assert.throws(() => V.packRequests([[{...sets_[0], pubkey: new Uint8Array(47)}]], new Uint8Array(32)), TypeError);
+});
+
+class TableBackend extends MockBackend {
+  constructor() {
+    super(2);
+    this.table = 0;
+    this.synced = [];
+  }
+  async syncPubkeys(blob, pkLen) {
+    this.synced.push({n: blob.length / pkLen, pkLen, first: blob[0]});
+    this.table += blob.length / pkLen;
+    return this.table;
+  }
+  async verifyRequests(b, opts) {
+    this.lastBatch = b;
+    return super.verifyRequests(b, opts);
+  }
+  async verifySameMessage(b) {
+    this.lastSame = b;
+    return super.verifySameMessage(b);
+  }
+}
+
+test("index2pubkey objects mirrored by syncPubkeys ship as validator indices", async () => {
+  const bs = [new TableBackend(), new TableBackend()];
+  const v = new V.BlsGpuVerifier({backends: bs, seedSource: seed});
+  const index2pubkey = Array.from({length: 600}, (_, i) => new MockPublicKey(1 + (i % 200)));
+  assert.strictEqual(await v.syncIndex2pubkey(index2pubkey.slice(0, 500)), 500);
+  assert.strictEqual(await v.syncIndex2pubkey(index2pubkey), 600);  // incremental: 100 more
+  assert.deepStrictEqual(bs[0].synced.map((x) => [x.n, x.pkLen]), [[500, 48], [100, 48]]);
+  assert.deepStrictEqual(index2pubkey[0].formats, ["compressed"]);  // serialized once, at sync
+  // a C4-shaped aggregate (488 keys of a committee) + a single set, built from index2pubkey
+  const committee = Array.from({length: 488}, (_, i) => index2pubkey[(i * 7) % 600]);
+  const r = await v.verifySignatureSets([
+    {type: "aggregate", pubkeys: committee, signingRoot: new Uint8Array(32), signature: GOOD},
+    {type: "single", pubkey: index2pubkey[42], signingRoot: new Uint8Array(32), signature: GOOD},
+  ]);
+  assert.strictEqual(r, true);
+  const b = bs.find((x) => x.lastBatch).lastBatch;
+  assert.strictEqual(b.pubkeys, undefined);
+  assert.deepStrictEqual(Array.from(b.pubkeyIndices.subarray(0, 3)), [0, 7, 14]);
+  assert.strictEqual(b.pubkeyIndices[488], 42);
+  assert(index2pubkey.every((k) => k.formats.length === 1), "a mirrored key was serialized again");
+  // an unmirrored key beside mirrored ones: a mixed package (its row, serialized uncompressed)
+  const stranger = new MockPublicKey(250);
+  await v.verifySignatureSets([{type: "aggregate", pubkeys: [index2pubkey[3], stranger], signingRoot: new Uint8Array(32), signature: GOOD}]);
+  const b2 = bs.map((x) => x.lastBatch).filter(Boolean).pop();
+  assert.deepStrictEqual(Array.from(b2.pubkeyIndices), [3, 0x80000000]);
+  assert.deepStrictEqual(stranger.formats, ["uncompressed"]);
+  // same-message sets from index2pubkey: by index
+  await v.verifySignatureSetsSameMessage([{publicKey: index2pubkey[5], signature: GOOD}, {publicKey: index2pubkey[6], signature: GOOD}],
+    new Uint8Array(32));
+  const sm = bs.map((x) => x.lastSame).filter(Boolean).pop();
+  assert.deepStrictEqual(Array.from(sm.pubkeyIndices), [5, 6]);
+  assert.strictEqual(sm.pubkeys, undefined);
+  await v.close();
+  // the single-thread verifier keeps the same map
+  const st = new V.BlsGpuSingleThreadVerifier({backend: new TableBackend(), seedSource: seed});
+  await st.syncIndex2pubkey(index2pubkey.slice(0, 10));
+  await st.verifySignatureSets([{type: "single", pubkey: index2pubkey[4], signingRoot: new Uint8Array(32), signature: GOOD}]);
+  assert.deepStrictEqual(Array.from(st.backend.lastBatch.pubkeyIndices), [4]);
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {

@@ -218,3 +218,68 @@ def test_async_lone_call_borrows_a_stream(device, workload):
     assert [bool(v) for v in device.wait_call(lone).valid] == want
     device.verify_finish(pp, False)
     assert [bool(v) for v in device.wait_call(pp).valid] == want
+
+
+def _pack_requests(reqs):
+    pks, pk_off, msgs, sigs, req_off = [], [0], [], [], [0]
+    for r in reqs:
+        for s in r:
+            keys = [s.pubkey] if s.pubkey is not None else s.pubkeys
+            pks += [k.uncompressed for k in keys]
+            pk_off.append(len(pks))
+            msgs.append(s.signing_root)
+            sigs.append(s.signature)
+        req_off.append(len(msgs))
+    blob, offs = pack_blobs(sigs)
+    return (np.array(req_off, np.uint32), np.frombuffer(b"".join(pks), np.uint8), np.array(pk_off, np.uint32),
+            np.frombuffer(b"".join(msgs), np.uint8), blob, offs)
+
+
+def _dev_env(**env):
+    from lodestar_amd.native import Device
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Device(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("gt_lp", ["1", "0"])
+def test_partials_round_program_tail(workload, gt_lp):
+    """Two-phase calls whose merged product comes from the round program (the bucket MSM
+    forced on, LB_MTAIL=1: k_lp_mtail's partial form) and from the one-lane chain
+    (LB_MTAIL=0): each mode's shard partials combine to the right verdict, partials of
+    the two modes combine with each other (they differ only by factors the final
+    exponentiation kills), and lb_gt_check's final exponentiation as a round program
+    (LB_GT_LP=1) agrees with the one-wave chain (0)."""
+    seed = bytes(32)
+    ok_a, ok_b = _pack_requests(workload[:32]), _pack_requests(workload[32:])
+    bad = _pack_requests(_corrupt(workload[32:], [7]))
+    parts = {}
+    for mtail in ("1", "0"):
+        dev = _dev_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail, LB_GT_LP=gt_lp)
+        try:
+            pcs = [dev.verify_requests_async(*x, seed, partial=True) for x in (ok_a, ok_b, bad)]
+            parts[mtail] = [dev.partial_wait(pc) for pc in pcs]
+            Pa, Pb, Pbad = parts[mtail]
+            assert dev.gt_check([Pa, Pb]) is True
+            assert dev.gt_check([Pa, Pbad]) is False
+            dev.verify_finish(pcs[0], True)
+            dev.verify_finish(pcs[1], True)
+            dev.verify_finish(pcs[2], False)
+            r = [dev.wait_call(pc) for pc in pcs]
+            assert r[0].valid.all() and r[1].valid.all()
+            assert [bool(v) for v in r[2].valid] == [k != 7 for k in range(len(workload) - 32)]
+        finally:
+            dev.close()
+    dev = _dev_env(LB_GT_LP=gt_lp)
+    try:
+        assert dev.gt_check([parts["1"][0], parts["0"][1]]) is True
+        assert dev.gt_check([parts["0"][0], parts["1"][2]]) is False
+    finally:
+        dev.close()

@@ -368,24 +368,29 @@ def _device_with_env(**env):
                 os.environ[k] = v
 
 
+@pytest.mark.parametrize("mtail", ["1", "0"])
 @pytest.mark.parametrize("inject", [True, False])
-def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject):
+def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail):
     """The merged check's sum of r_i sig_i from the bucket MSM (k_msm.hip), forced
     onto this 1,500-set call (LB_MSM_MIN=1; by default calls of >= 4096 sets):
     with injected failures the merged check fails and the per-request tails take
     their S_k from the per-set ladders; without, the merged check passes on the
-    MSM's sum alone.  Verdicts and rejection codes == the C oracle's."""
+    MSM's sum alone.  The merged check itself runs as the round program (LB_MTAIL=1,
+    k_lp_mtail: S_all from the MSM's bit sums, its Miller value, the final
+    exponentiation) or as the one-lane / one-wave chain (msm_final, lines of S_all,
+    k_tail).  Verdicts and rejection codes == the C oracle's."""
     from oracle import c_oracle as C
     args = mixed_workload_cache(device, inject)
     seed = hashlib.sha256(b"msm-seed").digest()
-    dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines")
+    dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail)
     try:
         res = dev.verify_requests(*args, seed)
         stages = dict(dev.last_stage_times())
         valid, err = C.verify_requests(*args, seed, threads=16)
         assert list(res.errors) == list(err)
         assert list(res.valid) == list(valid)
-        assert "msm_final" in stages and "msm_chunks" in stages
+        assert "msm_chunks" in stages
+        assert ("mtail" in stages) == (mtail == "1") and ("msm_final" in stages) == (mtail == "0")
         if inject:
             assert res.batch_retries == 1 and "scalar_sig" in stages
         else:

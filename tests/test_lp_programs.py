@@ -175,3 +175,74 @@ def test_set_then_mul_then_final_chain(single):
     prod, _ = prog("mul").run(outs[0] + outs[1], [])
     assert all(v < P for v in prod)
     assert prog("final").run(prod, [])[1] == [1]
+
+
+# ---- the throughput pipeline's merged check (mtail) and the combine's final exponentiation
+@functools.lru_cache(maxsize=None)
+def mtail_prog(partial):
+    return lpc.compile_graph(bls.mtail_program(partial), rows=32)
+
+
+def _jac_inputs(pt, z):
+    """G2 point (affine, or None = O) as one-lane Jacobian inputs with Z = z"""
+    if pt is None:
+        return [1, 0, 1, 0, 0, 0]
+    (x0, x1), (y0, y1) = pt
+    z2 = z * z % P
+    z3 = z2 * z % P
+    # Jacobian over Fp2 with z in Fp: X = x z^2, Y = y z^3
+    return [x0 * z2 % P, x1 * z2 % P, y0 * z3 % P, y1 * z3 % P, z, 0]
+
+
+def _mtail_inputs(h, pts, seed=7):
+    import random
+    rnd = random.Random(seed)
+    vals = f12_fps(h)
+    for pt in pts:
+        vals += _jac_inputs(pt, rnd.randrange(1, P))
+    return [mont(v) for v in vals]
+
+
+def _msm_points(n_inf=3):
+    """33 bit sums: multiples of G2, a few infinite; S = sum 2^p G_p"""
+    pts, S = [], None
+    for p in range(bls.MSM_POS):
+        if p in (0, 5, 32)[:n_inf]:
+            pts.append(None)
+            continue
+        g = O.g2_mul(O.G2, 1000 + 37 * p)
+        pts.append(g)
+        t = O.g2_mul(g, 1 << p)
+        S = t if S is None else O.g2_add(S, t)
+    return pts, S
+
+
+def test_mtail_programs_against_oracle():
+    """check: final_exp(h * Miller(-g1, S_all)) == 1 exactly when h cancels e(-g1, S_all);
+    partial: the same product (up to the factors the final exponentiation kills)"""
+    pts, S = _msm_points()
+    good = O.miller_loop(O.G1, S)      # e(g1, S) e(-g1, S) = 1
+    bad = O.miller_loop(O.G1, O.g2_add(S, O.G2))
+    for h, want in ((good, 1), (bad, 0)):
+        _, fl = mtail_prog(False).run(_mtail_inputs(h, pts), [])
+        assert fl == [want]
+        outs, _ = mtail_prog(True).run(_mtail_inputs(h, pts), [])
+        f = tuple(tuple((outs[6 * a + 2 * b] * pow(1 << 384, -1, P) % P,
+                         outs[6 * a + 2 * b + 1] * pow(1 << 384, -1, P) % P) for b in range(3)) for a in range(2))
+        assert all(o < P for o in outs)  # canonical one-lane form
+        assert O.f12_is_one(O.final_exp(f)) == bool(want)
+    # S_all = O (every bit sum infinite): the Miller factor is 1
+    inf_pts = [None] * bls.MSM_POS
+    one = O.f12_mul(O.miller_loop(O.G1, O.G2), O.miller_loop(O.E1.neg(O.G1), O.G2))
+    _, fl = mtail_prog(False).run(_mtail_inputs(one, inf_pts), [])
+    assert fl == [1]
+    _, fl = mtail_prog(False).run(_mtail_inputs(O.miller_loop(O.G1, O.G2), inf_pts), [])
+    assert fl == [0]
+
+
+def test_final_lane_program():
+    g = lpc.compile_graph(bls.final_lane_program(), rows=32)
+    one = O.f12_mul(O.miller_loop(O.G1, O.G2), O.miller_loop(O.E1.neg(O.G1), O.G2))
+    for f, want in ((one, 1), (O.miller_loop(O.G1, O.G2), 0)):
+        _, fl = g.run([mont(v) for v in f12_fps(f)], [])
+        assert fl == [want]
