@@ -490,11 +490,12 @@ def main():
     legs = {}
     if world == 1 and not a.no_legs:
         legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off)
+        agg = c4_aggregates(dev, sks)
         # the node leg runs with this process's context closed: two processes with 16 HIP
         # hardware queues each oversubscribe the GPU's queue scheduler (the node p50s went
         # 20 -> 39 ms with the bench's context alive)
         dev.close()
-        legs["node"] = node_leg(pks, msgs, sigs, a.node_rounds)
+        legs["node"] = node_leg(pks, msgs, sigs, a.node_rounds, agg)
 
     if rank != 0:
         if world > 1:
@@ -646,9 +647,35 @@ def roofline(iso_ms, stage_ms, n, value, iso_reps, n_req):
     return roof
 
 
-def node_leg(pks, msgs, sigs, rounds: int = 4):
+def compress_g1(unc: bytes) -> bytes:
+    """ZCash compression of a 96-byte uncompressed G1 encoding (x with the 0x80 flag, 0x20
+    when y is the lexicographically larger root)"""
+    p = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+    if unc[0] & 0x40:
+        return bytes([0xC0]) + bytes(47)
+    y = int.from_bytes(unc[48:96], "big")
+    return bytes([unc[0] | 0x80 | (0x20 if 2 * y > p else 0)]) + unc[1:48]
+
+
+def c4_aggregates(dev, sks, n_agg: int = 1024, k: int = 488):
+    """C4's aggregate attestations (committees of ~488 keys): n_agg committees of
+    k validator indices, a message each, the aggregate signature = a signature by the sum
+    of the committee's secret keys (= the sum of their signatures)"""
+    n = len(sks)
+    ints = [int.from_bytes(s, "big") for s in sks]
+    idx = np.array([(a * k + q) * 7 % n for a in range(n_agg) for q in range(k)], np.uint32)
+    msgs = [hashlib.sha256(b"c4-agg" + a.to_bytes(4, "little")).digest() for a in range(n_agg)]
+    agg_sk = [(sum(ints[int(i)] for i in idx[a * k:(a + 1) * k]) % R_ORDER).to_bytes(32, "big") for a in range(n_agg)]
+    sigs = []
+    for s in range(0, n_agg, 16384):
+        sigs += dev.sign(agg_sk[s:s + 16384], msgs[s:s + 16384])
+    return idx, msgs, sigs
+
+
+def node_leg(pks, msgs, sigs, rounds: int = 4, agg=None):
     """The Lodestar path (tools/bench_node.js): BlsGpuVerifier in node -> N-API addon ->
-    lb_verify_requests_async, pubkeys by index; throughput and p50 latencies."""
+    lb_verify_requests_async, pubkeys by index; throughput and p50 latencies; with `agg`,
+    C4-shaped AggregateAndProof triples with keys as PublicKey objects."""
     import shutil
     import tempfile
     if not shutil.which("node") or not os.path.exists(os.path.join(ROOT, "lodestar_amd", "napi", "lodestar_bls.node")):
@@ -657,6 +684,16 @@ def node_leg(pks, msgs, sigs, rounds: int = 4):
         for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
             with open(os.path.join(d, name + ".bin"), "wb") as f:
                 f.write(b"".join(items))
+        if agg is not None:
+            with open(os.path.join(d, "pks_c.bin"), "wb") as f:
+                f.write(b"".join(compress_g1(k) for k in pks))
+            agg_idx, agg_msgs, agg_sigs = agg
+            with open(os.path.join(d, "agg_idx.bin"), "wb") as f:
+                f.write(agg_idx.tobytes())
+            with open(os.path.join(d, "agg_msgs.bin"), "wb") as f:
+                f.write(b"".join(agg_msgs))
+            with open(os.path.join(d, "agg_sigs.bin"), "wb") as f:
+                f.write(b"".join(agg_sigs))
         try:
             out = subprocess.run(["node", os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)],
                                  capture_output=True, text=True, timeout=300)

@@ -78,6 +78,18 @@ typedef struct lb_ctx lb_ctx;
 
 /* Create a context on HIP device `device` (one per process per GPU). */
 int lb_create(int device, lb_ctx** out_ctx);
+/* A latency-lane context on the same GPU: one slot plus the priority lane, no CU-masked
+ * streams.  A host that must never make a priority call wait behind its submission
+ * thread's staging of throughput packages (the reference verifies verifyOnMainThread sets
+ * at once and unshifts priority jobs, BN/chain/bls/multithread/index.ts:174-187,544-555)
+ * drives lb_verify_requests_priority_async on this context from a thread of its own and
+ * calls lb_mark_priority on the throughput context, whose calls then leave the reserved
+ * CUs free (LB_PRIO_CUS).  Its pubkey table is its own: append the same keys to both. */
+int lb_create_lane(int device, lb_ctx** out_ctx);
+/* Mark the priority lane in use now (LB_PRIO_DYN: calls submitted within LB_PRIO_HOLD_MS
+ * take the CU-masked streams).  The one entry point that may be called on a context
+ * while another thread uses it. */
+int lb_mark_priority(lb_ctx* ctx);
 /* Release device memory and streams.  Safe on NULL. */
 int lb_destroy(lb_ctx* ctx);
 /* Human-readable message for the last error on this context (never NULL); with

@@ -23,6 +23,7 @@
 //                                   one wave per request (wave-cooperative Fp12)
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <mutex>
@@ -204,7 +205,9 @@ struct lb_ctx {
   bool prio_dyn = false;
   int prio_dyn_slots = 0;  // slots [0, prio_dyn_slots) own masked streams (LB_PRIO_DYN_SLOTS)
   double prio_hold_ms = 250.0;
-  std::chrono::steady_clock::time_point last_prio{};
+  // steady-clock ns of the priority lane's last use (or lb_mark_priority from another
+  // thread: an atomic, the one field of a context another thread may write)
+  std::atomic<int64_t> last_prio_ns{INT64_MIN / 2};
   int next_slot = 0;
   uint64_t next_ticket = 1;
   // the last tickets issued to two-phase calls: lb_verify_requests_finish accepts a
@@ -286,6 +289,7 @@ struct lb_ctx {
   bool mtail_lp = true;
   bool gt_lp = true;  // lb_gt_check's final exponentiation as a round program (LB_GT_LP=0: one wave)
   int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
+  bool lane = false;  // lb_create_lane: a latency-lane context (one slot, no CU-masked streams)
   int last_call_streams = 0;  // streams of the last submitted verify call (begin_call)
 };
 
@@ -1092,13 +1096,14 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
   return lane * 64 * 32 * (size_t)cus;
 }
 
-int lb_create(int device, lb_ctx** out_ctx) {
+static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (!out_ctx) return LB_ERR_INVALID_ARGUMENT;
   *out_ctx = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || device < 0 || device >= n) return LB_ERR_NO_DEVICE;
   lb_ctx* ctx = new lb_ctx();
   ctx->device = device;
+  ctx->lane = lane;
   bool ok = hipSetDevice(device) == hipSuccess;
   // one single-stream slot per hardware queue HIP gives this process (4 by
   // default; a host that sets GPU_MAX_HW_QUEUES=8 before HIP starts gets 8 calls
@@ -1124,6 +1129,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
     const int v = atoi(e);
     if (v >= 1 && v <= lb_ctx::kMaxSlots) ctx->n_slots = v;
   }
+  if (lane) ctx->n_slots = 1;  // a latency-lane context: its priority lane (+ one slot for helpers)
   if (const char* e = getenv("LB_MILLER"))
     ctx->miller_mode = strcmp(e, "lane") == 0 ? 1 : strcmp(e, "lines") == 0 ? 2 : strcmp(e, "wave") == 0 ? 3 : 0;
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
@@ -1147,7 +1153,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
     if (v == 64 || v == 32 || v == 16) ctx->acc_lpr = v;
   }
   for (int s = 0; s < lb_ctx::kMaxSlots; s++)
-    ctx->streams_per_slot[s] = ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;
+    ctx->streams_per_slot[s] = lane ? 1 : ctx->n_slots <= 2 ? 2 : (ctx->n_slots == 3 && s == 0) ? 2 : 1;
   ctx->streams_per_slot[ctx->n_slots] = 1;  // the priority lane
   // LB_SLOT0_STREAMS=1|2 overrides slot 0's two-stream DAG (the synchronous, lowest-latency slot)
   if (const char* e = getenv("LB_SLOT0_STREAMS")) ctx->streams_per_slot[0] = atoi(e) == 1 ? 1 : 2;
@@ -1168,6 +1174,7 @@ int lb_create(int device, lb_ctx** out_ctx) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     int k = cus >= 128 ? 64 : 0;
     if (const char* e = getenv("LB_PRIO_CUS")) k = atoi(e);
+    if (lane) k = 0;  // (the reservation belongs to the throughput context: lb_mark_priority)
     if (k > 0 && k < cus) {
       cu_mask.assign((size_t)(cus + 31) / 32, 0u);
       // LB_PRIO_SPREAD=1: the K reserved CUs evenly spaced over the CU ids instead (measured
@@ -1292,6 +1299,18 @@ int lb_create(int device, lb_ctx** out_ctx) {
   return LB_OK;
 }
 
+int lb_create(int device, lb_ctx** out_ctx) { return create_ctx(device, out_ctx, false); }
+
+int lb_create_lane(int device, lb_ctx** out_ctx) { return create_ctx(device, out_ctx, true); }
+
+int lb_mark_priority(lb_ctx* ctx) {
+  if (!ctx) return LB_ERR_INVALID_ARGUMENT;
+  ctx->last_prio_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count(),
+                          std::memory_order_relaxed);
+  return LB_OK;
+}
+
 int lb_destroy(lb_ctx* ctx) {
   if (!ctx) return LB_OK;
   (void)hipSetDevice(ctx->device);
@@ -1383,8 +1402,9 @@ int lb_last_stage_times(const lb_ctx* ctx, float* out_ms, const char** out_names
 
 // the priority lane used within the last prio_hold_ms (LB_PRIO_DYN)
 static bool prio_active(lb_ctx* ctx) {
-  return ctx->prio_dyn && std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
-                                                                    ctx->last_prio).count() < ctx->prio_hold_ms;
+  const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  return ctx->prio_dyn && (double)(now - ctx->last_prio_ns.load(std::memory_order_relaxed)) < ctx->prio_hold_ms * 1e6;
 }
 
 // A call about to run on slot sl (idle: finish_slot has retired its last call): with
@@ -1392,7 +1412,9 @@ static bool prio_active(lb_ctx* ctx) {
 // The priority slot marks the lane in use.
 static void pick_streams(lb_ctx* ctx, Slot& sl) {
   if (&sl == &ctx->prio()) {
-    ctx->last_prio = std::chrono::steady_clock::now();
+    ctx->last_prio_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now().time_since_epoch()).count(),
+                            std::memory_order_relaxed);
     return;
   }
   if (!ctx->prio_dyn) return;

@@ -283,6 +283,17 @@ struct Context {
   int pending = 0;        // JS thread only: tasks not yet completed
   uint64_t next_partial = 1;
   std::map<uint64_t, Task*> partials;  // worker thread only
+  // The latency lane (LB_PRIO_THREAD, default on): priority verify calls run on a context
+  // of their own (lb_create_lane) driven by a thread of their own, so they never wait for
+  // the submission thread's staging of throughput packages or its retiring of calls
+  // (the reference's verifyOnMainThread / priority unshift,
+  // BN/chain/bls/multithread/index.ts:174-187,544-555).  Its pubkey table mirrors ctx's.
+  lb_ctx* lctx = nullptr;
+  std::thread lane;
+  std::mutex lmu;
+  std::condition_variable lcv;
+  std::deque<Task*> lqueue;
+  bool lane_stop = false;
 };
 
 void complete(Context* c, Task* t) {
@@ -296,6 +307,64 @@ void complete(Context* c, Task* t) {
 void fail(Task* t, int rc, lb_ctx* ctx) {
   t->rc = rc;
   t->errmsg = ctx ? lb_last_error(ctx) : "no context";
+}
+
+// The lane thread: owns c->lctx.  Priority verify calls one at a time (the priority slot
+// admits one), and the second half of every pubkey-table append (the main worker appends
+// to ctx first, then hands the task here).
+void lane_loop(Context* c) {
+  for (;;) {
+    Task* t = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(c->lmu);
+      c->lcv.wait(lk, [&] { return !c->lqueue.empty() || c->lane_stop; });
+      if (c->lqueue.empty()) break;  // stopped and drained
+      t = c->lqueue.front();
+      c->lqueue.pop_front();
+    }
+    if (c->finalizing) {
+      delete t;
+      continue;
+    }
+    if (t->kind == Kind::SyncPubkeys) {
+      int32_t bad = -1;
+      uint32_t n = 0;
+      const int rc = lb_pubkey_table_append(c->lctx, t->n_keys, t->pubkeys.data(), t->pk_len, &bad);
+      if (rc != LB_OK) {
+        fail(t, rc, c->lctx);
+      } else if (lb_pubkey_table_size(c->lctx, &n) != LB_OK || n != t->u32) {
+        t->rc = LB_ERR_DEVICE;
+        t->errmsg = "the latency lane's pubkey table is out of sync";
+      }
+      complete(c, t);
+      continue;
+    }
+    t->t_start = now_ns();
+    alloc_outputs(*t);
+    lb_request_batch b = batch_of(*t);
+    int rc = lb_verify_requests_priority_async(c->lctx, &b, t->valid.data(), t->err.data(), t->sst.data(), &t->ticket);
+    t->t_submitted = now_ns();
+    if (rc == LB_OK) {
+      t->t_retire = now_ns();
+      rc = lb_wait(c->lctx, t->ticket, &t->stats);
+    }
+    if (rc != LB_OK) fail(t, rc, c->lctx);
+    t->t_end = now_ns();
+    complete(c, t);
+  }
+  lb_destroy(c->lctx);
+  c->lctx = nullptr;
+}
+
+// stop the lane thread after it has drained its queue (worker thread, before lb_destroy)
+void lane_join(Context* c) {
+  if (!c->lane.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(c->lmu);
+    c->lane_stop = true;
+  }
+  c->lcv.notify_one();
+  c->lane.join();
 }
 
 // A queued task the worker can start now: a priority call always (its lane is
@@ -478,6 +547,14 @@ void worker_loop(Context* c) {
           if (bad >= 0) t->errmsg += " (pubkey " + std::to_string(bad) + ")";
         } else {
           lb_pubkey_table_size(c->ctx, &t->u32);
+          if (c->lctx) {  // the same keys into the latency lane's table, then resolve
+            {
+              std::lock_guard<std::mutex> lk(c->lmu);
+              c->lqueue.push_back(t);
+            }
+            c->lcv.notify_one();
+            break;
+          }
         }
         complete(c, t);
         break;
@@ -531,6 +608,7 @@ void worker_loop(Context* c) {
         }
         for (auto& kv : c->partials) delete kv.second;
         c->partials.clear();
+        lane_join(c);  // (its queued priority calls complete first)
         lb_destroy(c->ctx);
         c->ctx = nullptr;
         complete(c, t);
@@ -549,6 +627,7 @@ void worker_loop(Context* c) {
     delete w;
   }
   for (auto& kv : c->partials) delete kv.second;
+  lane_join(c);
   lb_destroy(c->ctx);
   c->ctx = nullptr;
 }
@@ -678,6 +757,18 @@ napi_value submit(napi_env env, Context* c, Task* t) {
       return promise;
     }
     if (t->kind == Kind::Close) c->closing = true;
+    if (t->prio && t->kind == Kind::Verify && c->lctx) {
+      // the latency lane: its own thread and context; the throughput context's calls
+      // submitted from now on leave the reserved CUs free (lb_mark_priority)
+      lb_mark_priority(c->ctx);
+      {
+        std::lock_guard<std::mutex> lk2(c->lmu);
+        c->lqueue.push_back(t);
+      }
+      if (c->pending++ == 0) napi_ref_threadsafe_function(env, c->tsfn);
+      c->lcv.notify_one();
+      return promise;
+    }
     if (t->prio) {  // ahead of every queued non-priority task, behind earlier priority ones
       auto it = c->queue.begin();
       while (it != c->queue.end() && (*it)->prio) ++it;
@@ -898,6 +989,14 @@ void finalize_ctx(napi_env env, void* data, void* /*hint*/) {
       }
       c->queue.clear();
     }
+    {
+      std::lock_guard<std::mutex> lk(c->lmu);
+      for (Task* t : c->lqueue) {
+        release_refs(env, t);
+        delete t;
+      }
+      c->lqueue.clear();
+    }
     c->cv.notify_one();
     if (c->worker.joinable()) c->worker.join();
     if (c->tsfn) napi_release_threadsafe_function(c->tsfn, napi_tsfn_abort);
@@ -926,11 +1025,16 @@ napi_value New(napi_env env, napi_callback_info info) {
   c->device = device;
   c->capacity = capacity < 1 ? 1 : capacity;
   c->env = env;
+  {
+    const char* e = getenv("LB_PRIO_THREAD");
+    if (!(e && atoi(e) == 0) && lb_create_lane(device, &c->lctx) != LB_OK) c->lctx = nullptr;  // (then: no lane)
+  }
   napi_value name;
   napi_create_string_utf8(env, "lodestar_bls_gpu", NAPI_AUTO_LENGTH, &name);
   napi_create_threadsafe_function(env, nullptr, nullptr, name, 0, 1, nullptr, nullptr, c, call_js, &c->tsfn);
   napi_unref_threadsafe_function(env, c->tsfn);  // idle contexts do not keep the process alive
   c->worker = std::thread(worker_loop, c);
+  if (c->lctx) c->lane = std::thread(lane_loop, c);
   napi_wrap(env, self, c, finalize_ctx, nullptr, nullptr);
   napi_value dev, cap;
   napi_create_int32(env, device, &dev);

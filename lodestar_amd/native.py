@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
     "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
     "lb_verify_requests_priority_async", "lb_partial_poll", "lb_hw_queues", "lb_last_call_streams",
+    "lb_create_lane", "lb_mark_priority",
 )
 
 LB_BATCH_DEVICE = 1
@@ -128,6 +129,8 @@ def load_library() -> ctypes.CDLL:
     lib = ctypes.CDLL(path)
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.lb_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.lb_create_lane.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.lb_mark_priority.argtypes = [vp]
     lib.lb_destroy.argtypes = [vp]
     lib.lb_last_error.argtypes = [vp]
     lib.lb_last_error.restype = ctypes.c_char_p

@@ -429,6 +429,23 @@ test("index2pubkey objects mirrored by syncPubkeys ship as validator indices", a
   assert.deepStrictEqual(Array.from(st.backend.lastBatch.pubkeyIndices), [4]);
 });
 
+test("packRequestsAsync (sliced, yielding) packs exactly what packRequests packs", async () => {
+  const reqs = [];
+  for (let r = 0; r < 40; r++) {
+    const req = [];
+    for (let q = 0; q < 1 + (r % 5); q++)
+      req.push(q % 3 === 2
+        ? {type: "aggregate", pubkeys: [{index: r}, new MockPublicKey(1 + q), new MockPublicKey(9, true)],
+           signingRoot: new Uint8Array(32).fill(r), signature: GOOD}
+        : {type: "single", pubkey: q % 2 ? {index: q} : new MockPublicKey(3 + r), signingRoot: new Uint8Array(32).fill(q),
+           signature: r === 7 ? new Uint8Array(192).fill(1) : GOOD});
+    reqs.push(req);
+  }
+  const a = V.packRequests(reqs, new Uint8Array(32));
+  const b = await V.packRequestsAsync(reqs, new Uint8Array(32), undefined, 7);
+  for (const key of Object.keys(a)) assert.deepStrictEqual(Array.from(b[key]), Array.from(a[key]), key);
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {

@@ -24,6 +24,69 @@ function median(xs) {
   return s[Math.floor(s.length / 2)];
 }
 
+class PublicKey {  // @chainsafe/bls-shaped: compressed unless "uncompressed"
+  constructor(unc, comp) {
+    this.unc = unc;
+    this.comp = comp;
+  }
+  toBytes(format) {
+    return format === "uncompressed" ? this.unc : this.comp;
+  }
+}
+
+async function c4Leg(dir, n, pks, msgs, sigs) {
+  const pkc = rd("pks_c.bin");
+  const aggIdx = new Uint32Array(rd("agg_idx.bin").buffer);
+  const aggMsg = rd("agg_msgs.bin");
+  const aggSig = rd("agg_sigs.bin");
+  const nAgg = aggMsg.length / 32;
+  const k = aggIdx.length / nAgg;
+  const index2pubkey = [];
+  for (let i = 0; i < n; i++) index2pubkey.push(new PublicKey(pks.subarray(96 * i, 96 * i + 96), pkc.subarray(48 * i, 48 * i + 48)));
+  const tSync = Number(process.hrtime.bigint()) / 1e6;
+  // a fresh verifier: its own tables mirror index2pubkey from entry 0
+  const w = new V.BlsGpuVerifier({devices: [0]});
+  await w.syncIndex2pubkey(index2pubkey);
+  const syncMs = Number(process.hrtime.bigint()) / 1e6 - tSync;
+  const single = (i) => ({type: "single", pubkey: index2pubkey[i], signingRoot: msgs.subarray(32 * i, 32 * i + 32),
+                          signature: sigs.subarray(96 * i, 96 * i + 96)});
+  const triples = [];
+  for (let a = 0; a < nAgg; a++) {
+    const keys = [];
+    for (let q = 0; q < k; q++) keys.push(index2pubkey[aggIdx[a * k + q]]);
+    triples.push([single((2 * a) % n), single((2 * a + 1) % n),
+                  {type: "aggregate", pubkeys: keys, signingRoot: aggMsg.subarray(32 * a, 32 * a + 32),
+                   signature: aggSig.subarray(96 * a, 96 * a + 96)}]);
+  }
+  const run = async (verifier, reps) => {
+    const m = verifier.metrics;
+    const h0 = m.hist.get(V.METRICS.PUBKEYS_AGGREGATION_MAIN_THREAD) || {count: 0, sum: 0};
+    const c0 = h0.count;
+    const s0 = h0.sum;
+    const t0 = Number(process.hrtime.bigint()) / 1e6;
+    const all = [];
+    for (let r = 0; r < reps; r++) for (const t of triples) all.push(verifier.verifySignatureSets(t, {batchable: true}));
+    const okAll = (await Promise.all(all)).every((x) => x === true);
+    const el = Number(process.hrtime.bigint()) / 1e6 - t0;
+    const h = m.hist.get(V.METRICS.PUBKEYS_AGGREGATION_MAIN_THREAD) || {count: 0, sum: 0};
+    return {sets_per_s: Math.round((reps * triples.length * 3 * 1000) / el), keys_per_s: Math.round((reps * nAgg * (k + 2) * 1000) / el),
+            pack_ms_per_package: h.count > c0 ? +(((h.sum - s0) / (h.count - c0)) * 1e3).toFixed(3) : null,
+            packages: h.count - c0, all_valid: okAll};
+  };
+  await run(w, 1);  // warm-up
+  const mirrored = await run(w, 4);
+  await w.close();
+  // the same calls on a verifier whose tables do not hold the keys: every key serialized
+  const u = new V.BlsGpuVerifier({devices: [0]});
+  await run(u, 1);
+  const unmirrored = await run(u, 1);
+  await u.close();
+  return {triples_per_round: triples.length, keys_per_aggregate: k, sync_index2pubkey_ms: +syncMs.toFixed(1),
+          mirrored, unmirrored,
+          api: "verifySignatureSets([selection proof, aggregator sig, aggregate of " + k +
+               " keys], {batchable}) with index2pubkey PublicKey objects"};
+}
+
 (async () => {
   const pks = rd("pks.bin");
   const msgs = rd("msgs.bin");
@@ -123,23 +186,38 @@ function median(xs) {
     };
     v.trace = null;
   }
-  // latency under load: `loadRounds` more rounds of packages queued at once (every slot
-  // busy with a 65,536-set call, more waiting in the JS queue); meanwhile one 1-set
-  // verifyOnMainThread call and one 128-set priority job at a time take the device's
-  // priority lane (BlsGpuVerifier priorityLane -> addon {priority} -> the library's
-  // priority slot on a highest-priority stream)
-  const loadRounds = Math.max(8, rounds >> 2);
+  // latency under load: packages kept queued (every slot busy with a 65,536-set call and
+  // LOAD_PACKAGES packages' jobs waiting in the JS queue, refilled as they retire);
+  // meanwhile one 1-set verifyOnMainThread call and one 128-set priority job at a time
+  // take the device's priority lane (BlsGpuVerifier priorityLane -> addon {priority} ->
+  // the addon's latency-lane thread and context -> the library's priority slot)
+  const loadPackages = Math.max(8, rounds >> 2);
+  const loadJobs = loadPackages * jobs.length;
+  let outstanding = 0;
+  let stop = false;
+  let nextJob = 0;
+  let loadBad = 0;
+  let loadDoneJobs = 0;
   const loadAll = [];
-  for (let r = 0; r < loadRounds; r++) for (const js of jobs) loadAll.push(v.verifySignatureSets(js));
-  let loadDone = false;
-  const loadP = Promise.all(loadAll).then((xs) => {
-    loadDone = true;
-    return xs.every((x) => x === true);
-  });
+  const refill = () => {
+    while (!stop && outstanding < loadJobs) {
+      outstanding++;
+      loadAll.push(v.verifySignatureSets(jobs[nextJob++ % jobs.length]).then((x) => {
+        outstanding--;
+        loadDoneJobs++;
+        if (x !== true) loadBad++;
+        refill();
+      }));
+    }
+  };
+  refill();
   await new Promise((r) => setTimeout(r, 300));  // the pipe full
   const load1 = [];
   const load128 = [];
-  for (let r = 0; r < 11 && !loadDone; r++) {
+  const tLoad = ms();
+  const loadJobs0 = loadDoneJobs;
+  const samples = parseInt(process.env.LB_NODE_LOAD_SAMPLES || "25", 10);
+  for (let r = 0; r < samples; r++) {
     let t = ms();
     ok = ok && (await v.verifySignatureSets([set(r + 7)], {verifyOnMainThread: true})) === true;
     load1.push(ms() - t);
@@ -148,7 +226,10 @@ function median(xs) {
     load128.push(ms() - t);
     await new Promise((res) => setTimeout(res, 10));
   }
-  ok = ok && (await loadP);
+  const loadRate = ((loadDoneJobs - loadJobs0) * 128 * 1000) / (ms() - tLoad);
+  stop = true;
+  await Promise.all(loadAll);
+  ok = ok && loadBad === 0;
   const lat128 = [];
   const lat1 = [];
   if (process.env.LB_JS_TRACE === "1") v.trace = [];
@@ -168,7 +249,16 @@ function median(xs) {
     };
     v.trace = null;
   }
+  // C4-shaped AggregateAndProof triples (BN/chain/validation/aggregateAndProof.ts:200: a
+  // selection proof, the aggregator's signature, the aggregate attestation of ~488
+  // committee keys), keys as @chainsafe/bls-shaped PublicKey objects out of index2pubkey:
+  // mirrored (syncIndex2pubkey: shipped as 4-byte indices) and not (serialized with
+  // toBytes("uncompressed") per key, as the reference does, index.ts:144)
+  // (after closing v: one verifier's contexts at a time, every context's hardware queues
+  // reserve scratch, DESIGN.md §5.1)
   await v.close();
+  let c4 = null;
+  if (fs.existsSync(path.join(dir, "agg_idx.bin"))) c4 = await c4Leg(dir, n, pks, msgs, sigs);
   process.stdout.write(
     JSON.stringify({
       sets_per_s: Math.round((rounds * n * 1000) / el),
@@ -183,12 +273,16 @@ function median(xs) {
       under_load: {
         p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
         p50_ms_128set_priority: load128.length ? +median(load128).toFixed(3) : null,
+        ratio_1set_vs_idle: load1.length ? +(median(load1) / median(pre1)).toFixed(2) : null,
+        ratio_128set_vs_idle: load128.length ? +(median(load128) / median(pre128)).toFixed(2) : null,
         samples: load1.length,
-        load_packages: loadRounds,
+        load_packages_queued: loadPackages,
+        background_sets_per_s: Math.round(loadRate),
       },
       ...(trace ? {trace} : {}),
       ...(latTrace ? {latency_trace: latTrace} : {}),
       ...(latTraceAfter ? {latency_trace_after_throughput: latTraceAfter} : {}),
+      ...(c4 ? {c4_public_key_objects: c4} : {}),
       all_valid: ok,
       table_size: tableSize,
       capacity: v.capacity,
