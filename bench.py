@@ -430,7 +430,7 @@ def main():
     # p50 of ONE set (the verifyOnMainThread shape: a 1-set request, core verify,
     # BN/chain/validation/block.ts:146) and of one 128-set request through the
     # synchronous host-buffer entry point (numpy in, verdicts out, PCIe included)
-    lat1, lat_host = [], []
+    lat1, lat_host, lat1_clk = [], [], []
     if a.latency_reps > 0:
         d_req1 = torch.tensor([0, 1], dtype=torch.int32, device=cuda)
 
@@ -450,6 +450,7 @@ def main():
             t1 = time.perf_counter()
             one_set()
             lat1.append((time.perf_counter() - t1) * 1e3)
+            lat1_clk.append(dev.last_latency_clocks())
             t1 = time.perf_counter()
             dev.verify_requests(ro_h, pk_h, None, mg_h, sg_h, so_h, seed_h)
             lat_host.append((time.perf_counter() - t1) * 1e3)
@@ -541,6 +542,10 @@ def main():
         "p50_ms_128set_batch": round(p50, 3) if p50 is not None else None,
         "p50_stage_ms": lat_stages,
         "p50_ms_1set": round(p50_1, 3) if p50_1 is not None else None,
+        # the latency path's kernel alone (s_memrealtime inside k_lp_verify) and its shader clock
+        "p50_1set_kernel": ({"ms": round(float(np.median([c[0] for c in lat1_clk if c[0]])), 3),
+                             "clock_mhz": round(float(np.median([c[1] for c in lat1_clk if c[0]])), 1)}
+                            if any(c[0] for c in lat1_clk) else None),
         "p50_ms_128set_host": round(p50_host, 3) if p50_host is not None else None,
         "latency_under_load": loaded,
         "all_valid": ok,

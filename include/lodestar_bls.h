@@ -110,6 +110,11 @@ int lb_slots(const lb_ctx* ctx);
 int lb_hw_queues(const lb_ctx* ctx);
 /* Distinct streams the last submitted verify call runs on (2: the two-stream DAG). */
 int lb_last_call_streams(const lb_ctx* ctx);
+/* Clock stamps of the last retired latency-path call (diagnostics): [0] s_memrealtime
+ * (100 MHz) and [1] s_memtime (shader clock) when its first workgroup started, [2] / [3]
+ * when request 0's verdict was written -- the kernel's own duration and the shader clock
+ * it ran at, apart from any wait before its dispatch. */
+int lb_last_latency_clocks(const lb_ctx* ctx, uint64_t* out4);
 /* Number of visible HIP devices (0 when none). */
 int lb_device_count(void);
 /* Scratch one hardware queue reserves for the library's kernels: the largest

@@ -149,6 +149,10 @@ struct Slot {
   Slot* lent_to = nullptr;
   // a synchronous call's second stream (borrow_second_stream): pick_streams keeps it
   hipStream_t guard_st = nullptr;
+  // latency-path calls: the kernel's clock stamps (pinned, LpCall::clk), published to
+  // ctx->lp_clk when the call retires
+  unsigned long long* h_clk = nullptr;
+  bool lp_call = false;
 };
 
 // The context's last error message.  lb_gt_check may run on one thread while another
@@ -291,6 +295,7 @@ struct lb_ctx {
   int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
   bool lane = false;  // lb_create_lane: a latency-lane context (one slot, no CU-masked streams)
   int last_call_streams = 0;  // streams of the last submitted verify call (begin_call)
+  unsigned long long lp_clk[4] = {};  // clock stamps of the last retired latency-path call
 };
 
 namespace {
@@ -416,6 +421,7 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   uint32_t* d_setreq = ws.take<uint32_t>(ns);
   uint32_t* d_F = ws.take<uint32_t>((size_t)ns * 12 * 16);
   uint32_t* d_cnt = ws.take<uint32_t>((size_t)LB_LP_TREE_LEVELS * ns);
+  unsigned long long* d_clk = ws.take<unsigned long long>(4);
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
@@ -424,6 +430,7 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   LB_HIP(hipMemsetAsync(d_req_err, 0, n_req, sl.st[0]));
   if (!n_sets) return LB_OK;  // every request empty: false
   LB_HIP(hipMemsetAsync(d_cnt, 0, (size_t)LB_LP_TREE_LEVELS * ns * sizeof(uint32_t), sl.st[0]));
+  LB_HIP(hipMemsetAsync(d_clk, 0, 4 * sizeof(unsigned long long), sl.st[0]));
   const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
   LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
   if (d_pk_off)
@@ -447,7 +454,10 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   c.valid = d_valid;
   c.req_err = d_req_err;
   c.n_sets = n_sets;
+  c.clk = d_clk;
   LB_STAGE("lp_verify", 0, k_lp_verify, n_sets, LB_LP_TPB, c);
+  LB_HIP(hipMemcpyAsync(sl.h_clk, d_clk, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, sl.st[0]));
+  sl.lp_call = true;
   PipeState& ps = sl.ps;
   ps = PipeState{};
   ps.n_req = n_req;
@@ -945,6 +955,8 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
   LB_HIP(hipEventElapsedTime(&ctx->wall_ms, sl.wall0, sl.wall1));
   ctx->batch_retries = sl.h_stats[0];
   ctx->batch_sigs_success = sl.h_stats[1];
+  if (sl.lp_call)
+    for (int i = 0; i < 4; i++) ctx->lp_clk[i] = sl.h_clk[i];
   TicketStats& ts = ctx->tstats[sl.ticket % lb_ctx::kTicketRing];
   ts.ticket = sl.ticket;
   ts.batch_retries = sl.h_stats[0];
@@ -985,6 +997,7 @@ void borrow_idle_stream(lb_ctx* ctx, Slot& sl) {
 
 int begin_call(lb_ctx* ctx, Slot& sl) {
   ctx->last_call_streams = sl.st[1] != sl.st[0] ? 2 : 1;
+  sl.lp_call = false;
   sl.n_stages = 0;
   sl.partial_pending = false;
   sl.out_valid = sl.out_err = sl.out_sst = nullptr;
@@ -1273,7 +1286,8 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
          hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&sl.partial_ev, hipEventDisableTiming) == hipSuccess &&
          hipHostMalloc(&sl.h_stats, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
-         hipHostMalloc(&sl.h_partial, LB_GT_BYTES, hipHostMallocDefault) == hipSuccess;
+         hipHostMalloc(&sl.h_partial, LB_GT_BYTES, hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc(&sl.h_clk, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess;
     if (ok) sl.h_stats[0] = sl.h_stats[1] = 0;
   }
   ctx->stream = ctx->slots[0].st[0];
@@ -1335,6 +1349,7 @@ int lb_destroy(lb_ctx* ctx) {
     if (sl.partial_ev) (void)hipEventDestroy(sl.partial_ev);
     if (sl.h_stats) (void)hipHostFree(sl.h_stats);
     if (sl.h_partial) (void)hipHostFree(sl.h_partial);
+    if (sl.h_clk) (void)hipHostFree(sl.h_clk);
     for (int i = 0; i < ctx->streams_per_slot[s]; i++) {
       if (sl.st_mask[i] || sl.st_full[i]) {  // (st[] is one of these pairs)
         if (sl.st_mask[i] && !(i > 0 && sl.st_mask[i] == sl.st_mask[0])) (void)hipStreamDestroy(sl.st_mask[i]);
@@ -1379,6 +1394,11 @@ int lb_scratch_per_queue(int device, uint64_t* out_bytes, uint32_t* out_lane_byt
 int lb_slots(const lb_ctx* ctx) { return ctx ? ctx->n_slots : 0; }
 int lb_hw_queues(const lb_ctx* ctx) { return ctx ? ctx->hw_queues : 0; }
 int lb_last_call_streams(const lb_ctx* ctx) { return ctx ? ctx->last_call_streams : 0; }
+int lb_last_latency_clocks(const lb_ctx* ctx, uint64_t* out4) {
+  if (!ctx || !out4) return LB_ERR_INVALID_ARGUMENT;
+  for (int i = 0; i < 4; i++) out4[i] = ctx->lp_clk[i];
+  return LB_OK;
+}
 
 #ifdef LB_COUNT_OPS
 // Fp products executed per stage of the last completed verify call (count build only)

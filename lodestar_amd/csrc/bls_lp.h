@@ -69,6 +69,10 @@ struct LpCall {
   uint8_t* valid;     // n_req (zeroed)
   uint8_t* req_err;   // n_req (zeroed)
   uint32_t n_sets;
+  // diagnostics: [0] s_memrealtime (100 MHz) and [1] s_memtime (shader
+  // clock) when set 0's workgroup starts, [2] / [3] the same when request 0's verdict is
+  // written (zeroed; [2] and [3] by the workgroup that writes it)
+  unsigned long long* clk;
 };
 static constexpr uint32_t LB_LP_NIN = 11, LB_LP_NFL = 67;  // set program inputs / input flags
 __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __restrict__ req_off, uint32_t n_req,

@@ -534,6 +534,10 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
   __shared__ uint32_t sh_old, sh_bad, sh_err, s_fl[4];
   const uint32_t i = blockIdx.x, tid = threadIdx.x;
   if (i >= c.n_sets) return;
+  if (i == 0 && tid == 0 && c.clk) {
+    c.clk[0] = __builtin_amdgcn_s_memrealtime();
+    c.clk[1] = __builtin_amdgcn_s_memtime();
+  }
   const uint32_t k = c.set_req[i], base = c.req_off[k], n = c.req_off[k + 1] - base;
   const bool single = n == 1;
   // one interpreter call site, run per phase (the set program, each product of the
@@ -555,6 +559,10 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
       if (tid == 0) {
         c.valid[k] = s_fl[0] ? 1 : 0;
         c.req_err[k] = (sh_err & 2u) ? LB_REQ_EMPTY_AGGREGATE : (sh_err & 1u) ? LB_REQ_BAD_PUBKEY : LB_REQ_OK;
+        if (k == 0 && c.clk) {
+          c.clk[2] = __builtin_amdgcn_s_memrealtime();
+          c.clk[3] = __builtin_amdgcn_s_memtime();
+        }
       }
       return;
     }

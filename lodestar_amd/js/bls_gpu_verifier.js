@@ -525,6 +525,7 @@ class BlsGpuVerifier {
       try {
         const batch = packRequests([sets], this.seedSource(), this.keyMap);
         const r = await this.backends[0].verifyRequests(batch, this.priorityLane ? {priority: true} : undefined);
+        this.lastMainThreadResult = r;  // (diagnostics: deviceMs, the lane's kernelMs / kernelClockMHz)
         return this.requestVerdict(r, 0);
       } finally {
         const [s, ns] = process.hrtime(t0);

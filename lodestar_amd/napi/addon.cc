@@ -184,6 +184,7 @@ struct Task {
   uint32_t u32 = 0;
   uint64_t ticket = 0;
   uint64_t t_start = 0, t_end = 0, t_submitted = 0, t_retire = 0;
+  uint64_t clk[4] = {};  // latency-lane calls: lb_last_latency_clocks
   int rc = LB_OK;
   std::string errmsg;
   Task* target = nullptr;  // Finish: the two-phase call it resumes
@@ -347,6 +348,7 @@ void lane_loop(Context* c) {
     if (rc == LB_OK) {
       t->t_retire = now_ns();
       rc = lb_wait(c->lctx, t->ticket, &t->stats);
+      if (rc == LB_OK) lb_last_latency_clocks(c->lctx, t->clk);
     }
     if (rc != LB_OK) fail(t, rc, c->lctx);
     t->t_end = now_ns();
@@ -674,6 +676,11 @@ napi_value verify_result(napi_env env, Task* t) {
   set_num(env, o, "workerEndNs", (double)t->t_end);
   set_num(env, o, "workerSubmittedNs", (double)t->t_submitted);  // lb_verify_requests_async returned
   set_num(env, o, "workerRetireNs", (double)t->t_retire);        // lb_wait called on it
+  if (t->clk[2] > t->clk[0]) {  // latency lane: the kernel's own time and shader clock
+    const double rt = (double)(t->clk[2] - t->clk[0]);
+    set_num(env, o, "kernelMs", rt / 1e5);
+    set_num(env, o, "kernelClockMHz", (double)(t->clk[3] - t->clk[1]) / rt * 100.0);
+  }
   return o;
 }
 

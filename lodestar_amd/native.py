@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "lb_partial_wait", "lb_gt_check", "lb_verify_requests_finish", "lb_verify_same_message_batch",
     "lb_pubkeys_from_bytes", "lb_poll", "lb_set_latency_path", "lb_lp_program_run", "lb_scratch_per_queue",
     "lb_verify_requests_priority_async", "lb_partial_poll", "lb_hw_queues", "lb_last_call_streams",
-    "lb_create_lane", "lb_mark_priority",
+    "lb_create_lane", "lb_mark_priority", "lb_last_latency_clocks",
 )
 
 LB_BATCH_DEVICE = 1
@@ -131,6 +131,7 @@ def load_library() -> ctypes.CDLL:
     lib.lb_create.argtypes = [i32, ctypes.POINTER(vp)]
     lib.lb_create_lane.argtypes = [i32, ctypes.POINTER(vp)]
     lib.lb_mark_priority.argtypes = [vp]
+    lib.lb_last_latency_clocks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     lib.lb_destroy.argtypes = [vp]
     lib.lb_last_error.argtypes = [vp]
     lib.lb_last_error.restype = ctypes.c_char_p
@@ -272,6 +273,13 @@ class Device:
     def hw_queues(self) -> int:
         """HIP hardware queues this context opens (lb_hw_queues, priced by lb_create)."""
         return int(self.lib.lb_hw_queues(self._h))
+
+    def last_latency_clocks(self):
+        """(kernel ms by s_memrealtime at 100 MHz, shader clock MHz) of the last latency-path call"""
+        c = (ctypes.c_uint64 * 4)()
+        self._check(self.lib.lb_last_latency_clocks(self._h, c), "lb_last_latency_clocks")
+        rt = c[2] - c[0]
+        return (rt / 1e5, (c[3] - c[1]) / rt * 100.0) if rt > 0 and c[2] >= c[0] else (None, None)
 
     def last_call_streams(self) -> int:
         """Distinct streams of the last submitted verify call (2 = the two-stream DAG)."""

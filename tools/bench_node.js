@@ -58,6 +58,11 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
                   {type: "aggregate", pubkeys: keys, signingRoot: aggMsg.subarray(32 * a, 32 * a + 32),
                    signature: aggSig.subarray(96 * a, 96 * a + 96)}]);
   }
+  // a round in C4's proportions (SURVEY §8d: 901,696 single attestations beside 32,768
+  // AggregateAndProof triples): 220 jobs of 128 single sets + the triples
+  const singleJobs = [];
+  for (let j = 0; j < 220; j++) singleJobs.push(Array.from({length: 128}, (_, q) => single((j * 128 + q) % n)));
+  const roundSets = 220 * 128 + 3 * triples.length;
   const run = async (verifier, reps) => {
     const m = verifier.metrics;
     const h0 = m.hist.get(V.METRICS.PUBKEYS_AGGREGATION_MAIN_THREAD) || {count: 0, sum: 0};
@@ -65,24 +70,28 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
     const s0 = h0.sum;
     const t0 = Number(process.hrtime.bigint()) / 1e6;
     const all = [];
-    for (let r = 0; r < reps; r++) for (const t of triples) all.push(verifier.verifySignatureSets(t, {batchable: true}));
+    for (let r = 0; r < reps; r++) {
+      for (const js of singleJobs) all.push(verifier.verifySignatureSets(js, {batchable: true}));
+      for (const t of triples) all.push(verifier.verifySignatureSets(t, {batchable: true}));
+    }
     const okAll = (await Promise.all(all)).every((x) => x === true);
     const el = Number(process.hrtime.bigint()) / 1e6 - t0;
     const h = m.hist.get(V.METRICS.PUBKEYS_AGGREGATION_MAIN_THREAD) || {count: 0, sum: 0};
-    return {sets_per_s: Math.round((reps * triples.length * 3 * 1000) / el), keys_per_s: Math.round((reps * nAgg * (k + 2) * 1000) / el),
+    return {sets_per_s: Math.round((reps * roundSets * 1000) / el),
+            keys_per_s: Math.round((reps * (220 * 128 + nAgg * (k + 2)) * 1000) / el),
             pack_ms_per_package: h.count > c0 ? +(((h.sum - s0) / (h.count - c0)) * 1e3).toFixed(3) : null,
-            packages: h.count - c0, all_valid: okAll};
+            packages: h.count - c0, rounds: reps, all_valid: okAll};
   };
-  await run(w, 1);  // warm-up
-  const mirrored = await run(w, 4);
+  await run(w, 2);  // warm-up
+  const mirrored = await run(w, 32);
   await w.close();
   // the same calls on a verifier whose tables do not hold the keys: every key serialized
   const u = new V.BlsGpuVerifier({devices: [0]});
   await run(u, 1);
-  const unmirrored = await run(u, 1);
+  const unmirrored = await run(u, 4);
   await u.close();
-  return {triples_per_round: triples.length, keys_per_aggregate: k, sync_index2pubkey_ms: +syncMs.toFixed(1),
-          mirrored, unmirrored,
+  return {sets_per_round: roundSets, triples_per_round: triples.length, keys_per_aggregate: k,
+          sync_index2pubkey_ms: +syncMs.toFixed(1), mirrored, unmirrored,
           api: "verifySignatureSets([selection proof, aggregator sig, aggregate of " + k +
                " keys], {batchable}) with index2pubkey PublicKey objects"};
 }
@@ -113,6 +122,17 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   // latency on an idle verifier, before the throughput phase
   const pre128 = [];
   const pre1 = [];
+  const clkPre = [];
+  const clkAfter = [];
+  // where a lone call's time goes: the lane's device time (first to last event of the call),
+  // the kernel's own time and shader clock (s_memrealtime / s_memtime inside k_lp_verify)
+  const clockSummary = (rs) => {
+    const f = (k) => {
+      const xs = rs.filter((r) => r && r[k] !== undefined).map((r) => r[k]);
+      return xs.length ? +median(xs).toFixed(3) : null;
+    };
+    return {device_ms: f("deviceMs"), kernel_ms: f("kernelMs"), kernel_clock_mhz: f("kernelClockMHz")};
+  };
   if (process.env.LB_JS_TRACE === "1") v.trace = [];
   for (let r = 0; r < 11; r++) {
     let t = Number(process.hrtime.bigint()) / 1e6;
@@ -121,6 +141,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
     t = Number(process.hrtime.bigint()) / 1e6;
     ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
     pre1.push(Number(process.hrtime.bigint()) / 1e6 - t);
+    clkPre.push(v.lastMainThreadResult);
   }
   const latSummary = (tr) => {
     const avg = (f) => +(tr.reduce((s, x) => s + f(x), 0) / Math.max(tr.length, 1) / 1e6).toFixed(3);
@@ -240,6 +261,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
     t = ms();
     ok = ok && (await v.verifySignatureSets([set(r)], {verifyOnMainThread: true})) === true;
     lat1.push(ms() - t);
+    clkAfter.push(v.lastMainThreadResult);
   }
   let latTraceAfter = null;
   if (v.trace) {
@@ -269,6 +291,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
       // the same after the throughput phase (a process that has just run 96 packages)
       p50_ms_128set_after_throughput: +median(lat128).toFixed(3),
       p50_ms_1set_after_throughput: +median(lat1).toFixed(3),
+      lane_1set_clocks: {fresh: clockSummary(clkPre), after_throughput: clockSummary(clkAfter)},
       // while every slot is busy with a 65,536-set package (priority lane)
       under_load: {
         p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
