@@ -175,6 +175,18 @@ class ErrorText {
   std::string s_;
 };
 
+// A released two-phase call (LB_TP_RELEASE): what lb_partial_wait, lb_verify_requests_finish
+// and lb_wait need once its slot has moved on -- the partial, and the call itself (the
+// caller's buffers stay valid until lb_wait returns) for a re-run when the combine fails.
+struct TwoPhaseRec {
+  uint64_t ticket = 0;
+  bool device = false, finished = false, have_partial = false;
+  uint64_t rerun = 0;  // the one-phase re-run's ticket (failed combine)
+  lb_request_batch batch{};
+  uint8_t *valid = nullptr, *err = nullptr, *sst = nullptr;
+  uint8_t partial[LB_GT_BYTES];
+};
+
 // Stats of a retired call, kept per ticket (lb_wait reports the stats of ITS
 // ticket even when another call retired the slot first).
 struct TicketStats {
@@ -219,6 +231,12 @@ struct lb_ctx {
   static constexpr int kTwoPhaseRing = 256;
   uint64_t two_phase[kTwoPhaseRing] = {};
   int two_phase_pos = 0;
+  // LB_TP_RELEASE (default 1): a two-phase call completes as if the combined check passed and
+  // frees its slot when its partial is out, instead of holding the slot through the host's
+  // combine (-5..-7 % at N = 1); a failed combined check re-runs the shard
+  // as a one-phase call.  One record per two-phase ticket (ring by ticket).
+  bool tp_release = true;
+  TwoPhaseRec tp[kTwoPhaseRing];
   ErrorText err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
   // Miller organisation: stored lines + one wave per pair (k_lines/k_pair_wc,
@@ -839,6 +857,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
         LB_HIP(hipEventRecord(sl.dep[4], ts));
         LB_HIP(hipStreamWaitEvent(sl.st[0], sl.dep[4], 0));
       }
+      if (ctx->tp_release) {
+        // the call completes on its own as if the combined check passed (every request not
+        // already false valid: no per-request work) and frees its slot at once; a failed
+        // combined check re-verifies the shard as a one-phase call (lb_verify_requests_finish)
+        LB_HIP(hipMemsetAsync(d_mflag, 1, 1, sl.st[0]));
+        return run_tails(ctx, sl);
+      }
       sl.partial_pending = true;
       return LB_OK;
     }
@@ -957,6 +982,13 @@ int finish_slot(lb_ctx* ctx, Slot& sl) {
   ctx->batch_sigs_success = sl.h_stats[1];
   if (sl.lp_call)
     for (int i = 0; i < 4; i++) ctx->lp_clk[i] = sl.h_clk[i];
+  {  // a released two-phase call: its partial outlives the slot
+    TwoPhaseRec& r = ctx->tp[sl.ticket % lb_ctx::kTwoPhaseRing];
+    if (sl.ticket && r.ticket == sl.ticket && !r.have_partial) {
+      memcpy(r.partial, sl.h_partial, LB_GT_BYTES);
+      r.have_partial = true;
+    }
+  }
   TicketStats& ts = ctx->tstats[sl.ticket % lb_ctx::kTicketRing];
   ts.ticket = sl.ticket;
   ts.batch_retries = sl.h_stats[0];
@@ -1149,6 +1181,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = atoi(e) != 0;
   if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_MAX")) {
     const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
@@ -1453,6 +1486,31 @@ static void pick_streams(lb_ctx* ctx, Slot& sl) {
   if (sl.guard_st) sl.st[1] = sl.guard_st;
 }
 
+// a two-phase call's record (LB_TP_RELEASE; the legacy mode keeps only the ticket ring)
+static void tp_record(lb_ctx* ctx, uint64_t ticket, const lb_request_batch* b, bool device, uint8_t* valid,
+                      uint8_t* err, uint8_t* sst) {
+  if (!ctx->tp_release) return;
+  TwoPhaseRec& r = ctx->tp[ticket % lb_ctx::kTwoPhaseRing];
+  r.ticket = ticket;
+  r.device = device;
+  r.finished = r.have_partial = false;
+  r.rerun = 0;
+  r.batch = *b;
+  r.valid = valid;
+  r.err = err;
+  r.sst = sst;
+  if (!b->n_requests) {  // an empty shard: its partial is 1, known now
+    memset(r.partial, 0, LB_GT_BYTES);
+    r.partial[47] = 1;
+    r.have_partial = true;
+  }
+}
+
+static TwoPhaseRec* tp_find(lb_ctx* ctx, uint64_t ticket) {
+  TwoPhaseRec& r = ctx->tp[ticket % lb_ctx::kTwoPhaseRing];
+  return (ticket && ctx->tp_release && r.ticket == ticket) ? &r : nullptr;
+}
+
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
                          uint8_t* d_set_status, bool partial, uint64_t* out_ticket) {
   LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
@@ -1471,10 +1529,11 @@ static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8
     sl.h_partial[47] = 1;
     LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
     sl.ps = PipeState{};
-    sl.partial_pending = true;
+    sl.partial_pending = !ctx->tp_release;
   }
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
+  if (partial) tp_record(ctx, sl.ticket, b, true, d_valid, d_req_err, d_set_status);
   return LB_OK;
 }
 
@@ -1616,10 +1675,11 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
     sl.h_partial[47] = 1;
     LB_HIP(hipEventRecord(sl.partial_ev, sl.st[0]));
     sl.ps = PipeState{};
-    sl.partial_pending = true;
+    sl.partial_pending = !ctx->tp_release;
   }
   LB_TRY(end_call_async(ctx, sl));
   *out_ticket = sl.ticket;
+  if (partial) tp_record(ctx, sl.ticket, b, false, out_valid, out_req_err, out_set_status);
   if (host_trace())
     fprintf(stderr, "lb_host_trace sets=%u check=%.3f finish_slot=%.3f stage=%.3f pipeline=%.3f total=%.3f dag=%d slot=%d\n",
             ns, t_check, t_finish, t_stage, t_pipe, ms_since(t0), sl.st[1] != sl.st[0] ? 1 : 0,
@@ -1693,6 +1753,17 @@ int lb_partial_wait(lb_ctx* ctx, uint64_t ticket, uint8_t* out576) {
   if (!ctx || !out576) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   Slot* sl = slot_of_ticket(ctx, ticket);
+  if (TwoPhaseRec* r = tp_find(ctx, ticket)) {  // released: on its slot, or saved when it retired
+    if (!r->have_partial && sl) {
+      LB_HIP(hipEventSynchronize(sl->partial_ev));
+      memcpy(out576, sl->h_partial, LB_GT_BYTES);
+      return LB_OK;
+    }
+    if (r->have_partial) {
+      memcpy(out576, r->partial, LB_GT_BYTES);
+      return LB_OK;
+    }
+  }
   if (!sl || !sl->partial_pending) {
     ctx->err = "ticket is not a pending two-phase call";
     return LB_ERR_INVALID_ARGUMENT;
@@ -1706,6 +1777,22 @@ int lb_partial_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_ready) {
   if (!ctx || !out_ready) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   Slot* sl = slot_of_ticket(ctx, ticket);
+  if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
+    if (r->have_partial) {
+      *out_ready = 1;
+      return LB_OK;
+    }
+    if (sl) {
+      const hipError_t q = hipEventQuery(sl->partial_ev);
+      if (q == hipErrorNotReady) {
+        *out_ready = 0;
+        return LB_OK;
+      }
+      LB_HIP(q);
+      *out_ready = 1;
+      return LB_OK;
+    }
+  }
   if (!sl || !sl->partial_pending) {
     ctx->err = "ticket is not a pending two-phase call";
     return LB_ERR_INVALID_ARGUMENT;
@@ -1723,6 +1810,23 @@ int lb_partial_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_ready) {
 int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
+  if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
+    if (r->finished) return LB_OK;
+    r->finished = true;
+    if (merged_ok) return LB_OK;  // its verdicts (every request not already false valid) stand
+    // the combined check failed: the shard again as a one-phase call -- its own merged check
+    // fails and every request is verified alone (worker.ts:74-85) -- into the same outputs,
+    // after the released call has retired (its verdicts must not land after the re-run's)
+    if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
+    const lb_request_batch b = r->batch;
+    uint8_t *v = r->valid, *e = r->err, *st = r->sst;
+    const bool device = r->device;
+    uint64_t t2 = 0;
+    LB_TRY(device ? submit_device(ctx, next_async_slot(ctx), &b, v, e, st, false, &t2)
+                  : submit_host(ctx, next_async_slot(ctx), &b, v, e, st, false, &t2));
+    if (TwoPhaseRec* r2 = tp_find(ctx, ticket)) r2->rerun = t2;
+    return LB_OK;
+  }
   Slot* sl = slot_of_ticket(ctx, ticket);
   if (!sl || !sl->partial_pending) {
     // a two-phase call another call's slot reuse already resumed (with merged_ok
@@ -1795,6 +1899,13 @@ int lb_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_done) {
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(sm_pump(ctx));
   *out_done = 1;
+  if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
+    if (!r->finished) {  // (lb_wait would first finish it with merged_ok = 0)
+      *out_done = 0;
+      return LB_OK;
+    }
+    if (r->rerun) ticket = r->rerun;
+  }
   Slot* sl = slot_of_ticket(ctx, ticket);
   if (!sl) return LB_OK;  // retired
   // (a same-message package's phase 1 still running: sm_pump above found it unfinished;
@@ -1816,6 +1927,11 @@ int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(sm_pump(ctx));
+  if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
+    // waited for without a combined verdict: as before, each request verified alone
+    if (!r->finished) LB_TRY(lb_verify_requests_finish(ctx, ticket, 0));
+    if (TwoPhaseRec* r2 = tp_find(ctx, ticket); r2 && r2->rerun) ticket = r2->rerun;
+  }
   if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
   fill_stats(ctx, ticket, stats);
   return LB_OK;
