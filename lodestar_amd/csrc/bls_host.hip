@@ -1927,13 +1927,23 @@ int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   if (!ctx) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(sm_pump(ctx));
+  bool rerun = false;
   if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
     // waited for without a combined verdict: as before, each request verified alone
     if (!r->finished) LB_TRY(lb_verify_requests_finish(ctx, ticket, 0));
-    if (TwoPhaseRec* r2 = tp_find(ctx, ticket); r2 && r2->rerun) ticket = r2->rerun;
+    if (TwoPhaseRec* r2 = tp_find(ctx, ticket); r2 && r2->rerun) {
+      ticket = r2->rerun;
+      rerun = true;
+    }
   }
   if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
   fill_stats(ctx, ticket, stats);
+  // a re-run after a failed combined check: the shard's batch failed once and every request
+  // was verified alone (worker.ts:74-85 counts that as one retry of the merged batch)
+  if (rerun && stats) {
+    stats->batch_retries = 1;
+    stats->batch_sigs_success = 0;
+  }
   return LB_OK;
 }
 
