@@ -523,9 +523,15 @@ class BlsGpuVerifier {
       // not block the event loop, unlike blst on the reference's main thread)
       const t0 = process.hrtime();
       try {
+        const d0 = this.trace ? hrNowNs() : 0;
         const batch = packRequests([sets], this.seedSource(), this.keyMap);
+        const packed = this.trace ? hrNowNs() : 0;
         const r = await this.backends[0].verifyRequests(batch, this.priorityLane ? {priority: true} : undefined);
         this.lastMainThreadResult = r;  // (diagnostics: deviceMs, the lane's kernelMs / kernelClockMHz)
+        if (this.trace)
+          this.trace.push({main: true, dispatchNs: d0, packedNs: packed, submittedNs: packed, backNs: hrNowNs(),
+                           workerStartNs: r.workerStartNs, workerEndNs: r.workerEndNs, deviceMs: r.deviceMs,
+                           workerSubmittedNs: r.workerSubmittedNs, workerRetireNs: r.workerRetireNs});
         return this.requestVerdict(r, 0);
       } finally {
         const [s, ns] = process.hrtime(t0);
@@ -727,7 +733,7 @@ class BlsGpuVerifier {
           m.observe(M.PUBKEYS_AGGREGATION_MAIN_THREAD, s0 + ns0 / 1e9);
         const packedNs = hrNowNs();
         waits.push(priority ? backend.verifyRequests(batch, {priority: true}) : backend.verifyRequests(batch));
-        if (this.trace) this.trace.push({dispatchNs, packedNs, submittedNs: hrNowNs(), inFlight: this.running.size});
+        if (this.trace) this.trace.push({dispatchNs, packedNs, submittedNs: hrNowNs(), inFlight: this.running.size, prio: priority});
       }
       if (same.length) {
         // jobItem.ts:72-74 times Signature.fromBytes on the main thread; here the bytes are

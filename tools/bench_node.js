@@ -238,6 +238,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   const tLoad = ms();
   const loadJobs0 = loadDoneJobs;
   const samples = parseInt(process.env.LB_NODE_LOAD_SAMPLES || "25", 10);
+  if (process.env.LB_JS_TRACE === "1") v.trace = [];
   for (let r = 0; r < samples; r++) {
     let t = ms();
     ok = ok && (await v.verifySignatureSets([set(r + 7)], {verifyOnMainThread: true})) === true;
@@ -248,6 +249,12 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
     await new Promise((res) => setTimeout(res, 10));
   }
   const loadRate = ((loadDoneJobs - loadJobs0) * 128 * 1000) / (ms() - tLoad);
+  let loadTrace = null;
+  if (v.trace) {  // the priority calls' phases under load (the packages' own entries left out)
+    loadTrace = {set1: latSummary(v.trace.filter((x) => x.main && x.backNs)),
+                 set128: latSummary(v.trace.filter((x) => !x.main && x.backNs && x.inFlight !== undefined && x.prio))};
+    v.trace = null;
+  }
   stop = true;
   await Promise.all(loadAll);
   ok = ok && loadBad === 0;
@@ -266,8 +273,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   let latTraceAfter = null;
   if (v.trace) {
     latTraceAfter = {
-      set128: latSummary(v.trace.filter((x, q) => x.backNs && q % 2 === 0)),
-      set1: latSummary(v.trace.filter((x, q) => x.backNs && q % 2 === 1)),
+      set128: latSummary(v.trace.filter((x) => x.backNs && !x.main)),
+      set1: latSummary(v.trace.filter((x) => x.backNs && x.main)),
     };
     v.trace = null;
   }
@@ -305,6 +312,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
       ...(trace ? {trace} : {}),
       ...(latTrace ? {latency_trace: latTrace} : {}),
       ...(latTraceAfter ? {latency_trace_after_throughput: latTraceAfter} : {}),
+      ...(loadTrace ? {latency_trace_under_load: loadTrace} : {}),
       ...(c4 ? {c4_public_key_objects: c4} : {}),
       all_valid: ok,
       table_size: tableSize,
