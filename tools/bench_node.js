@@ -306,6 +306,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
         ratio_1set_vs_idle: load1.length ? +(median(load1) / median(pre1)).toFixed(2) : null,
         ratio_128set_vs_idle: load128.length ? +(median(load128) / median(pre128)).toFixed(2) : null,
         samples: load1.length,
+        ...(process.env.LB_JS_TRACE === "1"
+          ? {ms_1set: load1.map((x) => +x.toFixed(2)), ms_128set: load128.map((x) => +x.toFixed(2))} : {}),
         load_packages_queued: loadPackages,
         background_sets_per_s: Math.round(loadRate),
       },
