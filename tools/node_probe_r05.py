@@ -22,8 +22,8 @@ def main():
     dev = Device(0)
     sks, pks, msgs, sigs = make_workload(dev, 65536, 0, hashlib.sha256(b"lodestar-mi355x-bench").digest())
     dev.close()
-    d = os.path.join(out, "data")
-    os.makedirs(d, exist_ok=True)
+    import tempfile
+    d = tempfile.mkdtemp(prefix="lb_node_probe_")  # (not under gpurun_out: ~17 MB of inputs)
     for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
         with open(os.path.join(d, name + ".bin"), "wb") as f:
             f.write(b"".join(items))
@@ -44,6 +44,8 @@ def main():
     res["gc"] = {"events": len(gc), "pause_ms_total": round(sum(pauses), 1),
                  "pause_ms_max": round(max(pauses), 1) if pauses else 0,
                  "mark_sweep": sum(1 for ln in gc if "Mark" in ln)}
+    import shutil
+    shutil.rmtree(d, ignore_errors=True)
     print(json.dumps(res))
 
 
