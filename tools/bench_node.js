@@ -233,16 +233,38 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   };
   refill();
   await new Promise((r) => setTimeout(r, 300));  // the pipe full
+  // onset: a verifyOnMainThread set arriving after >= 600 ms without priority traffic (every
+  // call in flight on the full streams, the CU reservation lapsed): the first block of a
+  // slot under gossip load.  A priority call's workgroups cannot preempt the throughput
+  // waves already on the GPU, so it waits for CUs to drain (DESIGN.md §7).
+  const onset1 = [];
+  for (let r = 0; r < 5; r++) {
+    await new Promise((res) => setTimeout(res, 600));
+    const t = ms();
+    ok = ok && (await v.verifySignatureSets([set(r + 3)], {verifyOnMainThread: true})) === true;
+    onset1.push(ms() - t);
+  }
+  // steady state: priority traffic every ~10 ms (the reservation held)
   const load1 = [];
   const load128 = [];
+  const detail1 = [];
   const tLoad = ms();
   const loadJobs0 = loadDoneJobs;
   const samples = parseInt(process.env.LB_NODE_LOAD_SAMPLES || "25", 10);
   if (process.env.LB_JS_TRACE === "1") v.trace = [];
+  // (the first priority calls after the onset still find the calls submitted before it on the
+  // full streams: 300 ms of warm-up traffic, not sampled)
+  for (const tEnd = ms() + 300; ms() < tEnd;) {
+    ok = ok && (await v.verifySignatureSets([set(1)], {verifyOnMainThread: true})) === true;
+    await new Promise((res) => setTimeout(res, 10));
+  }
   for (let r = 0; r < samples; r++) {
     let t = ms();
     ok = ok && (await v.verifySignatureSets([set(r + 7)], {verifyOnMainThread: true})) === true;
     load1.push(ms() - t);
+    const lr = v.lastMainThreadResult || {};
+    detail1.push([+load1[load1.length - 1].toFixed(2), +(((lr.workerEndNs || 0) - (lr.workerStartNs || 0)) / 1e6).toFixed(2),
+                  +(lr.deviceMs || 0).toFixed(2), +(lr.kernelMs || 0).toFixed(2)]);
     t = ms();
     ok = ok && (await v.verifySignatureSets(jobs[(r + 3) % jobs.length], {priority: true})) === true;
     load128.push(ms() - t);
@@ -300,6 +322,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
       p50_ms_1set_after_throughput: +median(lat1).toFixed(3),
       lane_1set_clocks: {fresh: clockSummary(clkPre), after_throughput: clockSummary(clkAfter)},
       // while every slot is busy with a 65,536-set package (priority lane)
+      under_load_onset: {ms_1set: onset1.map((x) => +x.toFixed(2)), p50_ms_1set: +median(onset1).toFixed(3),
+                         gap_ms: 600},
       under_load: {
         p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
         p50_ms_128set_priority: load128.length ? +median(load128).toFixed(3) : null,
@@ -307,7 +331,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
         ratio_128set_vs_idle: load128.length ? +(median(load128) / median(pre128)).toFixed(2) : null,
         samples: load1.length,
         ...(process.env.LB_JS_TRACE === "1"
-          ? {ms_1set: load1.map((x) => +x.toFixed(2)), ms_128set: load128.map((x) => +x.toFixed(2))} : {}),
+          ? {ms_1set: load1.map((x) => +x.toFixed(2)), ms_128set: load128.map((x) => +x.toFixed(2)),
+             detail_1set_total_lane_device_kernel_ms: detail1} : {}),
         load_packages_queued: loadPackages,
         background_sets_per_s: Math.round(loadRate),
       },
