@@ -380,6 +380,79 @@ LB_DEV void clear_cofactor_g2(g2j& r, const g2j& p, g2j* stash = nullptr) {
   jac_add(r, D, t);
 }
 
+// Register-lean form of clear_cofactor_g2 for the throughput kernel (k_hash_finish):
+// every point that is not being worked on waits in global memory (two per-lane slots),
+// so across each |x|-ladder only its accumulator and the doubling's temporaries are
+// live -- the base is re-read at the ladder's 5 additions and for the final Z product.
+// The same operations in the same order as clear_cofactor_g2 (bit-identical output).
+// A compiler barrier before each re-read keeps it a load (no value held across the loop).
+LB_DEV void g2_load_barrier(g2j& r, const g2j* m) {
+  __asm__ volatile("" ::: "memory");
+  r = *m;
+}
+LB_DEV void g2_mul_xabs_mem(g2j& r, const g2j* pm) {
+  g2j acc;
+  g2_load_barrier(acc, pm);
+  if (jac_is_inf(acc)) {
+    r = acc;
+    return;
+  }
+  fp2_one(acc.Z);
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((LB_X_ABS >> i) & 1ull) {
+      __asm__ volatile("" ::: "memory");
+      g2a q;
+      q.x = pm->X;
+      q.y = pm->Y;
+      q.inf = false;
+      jac_add_aff(acc, acc, q);
+    }
+  }
+  __asm__ volatile("" ::: "memory");
+  const fp2 z = pm->Z;
+  fmul(acc.Z, acc.Z, z);
+  r = acc;
+}
+// g2_in_subgroup (psi(P) == [x]P) with P in memory: across the ladder only its
+// accumulator is live (k_decode_sigs parks the decoded point in its output slot).
+LB_DEV bool g2_in_subgroup_mem(const g2j* pm) {
+  g2j xp, ps;
+  g2_load_barrier(ps, pm);
+  if (jac_is_inf(ps)) return true;
+  g2_mul_xabs_mem(xp, pm);
+  jac_neg(xp, xp);
+  g2_load_barrier(ps, pm);
+  g2_psi(ps, ps);
+  return jac_eq(ps, xp);
+}
+
+// On entry sP holds P; sB is a second slot.  r = h_eff P.
+LB_DEV void clear_cofactor_g2_mem(g2j& r, g2j* sP, g2j* sB) {
+  g2j A, B, t, D;
+  g2_mul_xabs_mem(A, sP);  // A = [z]P
+  g2_load_barrier(t, sP);
+  g2_psi(B, t);
+  jac_neg(A, A);
+  jac_add(B, B, A);  // B = psi(P) - A
+  *sB = B;
+  g2_load_barrier(t, sP);
+  jac_neg(D, t);
+  jac_dbl(t, t);
+  g2_psi(t, t);
+  g2_psi(t, t);      // psi^2(2P)
+  jac_add(t, t, D);  // psi^2(2P) - P
+  g2_load_barrier(B, sB);
+  jac_neg(D, B);
+  jac_add(D, t, D);  // D
+  *sP = D;           // (P is no longer needed)
+  g2_mul_xabs_mem(t, sB);  // C
+  jac_neg(t, t);
+  g2_load_barrier(D, sP);
+  jac_add(r, D, t);
+}
+
 // One half of hash_to_curve: u_j = hash_to_field(msg)[j] -> SSWU -> iso (Jacobian).
 // Two lanes per message run j = 0, 1 concurrently (the halves are independent).
 LB_DEV void hash_to_g2_half(g2j& r, const uint8_t msg[32], int j) {

@@ -629,7 +629,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   LB_TRY(stream_wait(ctx, sl, 0, 1, 0));
   if (n_sets) {
     LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
-    LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, (const g2j*)d_q, d_h);
+    LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, d_q, d_h);
   }
   LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
   if (steps) {  // size-descending order and row offsets (before stream 1's lines)
@@ -659,10 +659,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   if (steps) {
     if (ctx->lines_waves == 1)
       LB_STAGE("lines", 1, k_lines_rows<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
-               (const g1j*)d_rpk, (const g2j*)d_h, d_lines);
+               (const g1j*)d_rpk, d_h, d_lines);
     else
       LB_STAGE("lines", 1, k_lines_rows<2>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
-               (const g1j*)d_rpk, (const g2j*)d_h, d_lines);
+               (const g1j*)d_rpk, d_h, d_lines);
   } else if (n_sets && (by_lines || by_wave)) {
     // (small calls are latency-bound: the spill-free one-wave build unless LB_LINES_WAVES=2)
     if (ctx->lines_waves_small == 1)

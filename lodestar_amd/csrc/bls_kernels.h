@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(TPB) k_pubkey_validate(uint32_t n, const uint8
                                                          uint8_t* __restrict__ out96, uint8_t* __restrict__ status);
 __global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const uint8_t* __restrict__ msgs,
                                                    g2j* __restrict__ q);
-__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h);
+__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, g2j* __restrict__ q, g2j* __restrict__ out_h);
 __global__ void __launch_bounds__(TPB, LB_W_SSIG) k_scalar_sig(uint32_t n, const uint8_t* __restrict__ seed,
                                                     const g2j* __restrict__ sig,
                                                     const uint8_t* __restrict__ sig_status,
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) k_rows_pos(uint32_t n_req, const uint32_t
 template <int WAVES>
 __global__ void __launch_bounds__(TPB, WAVES) k_lines_rows(uint32_t n_sets, uint32_t n_pairs, Rows R,
                                                            const uint32_t* __restrict__ req_off,
-                                                           const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                           const g1j* __restrict__ P, g2j* __restrict__ Q,
                                                            uint32_t* __restrict__ lines);
 __global__ void __launch_bounds__(TPB) k_req_status(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                     const uint8_t* __restrict__ sig_status,

@@ -18,11 +18,23 @@ __global__ void __launch_bounds__(TPB, LB_W_MAP) k_hash_half(uint32_t n, const u
 }
 // hash_to_G2, second half: Q0 + Q1, clear cofactor (Jacobian out: the
 // affine conversion shares its inversion with r_i pk_i, jac_pair_to_aff)
-__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, const g2j* __restrict__ q, g2j* __restrict__ out_h) {
+// LB_HASH_FINISH_MEM (default): the register-lean cofactor clearing, the two halves' slots
+// of q (consumed here) holding the points that are not being worked on
+__global__ void __launch_bounds__(TPB, LB_W_HASH) k_hash_finish(uint32_t n, g2j* __restrict__ q, g2j* __restrict__ out_h) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  g2j q0 = q[2 * i], q1 = q[2 * i + 1], h;
+  g2j h;
+#ifdef LB_HASH_FINISH_REGS
+  g2j q0 = q[2 * i], q1 = q[2 * i + 1];
   hash_to_g2_finish(h, q0, q1, out_h + i);  // out_h[i] doubles as the stash
+#else
+  {
+    g2j q0 = q[2 * i], q1 = q[2 * i + 1], s;
+    jac_add(s, q0, q1);
+    q[2 * i] = s;
+  }
+  clear_cofactor_g2_mem(h, q + 2 * i, q + 2 * i + 1);
+#endif
   out_h[i] = h;
 }
 

@@ -25,12 +25,18 @@ __global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, co
   uint8_t st = g2_deserialize(s, sigs + a, b - a);
   g2j sj;
   jac_set_inf(sj);
+  if (st == LB_ST_OK) jac_from_aff(sj, s);
+  // the decoded point waits in its output slot across the subgroup check's ladder
+  out_sig[i] = sj;
   if (st == LB_ST_OK) {
-    jac_from_aff(sj, s);
-    if (!g2_in_subgroup(sj)) st = LB_ST_NOT_IN_GROUP;
+#ifdef LB_DECODE_REGS
+    const bool in_group = g2_in_subgroup(sj);
+#else
+    const bool in_group = g2_in_subgroup_mem(out_sig + i);
+#endif
+    if (!in_group) st = LB_ST_NOT_IN_GROUP;
     else if (single_flag && single_flag[i] && s.inf) st = LB_ST_ZERO_SIGNATURE;
   }
-  out_sig[i] = sj;
   status[i] = st;
 }
 

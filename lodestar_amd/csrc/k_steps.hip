@@ -131,10 +131,13 @@ LB_DEV void slot_row(const Rows& R, uint32_t q, uint32_t& i, uint32_t& r) {
 }
 
 // Lines of every set pair, stored at its slot: lane q is slot q (coalesced stores).
+// (LB_LINES_QREGS: Q held in registers; default: the affine H(m) replaces its Jacobian
+// form in Q -- which nothing reads after this kernel -- and the Miller loop re-reads it at
+// its 5 addition steps, miller_lines_qmem)
 template <int WAVES>
 __global__ void __launch_bounds__(TPB, WAVES) k_lines_rows(uint32_t n_sets, uint32_t n_pairs, Rows R,
                                                            const uint32_t* __restrict__ req_off,
-                                                           const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                           const g1j* __restrict__ P, g2j* __restrict__ Q,
                                                            uint32_t* __restrict__ lines) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n_sets) return;
@@ -142,9 +145,29 @@ __global__ void __launch_bounds__(TPB, WAVES) k_lines_rows(uint32_t n_sets, uint
   slot_row(R, q, i, r);
   const uint32_t s = req_off[R.inv[r]] + i;
   g1a p;
+#ifdef LB_LINES_QREGS
   g2a h;
   jac_pair_to_aff(p, h, P[s], Q[s]);
   miller_lines(p, h, lines, n_pairs, q);
+#else
+  bool h_inf;
+  {
+    g2a h;
+    jac_pair_to_aff(p, h, P[s], Q[s]);
+    h_inf = h.inf;
+    if (!p.inf && !h.inf) {
+      Q[s].X = h.x;
+      Q[s].Y = h.y;
+    }
+  }
+  if (p.inf || h_inf) {
+    g2a none;
+    none.inf = true;
+    miller_lines(p, none, lines, n_pairs, q);  // (unit lines)
+  } else {
+    miller_lines_qmem(p, Q + s, lines, n_pairs, q);
+  }
+#endif
 }
 
 // Request status of the steps organisation (what k_miller_acc reduces on the
@@ -501,7 +524,7 @@ LB_INST_STEP(0, 2)
 LB_INST_STEP(2, 2)
 #define LB_INST_LINES_ROWS(W)                                                                                    \
   template __global__ void k_lines_rows<W>(uint32_t, uint32_t, Rows, const uint32_t* __restrict__,                \
-                                           const g1j* __restrict__, const g2j* __restrict__, uint32_t* __restrict__);
+                                           const g1j* __restrict__, g2j* __restrict__, uint32_t* __restrict__);
 LB_INST_LINES_ROWS(1)
 LB_INST_LINES_ROWS(2)
 
