@@ -384,19 +384,17 @@ LB_DEV void clear_cofactor_g2(g2j& r, const g2j& p, g2j* stash = nullptr) {
 // every point that is not being worked on waits in global memory (two per-lane slots),
 // so across each |x|-ladder only its accumulator and the doubling's temporaries are
 // live -- the base is re-read at the ladder's 5 additions and for the final Z product.
-// The same operations in the same order as clear_cofactor_g2 (bit-identical output).
+// The same operations in the same order as clear_cofactor_g2 (bit-identical output for
+// a finite P; an infinite one gives an infinity of another X, Y).
 // A compiler barrier before each re-read keeps it a load (no value held across the loop).
 LB_DEV void g2_load_barrier(g2j& r, const g2j* m) {
   __asm__ volatile("" ::: "memory");
   r = *m;
 }
 LB_DEV void g2_mul_xabs_mem(g2j& r, const g2j* pm) {
+  // (no branch on infinity: P = (X:Y:0) ends with Z = Z_acc * 0, infinity again)
   g2j acc;
   g2_load_barrier(acc, pm);
-  if (jac_is_inf(acc)) {
-    r = acc;
-    return;
-  }
   fp2_one(acc.Z);
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
@@ -415,12 +413,10 @@ LB_DEV void g2_mul_xabs_mem(g2j& r, const g2j* pm) {
   fmul(acc.Z, acc.Z, z);
   r = acc;
 }
-// g2_in_subgroup (psi(P) == [x]P) with P in memory: across the ladder only its
-// accumulator is live (k_decode_sigs parks the decoded point in its output slot).
+// g2_in_subgroup (psi(P) == [x]P) with P (not infinity) in memory: across the ladder
+// only its accumulator is live (k_decode_sigs parks the decoded point in its output slot).
 LB_DEV bool g2_in_subgroup_mem(const g2j* pm) {
   g2j xp, ps;
-  g2_load_barrier(ps, pm);
-  if (jac_is_inf(ps)) return true;
   g2_mul_xabs_mem(xp, pm);
   jac_neg(xp, xp);
   g2_load_barrier(ps, pm);

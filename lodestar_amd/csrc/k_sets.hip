@@ -26,18 +26,24 @@ __global__ void __launch_bounds__(TPB, LB_W_DECODE) k_decode_sigs(uint32_t n, co
   g2j sj;
   jac_set_inf(sj);
   if (st == LB_ST_OK) jac_from_aff(sj, s);
-  // the decoded point waits in its output slot across the subgroup check's ladder
+#ifdef LB_DECODE_REGS
   out_sig[i] = sj;
   if (st == LB_ST_OK) {
-#ifdef LB_DECODE_REGS
     const bool in_group = g2_in_subgroup(sj);
-#else
-    const bool in_group = g2_in_subgroup_mem(out_sig + i);
-#endif
     if (!in_group) st = LB_ST_NOT_IN_GROUP;
     else if (single_flag && single_flag[i] && s.inf) st = LB_ST_ZERO_SIGNATURE;
   }
   status[i] = st;
+#else
+  // the decoded point waits in its output slot across the subgroup check's ladder;
+  // the status is final before it (only a failed check rewrites it), so nothing but
+  // the ladder's own state lives across it
+  if (st == LB_ST_OK && s.inf && single_flag && single_flag[i]) st = LB_ST_ZERO_SIGNATURE;
+  const bool ladder = st == LB_ST_OK && !s.inf;  // (infinity is in the group)
+  out_sig[i] = sj;
+  status[i] = st;
+  if (ladder && !g2_in_subgroup_mem(out_sig + i)) status[i] = LB_ST_NOT_IN_GROUP;
+#endif
 }
 
 // Sets with exactly one pubkey (the common case): one lane per set.
