@@ -1338,6 +1338,16 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   // flight: a synchronous copy on the first latency-path call would wait for the
   // throughput calls already running on blocking (CU-masked) streams
   if (ok && (ctx->lp_max_sets || ctx->mtail_lp || ctx->gt_lp) && lp_ensure(ctx) != LB_OK) ok = false;
+  // the priority slot's staging and workspace sized here for a latency-path call of
+  // lp_max_sets sets (16 keys each by bytes): growing them later frees the old buffers,
+  // and hipFree / hipHostFree synchronize the device -- the call would wait for every
+  // throughput call in flight (the node leg's first 128-set priority job under load took
+  // 0.9-1.5 s, profiles/r05/node_q/)
+  if (ok && ctx->lp_max_sets) {
+    Slot& pl = ctx->slots[ctx->n_slots];
+    const size_t ns = ctx->lp_max_sets, in = ns * (32 + 192 + 16 + 16 * 96) + 65536, out = 3 * ns + 4096;
+    ok = ensure_pin(ctx, pl, in + out) == LB_OK && ensure_ws(ctx, pl, in + out + pipeline_ws_bytes(ns, ns)) == LB_OK;
+  }
   if (!ok) {
     lb_destroy(ctx);
     return LB_ERR_DEVICE;

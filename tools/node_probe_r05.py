@@ -13,22 +13,34 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    out = sys.argv[1]
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 96
-    os.makedirs(out, exist_ok=True)
+def write_data(d):
     from bench import compress_g1, make_workload
     from lodestar_amd.native import Device
     dev = Device(0)
     sks, pks, msgs, sigs = make_workload(dev, 65536, 0, hashlib.sha256(b"lodestar-mi355x-bench").digest())
     dev.close()
-    import tempfile
-    d = tempfile.mkdtemp(prefix="lb_node_probe_")  # (not under gpurun_out: ~17 MB of inputs)
     for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
         with open(os.path.join(d, name + ".bin"), "wb") as f:
             f.write(b"".join(items))
     with open(os.path.join(d, "pks_c.bin"), "wb") as f:
         f.write(b"".join(compress_g1(k) for k in pks))
+
+
+def main():
+    if sys.argv[1] == "--write-data":
+        write_data(sys.argv[2])
+        return
+    out = sys.argv[1]
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 96
+    os.makedirs(out, exist_ok=True)
+    import tempfile
+    d = tempfile.mkdtemp(prefix="lb_node_probe_")  # (not under gpurun_out: ~17 MB of inputs)
+    if os.environ.get("LB_PROBE_CHILD_DATA") == "1":
+        # the inputs from a child process: this one never opens a HIP queue (HIP may keep
+        # a process's hardware queues after its streams are destroyed)
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--write-data", d], check=True, timeout=300)
+    else:
+        write_data(d)
     env = dict(os.environ, LB_JS_TRACE="1")
     extra = os.environ.get("LB_NODE_FLAGS", "--trace-gc").split()
     r = subprocess.run(["node"] + extra + [os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)],
