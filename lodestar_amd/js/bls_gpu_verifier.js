@@ -754,6 +754,7 @@ class BlsGpuVerifier {
       return;
     }
     const backNs = hrNowNs();
+    if (priority && def.length) this.lastPriorityResult = outs[0];  // (diagnostics, as lastMainThreadResult)
     if (this.trace && def.length) {
       for (let q = this.trace.length - 1; q >= 0; q--)
         if (this.trace[q].dispatchNs === dispatchNs) {

@@ -185,6 +185,10 @@ struct Task {
   uint64_t ticket = 0;
   uint64_t t_start = 0, t_end = 0, t_submitted = 0, t_retire = 0;
   uint64_t clk[4] = {};  // latency-lane calls: lb_last_latency_clocks
+  // latency-lane calls with LB_STAGE_EVENTS=1: the call's stage times (lb_last_stage_times)
+  float stage_ms[16] = {};
+  const char* stage_names[16] = {};
+  int n_stage = 0;
   int rc = LB_OK;
   std::string errmsg;
   Task* target = nullptr;  // Finish: the two-phase call it resumes
@@ -348,7 +352,11 @@ void lane_loop(Context* c) {
     if (rc == LB_OK) {
       t->t_retire = now_ns();
       rc = lb_wait(c->lctx, t->ticket, &t->stats);
-      if (rc == LB_OK) lb_last_latency_clocks(c->lctx, t->clk);
+      if (rc == LB_OK) {
+        lb_last_latency_clocks(c->lctx, t->clk);
+        t->n_stage = lb_last_stage_times(c->lctx, t->stage_ms, t->stage_names, 16);
+        if (t->n_stage > 16) t->n_stage = 16;
+      }
     }
     if (rc != LB_OK) fail(t, rc, c->lctx);
     t->t_end = now_ns();
@@ -680,6 +688,13 @@ napi_value verify_result(napi_env env, Task* t) {
     const double rt = (double)(t->clk[2] - t->clk[0]);
     set_num(env, o, "kernelMs", rt / 1e5);
     set_num(env, o, "kernelClockMHz", (double)(t->clk[3] - t->clk[1]) / rt * 100.0);
+  }
+  if (t->n_stage > 0) {
+    napi_value st;
+    napi_create_object(env, &st);
+    for (int i = 0; i < t->n_stage; i++)
+      if (t->stage_names[i]) set_num(env, st, t->stage_names[i], t->stage_ms[i]);
+    napi_set_named_property(env, o, "stageMs", st);
   }
   return o;
 }

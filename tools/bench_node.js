@@ -248,6 +248,7 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   const load1 = [];
   const load128 = [];
   const detail1 = [];
+  const detail128 = [];
   const tLoad = ms();
   const loadJobs0 = loadDoneJobs;
   const samples = parseInt(process.env.LB_NODE_LOAD_SAMPLES || "25", 10);
@@ -268,6 +269,9 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
     t = ms();
     ok = ok && (await v.verifySignatureSets(jobs[(r + 3) % jobs.length], {priority: true})) === true;
     load128.push(ms() - t);
+    const pr = v.lastPriorityResult || {};
+    detail128.push([+load128[load128.length - 1].toFixed(2), +(((pr.workerEndNs || 0) - (pr.workerStartNs || 0)) / 1e6).toFixed(2),
+                    +(pr.deviceMs || 0).toFixed(2), +(pr.kernelMs || 0).toFixed(2), pr.stageMs || null]);
     await new Promise((res) => setTimeout(res, 10));
   }
   const loadRate = ((loadDoneJobs - loadJobs0) * 128 * 1000) / (ms() - tLoad);
@@ -332,7 +336,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
         samples: load1.length,
         ...(process.env.LB_JS_TRACE === "1"
           ? {ms_1set: load1.map((x) => +x.toFixed(2)), ms_128set: load128.map((x) => +x.toFixed(2)),
-             detail_1set_total_lane_device_kernel_ms: detail1} : {}),
+             detail_1set_total_lane_device_kernel_ms: detail1,
+             detail_128set_total_lane_device_kernel_ms_stages: detail128} : {}),
         load_packages_queued: loadPackages,
         background_sets_per_s: Math.round(loadRate),
       },
