@@ -215,6 +215,7 @@ struct lb_ctx {
   // lp_max_sets sets): they never queue behind the calls in flight
   Slot slots[kMaxSlots + 1];
   Slot& prio() { return slots[n_slots]; }
+  bool prio_kcopy = true;  // the priority slot's host copies as kernels (slot_copy, LB_PRIO_KCOPY)
   int prio_cus = 0;  // CUs the throughput slots leave to the priority lane (LB_PRIO_CUS)
   // LB_PRIO_DYN=1 (with LB_PRIO_CUS): the throughput calls take the masked streams only
   // while the priority lane has been used within the last prio_hold_ms (LB_PRIO_HOLD_MS)
@@ -420,6 +421,7 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
   } while (0)
 
 int lp_ensure(lb_ctx* ctx);
+int slot_copy(lb_ctx* ctx, Slot& sl, void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st);
 
 // The latency path (k_lp.hip) for a small call: pubkeys -> per-set inputs -> one
 // workgroup per set (set program, the request's product tree, the root's final
@@ -474,7 +476,7 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
   c.n_sets = n_sets;
   c.clk = d_clk;
   LB_STAGE("lp_verify", 0, k_lp_verify, n_sets, LB_LP_TPB, c);
-  LB_HIP(hipMemcpyAsync(sl.h_clk, d_clk, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, sl.st[0]));
+  LB_TRY(slot_copy(ctx, sl, sl.h_clk, d_clk, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, sl.st[0]));
   sl.lp_call = true;
   PipeState& ps = sl.ps;
   ps = PipeState{};
@@ -905,14 +907,30 @@ int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
   return LB_OK;
 }
 
+// A host <-> device copy of a call on slot sl: on the priority slot a kernel (k_copy_bytes,
+// LB_PRIO_KCOPY=0: hipMemcpyAsync), never queued on an SDMA engine behind the throughput
+// calls' staging; elsewhere hipMemcpyAsync.  Host buffers are pinned (hipHostMalloc).
+int slot_copy(lb_ctx* ctx, Slot& sl, void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st) {
+  if (!n) return LB_OK;
+  if (ctx->prio_kcopy && &sl == &ctx->prio() && n < (1u << 30)) {
+    const size_t blocks = (n / 16 + 255) / 256;
+    hipLaunchKernelGGL(k_copy_bytes, dim3(blocks < 1 ? 1 : blocks > 512 ? 512 : (unsigned)blocks), dim3(256), 0, st,
+                       (const uint8_t*)src, (uint8_t*)dst, (uint32_t)n);
+    LB_HIP(hipGetLastError());
+    return LB_OK;
+  }
+  LB_HIP(hipMemcpyAsync(dst, src, n, kind, st));
+  return LB_OK;
+}
+
 // Copy a host-buffer call's verdicts from the device into its pinned staging
 // (enqueued after the tails; the caller's buffers are filled in finish_slot).
 int enqueue_host_out(lb_ctx* ctx, Slot& sl) {
   if (!sl.out_valid) return LB_OK;
   const size_t a = (sl.out_nr + 255) & ~(size_t)255;
-  LB_HIP(hipMemcpyAsync(sl.h_out, sl.dv_valid, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
-  LB_HIP(hipMemcpyAsync(sl.h_out + a, sl.dv_err, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
-  if (sl.out_ns) LB_HIP(hipMemcpyAsync(sl.h_out + 2 * a, sl.dv_sst, sl.out_ns, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_TRY(slot_copy(ctx, sl, sl.h_out, sl.dv_valid, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
+  LB_TRY(slot_copy(ctx, sl, sl.h_out + a, sl.dv_err, sl.out_nr, hipMemcpyDeviceToHost, sl.st[0]));
+  if (sl.out_ns) LB_TRY(slot_copy(ctx, sl, sl.h_out + 2 * a, sl.dv_sst, sl.out_ns, hipMemcpyDeviceToHost, sl.st[0]));
   return LB_OK;
 }
 
@@ -1183,6 +1201,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = atoi(e) != 0;
   if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_PRIO_KCOPY")) ctx->prio_kcopy = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_MAX")) {
     const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
     ctx->lp_max_sets = v <= 0 ? 0u : v < (1l << LB_LP_TREE_LEVELS) ? (uint32_t)v : (1u << LB_LP_TREE_LEVELS);
@@ -1660,7 +1679,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   sl.out_sst = out_set_status;
   sl.out_nr = nr;
   sl.out_ns = out_set_status ? ns : 0;
-  LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
+  LB_TRY(slot_copy(ctx, sl, d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
   size_t o = 0;
   auto dptr = [&](size_t n) {
     char* p = d_in + o;

@@ -159,6 +159,8 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_final(uint32_t n_req, const 
 __global__ void __launch_bounds__(TPB, LB_HEAVY_WAVES) k_hash(uint32_t n, const uint8_t* __restrict__ msgs, g2a* __restrict__ out_h);
 template <class F>
 __global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __restrict__ in, jac<F>* __restrict__ out);
+__global__ void __launch_bounds__(256) k_copy_bytes(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    uint32_t n);
 __global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96);
 __global__ void k_g2_serialize(uint32_t n, const g2j* __restrict__ in, uint8_t* __restrict__ out192);
 __global__ void k_g2a_serialize(uint32_t n, const g2a* __restrict__ in, uint8_t* __restrict__ out192);

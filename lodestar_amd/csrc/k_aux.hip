@@ -27,6 +27,24 @@ __global__ void __launch_bounds__(256) k_jac_sum(uint32_t n, const jac<F>* __res
   if (threadIdx.x == 0) out[0] = sh[0].v;
 }
 
+// A priority call's host <-> device copies as a kernel: the GPU reads / writes the pinned
+// host buffer over PCIe.  hipMemcpyAsync goes to an SDMA engine, where a priority call's
+// few KB waited behind the throughput calls' megabytes of staging (40-80 ms under load,
+// profiles/r05/node_q/).  Grid-stride, 16 bytes per thread where both ends are aligned.
+__global__ void __launch_bounds__(256) k_copy_bytes(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    uint32_t n) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t done = 0;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+    const uint32_t n16 = n >> 4;
+    for (uint32_t k = i; k < n16; k += stride)
+      reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
+    done = n16 << 4;
+  }
+  for (uint32_t k = done + i; k < n; k += stride) dst[k] = src[k];
+}
+
 __global__ void k_g1_serialize(uint32_t n, const g1j* __restrict__ in, uint8_t* __restrict__ out96) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
