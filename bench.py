@@ -159,10 +159,18 @@ def main():
     ap.add_argument("--inflight", type=int,
                     default=int(os.environ.get("LB_SLOTS", min(16, max(4, int(os.environ["GPU_MAX_HW_QUEUES"]))))),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
+    ap.add_argument("--node-data", help=argparse.SUPPRESS)  # (internal: the node leg's input child)
     a = ap.parse_args()
 
+    if a.node_data:
+        node_data_main(a.node_data, a.sets)
+        return
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(launch_ranks(a))
+    # the node leg first, while this process holds no HIP queue (node_leg)
+    node_res = None
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_legs:
+        node_res = node_leg(a.sets, a.node_rounds)
 
     import torch
     import torch.distributed as dist
@@ -491,12 +499,8 @@ def main():
     legs = {}
     if world == 1 and not a.no_legs:
         legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off)
-        agg = c4_aggregates(dev, sks)
-        # the node leg runs with this process's context closed: two processes with 16 HIP
-        # hardware queues each oversubscribe the GPU's queue scheduler (the node p50s went
-        # 20 -> 39 ms with the bench's context alive)
-        dev.close()
-        legs["node"] = node_leg(pks, msgs, sigs, a.node_rounds, agg)
+        if node_res is not None:
+            legs["node"] = node_res
 
     if rank != 0:
         if world > 1:
@@ -677,28 +681,50 @@ def c4_aggregates(dev, sks, n_agg: int = 1024, k: int = 488):
     return idx, msgs, sigs
 
 
-def node_leg(pks, msgs, sigs, rounds: int = 4, agg=None):
+def write_node_inputs(d, pks, msgs, sigs, agg):
+    for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
+        with open(os.path.join(d, name + ".bin"), "wb") as f:
+            f.write(b"".join(items))
+    with open(os.path.join(d, "pks_c.bin"), "wb") as f:
+        f.write(b"".join(compress_g1(k) for k in pks))
+    agg_idx, agg_msgs, agg_sigs = agg
+    with open(os.path.join(d, "agg_idx.bin"), "wb") as f:
+        f.write(agg_idx.tobytes())
+    with open(os.path.join(d, "agg_msgs.bin"), "wb") as f:
+        f.write(b"".join(agg_msgs))
+    with open(os.path.join(d, "agg_sigs.bin"), "wb") as f:
+        f.write(b"".join(agg_sigs))
+
+
+def node_data_main(d, n_sets):
+    """--node-data DIR (a child process): the node leg's inputs -- the C2 workload of the
+    main measurement and the C4 aggregates -- written to DIR; exits, releasing its queues."""
+    from lodestar_amd.native import Device
+    dev = Device(0)
+    sks, pks, msgs, sigs = make_workload(dev, n_sets, 0, hashlib.sha256(b"lodestar-mi355x-bench").digest())
+    agg = c4_aggregates(dev, sks)
+    dev.close()
+    write_node_inputs(d, pks, msgs, sigs, agg)
+
+
+def node_leg(n_sets: int, rounds: int = 4):
     """The Lodestar path (tools/bench_node.js): BlsGpuVerifier in node -> N-API addon ->
-    lb_verify_requests_async, pubkeys by index; throughput and p50 latencies; with `agg`,
-    C4-shaped AggregateAndProof triples with keys as PublicKey objects."""
+    lb_verify_requests_async, pubkeys by index; throughput and p50 latencies; C4-shaped
+    AggregateAndProof triples with keys as PublicKey objects.  Run BEFORE this process
+    opens a HIP queue, the inputs made by a child process: HIP keeps a process's hardware
+    queues after its streams are destroyed, and the node process's queues beside another
+    process's oversubscribe the GPU's queue scheduler (priority calls under load:
+    1-set p50 1.4-2.3x idle and 128-set spikes of 100-500 ms with this process's queues
+    alive, 1.14-1.18x / 1.24-1.31x without; profiles/r05/node_q/)."""
     import shutil
     import tempfile
     if not shutil.which("node") or not os.path.exists(os.path.join(ROOT, "lodestar_amd", "napi", "lodestar_bls.node")):
         return None
     with tempfile.TemporaryDirectory() as d:
-        for name, items in (("pks", pks), ("msgs", msgs), ("sigs", sigs)):
-            with open(os.path.join(d, name + ".bin"), "wb") as f:
-                f.write(b"".join(items))
-        if agg is not None:
-            with open(os.path.join(d, "pks_c.bin"), "wb") as f:
-                f.write(b"".join(compress_g1(k) for k in pks))
-            agg_idx, agg_msgs, agg_sigs = agg
-            with open(os.path.join(d, "agg_idx.bin"), "wb") as f:
-                f.write(agg_idx.tobytes())
-            with open(os.path.join(d, "agg_msgs.bin"), "wb") as f:
-                f.write(b"".join(agg_msgs))
-            with open(os.path.join(d, "agg_sigs.bin"), "wb") as f:
-                f.write(b"".join(agg_sigs))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--node-data", d, "--sets", str(n_sets)],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": "node inputs: " + r.stderr[-500:]}
         try:
             out = subprocess.run(["node", os.path.join(ROOT, "tools", "bench_node.js"), d, str(rounds)],
                                  capture_output=True, text=True, timeout=300)
