@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 5 profiles: rocprofv3 kernel stats of the bench (every call alone: --sync, and the
+# pipelined timed region), HBM traffic PMC passes of one C2 call
+set -o pipefail
+export TMPDIR=/tmp
+D=gpurun_out/${1:-prof_r05}; mkdir -p $D
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/sync -o run --output-format csv -- \
+  python3 bench.py --sync --steps 10 --warmup 2 --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 3 \
+  > $D/sync_line.json 2> $D/sync.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/pipe -o run --output-format csv -- \
+  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 3 \
+  > $D/pipe_line.json 2> $D/pipe.err || exit 2
+tools/pmc_traffic_ab.sh $D/pmc "default:-" > $D/pmc.log 2>&1 || exit 3
+echo done

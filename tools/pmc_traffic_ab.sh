@@ -4,6 +4,7 @@
 # usage: tools/pmc_traffic_ab.sh OUTDIR "NAME:LIBRARY_PATH_OR_-" ...
 set -e
 OUT=$1; shift
+mkdir -p $OUT
 export TMPDIR=/tmp
 CMD="python3 bench.py --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 0 --steps 1 --warmup 0 --inflight 1 --sync"
 for spec in "$@"; do
