@@ -10,5 +10,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/sync -o run --output-fo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/pipe -o run --output-format csv -- \
   python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 3 \
   > $D/pipe_line.json 2> $D/pipe.err || exit 2
-tools/pmc_traffic_ab.sh $D/pmc "default:-" > $D/pmc.log 2>&1 || exit 3
+tools/pmc.sh $D/pmc > $D/pmc.log 2>&1 || exit 3
 echo done
