@@ -30,7 +30,9 @@ namespace {
 struct LpShared {
   uint32_t reg[LB_LP_MAX_REGS * 16];
   uint32_t flag[LB_LP_MAX_FLAGS];
+#ifndef LB_LP_DIRECT
   uint32_t ring[LB_LP_RING];
+#endif
 };
 static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
 static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
@@ -117,8 +119,15 @@ struct Rec {
   uint32_t base;
   LB_CO uint32_t operator[](uint32_t i) const { return ring[(base + i) & RMASK]; }
 };
+// LB_LP_DIRECT: the record straight from the program stream in global memory (L2)
+struct RecG {
+  const uint32_t* __restrict__ sp;
+  uint32_t base;
+  LB_CO uint32_t operator[](uint32_t i) const { return sp[base + i]; }
+};
 
-LB_CO uint32_t ext_form(const Rec& rec, int& o, const uint32_t* __restrict__ reg, uint32_t lane, uint32_t pj) {
+template <class R>
+LB_CO uint32_t ext_form(const R& rec, int& o, const uint32_t* __restrict__ reg, uint32_t lane, uint32_t pj) {
   const uint32_t hdr = rec[o];
   const int nt = (int)(hdr & 255u);
   const bool red = (hdr >> 8) & 1u, neg = (hdr >> 9) & 1u;
@@ -146,7 +155,8 @@ LB_CO uint32_t ext_form(const Rec& rec, int& o, const uint32_t* __restrict__ reg
   return r;
 }
 
-LB_CO void skip_form(const Rec& rec, int& o) { o += 1 + (int)(rec[o] & 255u); }
+template <class R>
+LB_CO void skip_form(const R& rec, int& o) { o += 1 + (int)(rec[o] & 255u); }
 
 // the one-operand units on a normalized value x; returns true when it wrote a flag
 LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_t lane, uint32_t pj, uint32_t& v) {
@@ -183,7 +193,8 @@ LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_
   return true;
 }
 
-LB_CO void ext_unit(const Rec& rec, LpShared& S, uint32_t lane, uint32_t pj) {
+template <class R>
+LB_CO void ext_unit(const R& rec, LpShared& S, uint32_t lane, uint32_t pj) {
   const uint32_t w0 = rec[0];
   const uint32_t op = w0 & 15u, nops = (w0 >> 4) & 7u, nfl = (w0 >> 7) & 7u, dst = w0 >> 16;
   int o = 1 + (int)nfl;
@@ -208,7 +219,7 @@ LB_CO void ext_unit(const Rec& rec, LpShared& S, uint32_t lane, uint32_t pj) {
 
 // one unit from its prefetched record; every lane of the row calls it
 LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, uint32_t pj,
-                    unsigned long long* ustamp = nullptr) {
+                    const uint32_t* __restrict__ gsp, unsigned long long* ustamp = nullptr) {
   // ustamp (diagnostic): s_memtime after the register reads / x form / y form / product
 #define LB_LP_USTAMP(k)                                                       \
   do {                                                                        \
@@ -236,7 +247,12 @@ LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, ui
     return;
   }
   if ((w0 >> 18) & 1u) {
+#ifdef LB_LP_DIRECT
+    ext_unit(RecG{gsp, cons + aux}, S, lane, pj);
+#else
+    (void)gsp;
     ext_unit(Rec{S.ring, cons + aux}, S, lane, pj);
+#endif
     return;
   }
   const uint32_t nx = (w0 >> 4) & 31u, ny = (w0 >> 9) & 31u;
@@ -294,6 +310,37 @@ struct Stream {
 // into the ring first), then the chunk this round issues -- ONE register set: with a
 // double buffer swapped at the end of the round the compiler copies the fresh loads
 // right after issuing them, which waits out a global-memory round trip every round.
+#ifdef LB_LP_DIRECT
+// LB_LP_DIRECT: no LDS ring.  The next round's header and this row's record come straight
+// from the program stream (global memory; every workgroup running the program reads the
+// same blocks, so L2), issued one round ahead like the ring's prefetch and waited for only
+// where the next round uses them; extended records are read from the stream in place.
+LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
+                    uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
+                    unsigned long long* stamps, uint32_t r) {
+  (void)pf;
+  (void)tid;
+  (void)stamps;
+  (void)r;
+  const uint32_t cons_n = st.cons + bw;
+  Desc dn;
+  uint32_t bwn = 0, nun = 0;
+  if (cons_n < st.sw) {
+    const uint4 h = *reinterpret_cast<const uint4*>(st.sp + cons_n);
+    bwn = h.x;
+    nun = h.y;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      dn.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[cons_n + 4 + RECW * row + 16u * k + lane] : 0u;
+  }
+  if (row < nu) run_unit(d, S, st.cons, lane, pj, st.sp);
+  st.cons = cons_n;
+  d = dn;
+  bw = bwn;
+  nu = nun;
+  __syncthreads();
+}
+#else
 LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
                     uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
@@ -350,7 +397,7 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   LB_LP_STAMP(3);
   if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
   if (row < nu)
-    run_unit(d, S, st.cons, lane, pj,
+    run_unit(d, S, st.cons, lane, pj, st.sp,
              stamps ? stamps + r * LB_LP_STAMPS + 6 + 2 * LB_LP_TPB / 64 + 4 * (tid >> 6) : nullptr);
   if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + LB_LP_TPB / 64 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
   LB_LP_STAMP(4);
@@ -363,6 +410,8 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   LB_LP_STAMP(5);
 #undef LB_LP_STAMP
 }
+
+#endif
 
 }  // namespace
 
@@ -402,17 +451,30 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
   pos = (pos + 3u) & ~3u;  // (the stream starts 16-byte aligned)
   st.sp = prog + pos;
   st.cons = 0;
+  Desc d;
+  uint32_t bw = 0, nu = 0;
+#ifdef LB_LP_DIRECT
+  st.done = st.issued = 0;
+  __syncthreads();
+  if (st.sw) {
+    const uint4 h = *reinterpret_cast<const uint4*>(st.sp);
+    bw = h.x;
+    nu = h.y;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      d.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[4 + RECW * row + 16u * k + lane] : 0u;
+  }
+#else
   st.done = st.issued = min(st.sw, (uint32_t)(LB_LP_RING - LB_LP_CHUNK));
   for (uint32_t i = tid; i < st.done; i += LB_LP_TPB) S.ring[i] = st.sp[i];
   __syncthreads();
-  Desc d;
-  uint32_t bw = 0, nu = 0;
   if (st.sw) {
     const uint4 h = *reinterpret_cast<const uint4*>(S.ring);
     bw = h.x;
     nu = h.y;
     load_desc(d, S.ring, 4 + RECW * row, lane);
   }
+#endif
   uint4 pf = make_uint4(0u, 0u, 0u, 0u);
   // one copy of the round in the loop (the round's code is most of the kernel's, and the
   // instruction cache is 64 KB)
