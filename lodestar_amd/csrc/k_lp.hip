@@ -9,14 +9,23 @@
 // DAG depth of its products (~1.8k rounds for hash_to_G2 + decode + Miller
 // loop) instead of the ~12k-product serial chains of the one-lane kernels
 // (DESIGN.md §7), so the fixed cost of a round is what the design minimises:
-//   * the program stream (the rounds' blocks back to back) flows through an LDS
-//     ring ~50 rounds ahead of execution (each round issues its share of the
-//     next chunk and stores the chunk issued the round before);
-//   * a unit is a fixed 20-word record loaded into registers during the
-//     PREVIOUS round, so a round starts with every register read of its forms
-//     already addressable: one LDS round trip, then arithmetic;
+//   * the program stream (the rounds' blocks back to back) is read from global
+//     memory (L2: every workgroup running a program reads the same blocks), the
+//     next round's header and records issued at the start of a round and waited
+//     for only where the next round uses them (LB_LP_RING: through an LDS ring
+//     ~50 rounds ahead instead, which costs a ring store and an LDS read a round);
+//   * a unit is a fixed 36-word record loaded into registers during the
+//     PREVIOUS round (three words per lane of its row), so a round starts with
+//     every register read of its forms already addressable: one LDS round trip,
+//     then arithmetic;
 //   * forms multiply unreduced (13-limb Montgomery: operands up to ~2^399).
 #include "bls_coop.h"
+// The program stream: read straight from global memory one round ahead (default; lone set
+// 3.14 -> 2.94 ms, 128-set request 3.48 -> 3.28 ms, profiles/r05/lp_direct/), or through
+// an LDS ring filled ~50 rounds ahead (-DLB_LP_RING, rounds 4-5)
+#ifndef LB_LP_RING
+#define LB_LP_DIRECT 1
+#endif
 #include "bls_kernels.h"
 #include "bls_lp.h"
 #include "bls_lp_progs.h"
