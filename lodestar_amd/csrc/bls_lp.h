@@ -8,6 +8,11 @@
 
 #define LB_LP_ROWS 32                     // units per round = 16-lane rows per workgroup
 #define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
+// k_lp_verify's waves per SIMD target: 2 = one workgroup per CU (152 VGPRs); 4 = two per
+// CU (128 VGPRs, 12 spilled; LDS 2 x 68 KB) -- for calls of more sets than CUs
+#ifndef LB_LP_VERIFY_WPE
+#define LB_LP_VERIFY_WPE 2
+#endif
 #define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
 #define LB_LP_MAX_FLAGS 512
 #define LB_LP_STAMPS (6 + 6 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps): 6 of
@@ -81,7 +86,7 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
                                                  const uint8_t* __restrict__ seed, uint32_t* __restrict__ in16,
                                                  uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
                                                  uint32_t* __restrict__ set_req);
-__global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c);
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCall c);
 // The throughput pipeline's merged check as a round program (one workgroup): in16 =
 // LB_MTAIL_NIN records (k_mtail_prep); mflag (check program): [0] = final_exp == 1;
 // out16 (partial program): the shard's partial, 12 records in the one-lane form.

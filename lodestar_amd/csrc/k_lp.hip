@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
   }
 }
 
-__global__ void __launch_bounds__(LB_LP_TPB) k_lp_verify(LpCall c) {
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCall c) {
   __shared__ LpShared S;
   __shared__ uint32_t sh_old, sh_bad, sh_err, s_fl[4];
   const uint32_t i = blockIdx.x, tid = threadIdx.x;

@@ -20,12 +20,16 @@ def main():
     from bench import make_workload
     from lodestar_amd.native import Device, pack_blobs
     dev = Device(0)
-    n = 128
+    # LB_LP_BENCH_SIZES: request sizes (default 1,128); calls of several 128-set requests
+    # above 128 (e.g. 1024 = 8 requests: more workgroups than one per CU for a 512 one)
+    sizes = [int(x) for x in os.environ.get("LB_LP_BENCH_SIZES", "1,128").split(",")]
+    n = max(sizes)
     sks, pks, msgs, sigs = make_workload(dev, n, 0, hashlib.sha256(b"lp-bench").digest())
     seed = hashlib.sha256(b"lp-seed").digest()
     out = {}
-    for name, k in (("1set", 1), ("128set", 128)):
-        req = np.array([0, k], np.uint32)
+    for k in sizes:
+        name = "%dset" % k
+        req = np.array(list(range(0, k, 128)) + [k] if k > 128 else [0, k], np.uint32)
         blob, offs = pack_blobs(sigs[:k])
         args = (req, np.frombuffer(b"".join(pks[:k]), np.uint8), None, np.frombuffer(b"".join(msgs[:k]), np.uint8),
                 blob, offs, seed)
