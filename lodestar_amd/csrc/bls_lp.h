@@ -8,10 +8,11 @@
 
 #define LB_LP_ROWS 32                     // units per round = 16-lane rows per workgroup
 #define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
-// k_lp_verify's waves per SIMD target: 2 = one workgroup per CU (152 VGPRs); 4 = two per
-// CU (128 VGPRs, 12 spilled; LDS 2 x 68 KB) -- for calls of more sets than CUs
+// k_lp_verify's waves per SIMD target: 4 = two workgroups per CU (128 VGPRs, 12 spilled;
+// LDS 2 x 68 KB): 512-set calls 6.9 -> 4.6 ms, 1024-set 12.4 -> 8.5 ms, 1 and 128 sets
+// unchanged (profiles/r05/lp_direct/lp_v*); 2 = one per CU (152 VGPRs)
 #ifndef LB_LP_VERIFY_WPE
-#define LB_LP_VERIFY_WPE 2
+#define LB_LP_VERIFY_WPE 4
 #endif
 #define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
 #define LB_LP_MAX_FLAGS 512

@@ -337,8 +337,13 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   if (cons_n < st.sw) {
     // (the header is wave-uniform: scalar registers, so the round's control flow is scalar)
     const uint4 h = *reinterpret_cast<const uint4*>(st.sp + cons_n);
+#ifdef LB_LP_VHDR
+    bwn = h.x;
+    nun = h.y;
+#else
     bwn = __builtin_amdgcn_readfirstlane(h.x);
     nun = __builtin_amdgcn_readfirstlane(h.y);
+#endif
 #pragma unroll
     for (int k = 0; k < 3; k++)
       dn.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[cons_n + 4 + RECW * row + 16u * k + lane] : 0u;

@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 D=gpurun_out/${1:-prof_r05}; mkdir -p $D
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/sync -o run --output-format csv -- \
+LB_DAG=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/sync -o run --output-format csv -- \
   python3 bench.py --sync --steps 10 --warmup 2 --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 3 \
   > $D/sync_line.json 2> $D/sync.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/pipe -o run --output-format csv -- \
