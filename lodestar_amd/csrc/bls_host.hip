@@ -446,18 +446,19 @@ int run_lp(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_
     ctx->err = "workspace overflow";
     return LB_ERR_OUT_OF_MEMORY;
   }
-  LB_HIP(hipMemsetAsync(d_valid, 0, n_req, sl.st[0]));
-  LB_HIP(hipMemsetAsync(d_req_err, 0, n_req, sl.st[0]));
-  if (!n_sets) return LB_OK;  // every request empty: false
-  LB_HIP(hipMemsetAsync(d_cnt, 0, (size_t)LB_LP_TREE_LEVELS * ns * sizeof(uint32_t), sl.st[0]));
-  LB_HIP(hipMemsetAsync(d_clk, 0, 4 * sizeof(unsigned long long), sl.st[0]));
+  if (!n_sets) {  // every request empty: false (otherwise k_lp_prep zeroes the outputs)
+    LB_HIP(hipMemsetAsync(d_valid, 0, n_req, sl.st[0]));
+    LB_HIP(hipMemsetAsync(d_req_err, 0, n_req, sl.st[0]));
+    return LB_OK;
+  }
   const PkSource src{d_pks, d_pk_idx, ctx->d_table, ctx->table_n};
   LB_STAGE("pubkeys", 0, k_pubkeys_single, blocks_for(n_sets), TPB, n_sets, src, d_pk_off, d_pk, d_pk_st);
   if (d_pk_off)
     LB_STAGE("pubkeys_agg", 0, k_pubkeys_agg, n_sets < 16384u ? n_sets : 16384u, TPB, n_sets, src, d_pk_off, d_pk,
              d_pk_st);
   LB_STAGE("lp_prep", 0, k_lp_prep, blocks_for(n_sets), TPB, n_sets, d_req_off, n_req, d_msgs, d_sigs, d_sig_off,
-           (const g1j*)d_pk, d_seed, d_in16, d_fl, d_sig_st, d_setreq);
+           (const g1j*)d_pk, d_seed, d_in16, d_fl, d_sig_st, d_setreq, d_valid, d_req_err, d_cnt,
+           (uint32_t)LB_LP_TREE_LEVELS * ns, d_clk);
   LpCall c;
   c.prog_single = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SET_SINGLE].off;
   c.prog_batch = ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SET_BATCH].off;

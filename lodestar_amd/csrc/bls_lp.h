@@ -86,7 +86,9 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
                                                  const uint32_t* __restrict__ sig_off, const g1j* __restrict__ pk,
                                                  const uint8_t* __restrict__ seed, uint32_t* __restrict__ in16,
                                                  uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
-                                                 uint32_t* __restrict__ set_req);
+                                                 uint32_t* __restrict__ set_req,
+                                                 uint8_t* __restrict__ valid, uint8_t* __restrict__ req_err,
+                                                 uint32_t* __restrict__ cnt, uint32_t n_cnt, unsigned long long* __restrict__ clk);
 __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCall c);
 // The throughput pipeline's merged check as a round program (one workgroup): in16 =
 // LB_MTAIL_NIN records (k_mtail_prep); mflag (check program): [0] = final_exp == 1;

@@ -520,8 +520,19 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
                                                  const uint32_t* __restrict__ sig_off, const g1j* __restrict__ pk,
                                                  const uint8_t* __restrict__ seed, uint32_t* __restrict__ in16,
                                                  uint32_t* __restrict__ flags, uint8_t* __restrict__ sig_st,
-                                                 uint32_t* __restrict__ set_req) {
+                                                 uint32_t* __restrict__ set_req, uint8_t* __restrict__ valid,
+                                                 uint8_t* __restrict__ req_err, uint32_t* __restrict__ cnt, uint32_t n_cnt,
+                                                 unsigned long long* __restrict__ clk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the call's outputs and k_lp_verify's tree counters / clock stamps start at zero (here
+  // instead of four memset launches ahead of a lone set's critical path)
+  const uint32_t gsz = gridDim.x * blockDim.x;
+  for (uint32_t j = i; j < n_req; j += gsz) {
+    valid[j] = 0;
+    req_err[j] = 0;
+  }
+  for (uint32_t j = i; j < n_cnt; j += gsz) cnt[j] = 0u;
+  if (i < 4 && clk) clk[i] = 0ull;
   if (i >= n) return;
   // request of set i (binary search over the offsets)
   uint32_t lo = 0, hi = n_req;
