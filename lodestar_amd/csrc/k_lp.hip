@@ -607,9 +607,14 @@ __global__ void __launch_bounds__(TPB) k_lp_prep(uint32_t n, const uint32_t* __r
   fl[0] = inf ? 1u : 0u;
   fl[1] = sign ? 1u : 0u;
   fl[2] = comp ? 1u : 0u;
-  uint8_t sd[32];
-  for (int k = 0; k < 32; k++) sd[k] = seed[k];
-  const uint64_t r = batch_scalar(sd, i);
+  // the batch scalar's halves (set_batch only: a 1-set request runs set_single, which
+  // reads none of them -- no SHA-256 compression on a lone set's critical path)
+  uint64_t r = 0;
+  if (req_off[lo + 1] - req_off[lo] != 1) {
+    uint8_t sd[32];
+    for (int k = 0; k < 32; k++) sd[k] = seed[k];
+    r = batch_scalar(sd, i);
+  }
   const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
   for (int k = 0; k < 32; k++) {
     fl[3 + k] = (ra >> (31 - k)) & 1u;
