@@ -335,15 +335,11 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
   Desc dn;
   uint32_t bwn = 0, nun = 0;
   if (cons_n < st.sw) {
-    // (the header is wave-uniform: scalar registers, so the round's control flow is scalar)
+    // (kept in vector registers: a readfirstlane into scalar ones waits for the load in this
+    // round, exposing its latency -- lone set 2.93-2.96 -> 3.18 ms, profiles/r05/lp_direct/r05r)
     const uint4 h = *reinterpret_cast<const uint4*>(st.sp + cons_n);
-#ifdef LB_LP_VHDR
     bwn = h.x;
     nun = h.y;
-#else
-    bwn = __builtin_amdgcn_readfirstlane(h.x);
-    nun = __builtin_amdgcn_readfirstlane(h.y);
-#endif
 #pragma unroll
     for (int k = 0; k < 3; k++)
       dn.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[cons_n + 4 + RECW * row + 16u * k + lane] : 0u;
@@ -473,8 +469,8 @@ LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_
   __syncthreads();
   if (st.sw) {
     const uint4 h = *reinterpret_cast<const uint4*>(st.sp);
-    bw = __builtin_amdgcn_readfirstlane(h.x);
-    nu = __builtin_amdgcn_readfirstlane(h.y);
+    bw = h.x;
+    nu = h.y;
 #pragma unroll
     for (int k = 0; k < 3; k++)
       d.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[4 + RECW * row + 16u * k + lane] : 0u;
