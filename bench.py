@@ -127,10 +127,23 @@ def launch_ranks(a) -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    # ranks sharing a GPU (a rehearsal on fewer GPUs than ranks): their contexts' HIP
+    # hardware queues add up on that GPU, and past what its queue scheduler maps at once it
+    # time-slices them -- 2 ranks x 20 queues on one GPU ran at 0.6-1.0 M sets/s, 2 x 12 at
+    # 3.36 M (profiles/r05/rehearsal/).  Each rank then gets a share of the 16 calls in flight.
+    qenv = {}
+    try:
+        import torch  # (device_count does not initialise the GPU on this image)
+        ndev = torch.cuda.device_count()
+    except Exception:
+        ndev = 0
+    share = -(-a.gpus // ndev) if ndev else 1
+    if share > 1 and "LB_HW_QUEUES" not in os.environ:
+        qenv["LB_HW_QUEUES"] = str(max(4, 16 // share))
     procs = []
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **qenv)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     rcs = [p.wait() for p in procs]
