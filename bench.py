@@ -231,21 +231,22 @@ def main():
     d_seed = torch.from_numpy(np.frombuffer(hashlib.sha256(b"batch-rand").digest(), np.uint8).copy()).to(cuda)
     # one output buffer per in-flight call (the library keeps one call per slot)
     nbuf = max(1, a.inflight)
-    d_valid = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
-    d_err = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
+    # (+ a quarter more: the two-phase flow keeps that many more calls outstanding)
+    d_valid = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf + nbuf // 4)]
+    d_err = [torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(nbuf + nbuf // 4)]
     torch.cuda.synchronize()
 
     def submit(k, msg_ptr=None, partial=False):
         return dev.verify_requests_device_async(n_req, n, d_reqoff.data_ptr(), d_pk.data_ptr(), None,
                                                 msg_ptr or d_msg.data_ptr(), d_sig.data_ptr(), d_sigoff.data_ptr(),
-                                                d_seed.data_ptr(), d_valid[k % nbuf].data_ptr(),
-                                                d_err[k % nbuf].data_ptr(), partial=partial)
+                                                d_seed.data_ptr(), d_valid[k % len(d_valid)].data_ptr(),
+                                                d_err[k % len(d_err)].data_ptr(), partial=partial)
 
     def step(k=0, nr=n_req, ns=n):
         # synchronous call (library slot 0: two-stream DAG, lowest latency)
         dev.verify_requests_device(nr, ns, d_reqoff.data_ptr(), d_pk.data_ptr(), None, d_msg.data_ptr(),
                                    d_sig.data_ptr(), d_sigoff.data_ptr(), d_seed.data_ptr(),
-                                   d_valid[k % nbuf].data_ptr(), d_err[k % nbuf].data_ptr())
+                                   d_valid[k % len(d_valid)].data_ptr(), d_err[k % len(d_err)].data_ptr())
 
     combined = {"checks": 0, "passed": 0, "partials_per_check": 0, "gather_ms": 0.0, "check_ms": 0.0}
 
@@ -313,7 +314,12 @@ def main():
         import queue
         import threading
         lock = threading.Lock()
-        free = threading.Semaphore(nbuf)
+        # calls outstanding: the library's slots plus a quarter more -- a two-phase call frees
+        # its slot when its partial is ready (LB_TP_RELEASE, default), so the calls waiting
+        # for the combine do not keep the GPU's slots idle (without the release a submit
+        # would wait in the library for a slot held by a call the resolver has yet to finish)
+        extra = nbuf // 4 if os.environ.get("LB_TP_RELEASE", "1") != "0" else 0
+        free = threading.Semaphore(nbuf + extra)
         todo = queue.Queue()
         failed = []
 
@@ -406,7 +412,7 @@ def main():
         elapsed = float(tt.item())
     # (only the output buffers the timed steps wrote: with fewer steps than calls in flight the
     # rest were never used)
-    used = sorted({k % nbuf for k in range(a.steps)})
+    used = sorted({k % len(d_valid) for k in range(a.steps)})
     ok = all(bool(d_valid[i].cpu().numpy().all()) for i in used) and \
         not any(bool(d_err[i].cpu().numpy().any()) for i in used)
 
