@@ -168,7 +168,10 @@ def main():
                          "(enough packages past the 16 in flight that filling and draining the pipe is small)")
     ap.add_argument("--sync", action="store_true", help="one call at a time (no overlap between steps)")
     ap.add_argument("--combine", choices=["auto", "on", "off"], default="auto",
-                    help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on for N > 1)")
+                    help="two-phase calls + host combine of the ranks' Fp12 partials (auto: on -- at N = 1 too, "
+                         "where it measured 3.61-3.63 vs 3.53 M sets/s one-phase: the slot is released at the "
+                         "partial and the final exponentiation runs beside the calls, profiles/r05/combine_ab/; "
+                         "off: every call one-phase)")
     ap.add_argument("--inflight", type=int,
                     default=int(os.environ.get("LB_SLOTS", min(16, max(4, int(os.environ["GPU_MAX_HW_QUEUES"]))))),
                     help="calls kept in flight (= library slots, env LB_SLOTS)")
@@ -209,7 +212,7 @@ def main():
     torch.cuda.set_device(gpu)
     from lodestar_amd.native import Device
     dev = Device(gpu)
-    combine = a.combine == "on" or (a.combine == "auto" and world > 1)
+    combine = a.combine == "on" or (a.combine == "auto" and not a.sync)
 
     n = a.sets
     seed = hashlib.sha256(b"lodestar-mi355x-bench").digest()
@@ -573,9 +576,12 @@ def main():
         "latency_under_load": loaded,
         "all_valid": ok,
         "overlap": "sync" if a.sync else f"{nbuf} calls in flight",
-        "combine": ({"mode": "two-phase calls; per-step all-gather of the ranks' 576-byte Fp12 partials (gloo), "
-                             "one final exponentiation on rank 0's GPU (lb_gt_check), verdict broadcast; "
-                             "the combine runs on a resolver thread beside the submit loop",
+        "combine": ({"mode": ("two-phase calls; per-step all-gather of the ranks' 576-byte Fp12 partials (gloo), "
+                              "one final exponentiation on rank 0's GPU (lb_gt_check), verdict broadcast; "
+                              "the combine runs on a resolver thread beside the submit loop") if world > 1 else
+                             ("two-phase calls (the multi-GPU flow at N = 1): each call's 576-byte Fp12 partial, "
+                              "its final exponentiation (lb_gt_check) and finish on a resolver thread beside the "
+                              "submit loop; the call's slot is released at the partial"),
                      "checks": combined["checks"], "passed": combined["passed"],
                      "partials_per_check": combined["partials_per_check"],
                      "gather_ms_avg": round(combined["gather_ms"] / max(combined["checks"], 1), 3),
