@@ -492,7 +492,7 @@ def main():
     # a highest-priority stream, lb_verify_requests_device of <= lp_max sets); every
     # iteration retires the oldest call and submits the next, so the load never drains
     loaded = None
-    if a.latency_reps > 0 and world == 1 and not combine:
+    if a.latency_reps > 0 and world == 1:  # (one-phase background calls, after the timed region)
         pend = [submit(k) for k in range(nbuf)]
         kk = nbuf
         ll1, ll128 = [], []
