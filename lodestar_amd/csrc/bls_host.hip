@@ -215,7 +215,6 @@ struct lb_ctx {
   // lp_max_sets sets): they never queue behind the calls in flight
   Slot slots[kMaxSlots + 1];
   Slot& prio() { return slots[n_slots]; }
-  bool tail_aux = false;   // LB_TAIL_AUX
   bool prio_kcopy = true;  // the priority slot's host copies as kernels (slot_copy, LB_PRIO_KCOPY)
   int prio_cus = 0;  // CUs the throughput slots leave to the priority lane (LB_PRIO_CUS)
   // LB_PRIO_DYN=1 (with LB_PRIO_CUS): the throughput calls take the masked streams only
@@ -825,11 +824,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     // LB_TAIL_PRIO=1 runs its chain of one-wave kernels on a shared high-priority
     // stream instead of the slot's own (measured slower, off by default).
     hipStream_t ts = sl.st[0];
-    // LB_TAIL_AUX=1: a one-phase call's merged-check program on the context's high-priority
-    // aux stream (lb_gt_check's; no extra hardware queue)
-    hipStream_t tail_hi = ctx->tail_stream ? ctx->tail_stream : (ctx->tail_aux && mtail && !partial) ? ctx->aux_stream : nullptr;
-    if (tail_hi) {
-      ts = tail_hi;
+    if (ctx->tail_stream) {
+      ts = ctx->tail_stream;
       LB_HIP(hipEventRecord(sl.dep[3], sl.st[0]));
       LB_HIP(hipStreamWaitEvent(ts, sl.dep[3], 0));
     }
@@ -1207,7 +1203,6 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = atoi(e) != 0;
   if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_PRIO_KCOPY")) ctx->prio_kcopy = atoi(e) != 0;
-  if (const char* e = getenv("LB_TAIL_AUX")) ctx->tail_aux = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_MAX")) {
     const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
     ctx->lp_max_sets = v <= 0 ? 0u : v < (1l << LB_LP_TREE_LEVELS) ? (uint32_t)v : (1u << LB_LP_TREE_LEVELS);
