@@ -71,7 +71,7 @@ def _unit_deps_mtime(unit: str) -> float:
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0, lib: str = LIB, obj_dir: str = OBJ_DIR,
-          extra=()) -> str:
+          extra=(), blob: str = None) -> str:
     """Compile every unit for gfx950 (in parallel, each unit only when stale) and link the .so."""
     gen_constants()
     LIB = lib  # noqa: N806
@@ -84,7 +84,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, lib: str = 
         o = os.path.join(OBJ_DIR, os.path.splitext(u)[0] + ".o")
         objs.append(o)
         if force or not os.path.exists(o) or os.path.getmtime(o) < _unit_deps_mtime(u):
-            unit_flags = [blob_define()] if u == "lp_blob.hip" else []
+            unit_flags = [(blob_define() if blob is None else '-DLB_LP_BLOB_PATH="%s"' % blob)] if u == "lp_blob.hip" else []
             todo.append([HIPCC, f"--offload-arch={ARCH}", *FLAGS, *extra, *unit_flags, "-c", "-o", o,
                          os.path.join(CSRC, u)])
     jobs = jobs or max(1, min(len(todo), os.cpu_count() or 1, 16))
@@ -108,12 +108,12 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, lib: str = 
     return LIB
 
 
-def build_variant(name: str, extra, verbose: bool = False) -> str:
+def build_variant(name: str, extra, verbose: bool = False, blob: str = None) -> str:
     """Same library with extra compile flags, under build/variants/NAME/ (select it
     at run time with LB_LIBRARY=<path>); for tuning experiments only."""
     d = os.path.join(ROOT, "build", "variants", name)
     return build(verbose=verbose, lib=os.path.join(d, "liblodestar_bls.so"), obj_dir=os.path.join(d, "obj"),
-                 extra=tuple(extra))
+                 extra=tuple(extra), blob=blob)
 
 
 def build_opcount(out_dir: str) -> str:

@@ -34,7 +34,11 @@
 
 #include "bls_kernels.h"
 #include "bls_lp.h"
+#ifdef LB_LP_PROGS_HEADER  // (a variant's programs, tools/lp_rows_variant.py)
+#include LB_LP_PROGS_HEADER
+#else
 #include "bls_lp_progs.h"
+#endif
 
 using namespace lb;
 

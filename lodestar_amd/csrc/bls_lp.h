@@ -6,7 +6,9 @@
 
 #include "bls_kernels.h"
 
+#ifndef LB_LP_ROWS
 #define LB_LP_ROWS 32                     // units per round = 16-lane rows per workgroup
+#endif
 #define LB_LP_TPB (LB_LP_ROWS * 16)       // 8 waves: 2 per SIMD (256 VGPRs for the one-lane inversion)
 // k_lp_verify's waves per SIMD target: 4 = two workgroups per CU (128 VGPRs, 12 spilled;
 // LDS 2 x 68 KB): 512-set calls 6.9 -> 4.6 ms, 1024-set 12.4 -> 8.5 ms, 1 and 128 sets

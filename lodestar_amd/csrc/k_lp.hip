@@ -28,7 +28,11 @@
 #endif
 #include "bls_kernels.h"
 #include "bls_lp.h"
+#ifdef LB_LP_PROGS_HEADER  // (a variant's programs, tools/lp_rows_variant.py)
+#include LB_LP_PROGS_HEADER
+#else
 #include "bls_lp_progs.h"
+#endif
 
 namespace lb {
 
@@ -43,11 +47,13 @@ struct LpShared {
   uint32_t ring[LB_LP_RING];
 #endif
 };
+constexpr uint32_t RMASK = LB_LP_RING - 1;
+#ifndef LB_LP_DIRECT
 static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
 static_assert(LB_LP_CHUNK % LB_LP_TPB == 0 && LB_LP_RING >= LB_LP_CHUNK + 2 * LB_LP_BLOCK_CAP, "ring sizing");
-constexpr uint32_t RMASK = LB_LP_RING - 1;
 constexpr int PFW = LB_LP_CHUNK / LB_LP_TPB;  // stream words per thread per chunk (one 16-byte load)
 static_assert(PFW == 4, "one uint4 of the stream per thread and chunk");
+#endif
 constexpr int NT = 16;                        // inline terms per operand
 constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
 constexpr int YT = 3 + NT;                    // first y term word
