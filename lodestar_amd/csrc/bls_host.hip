@@ -1258,21 +1258,6 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
       ctx->prio_cus = k;
     }
   }
-  // LB_PRIO_STATIC_CUS=K (default 0): the throughput streams themselves ("full") leave the K
-  // highest-numbered CUs to the priority lane at all times, so a priority call after a quiet
-  // spell finds a free CU at once (the onset case); every full stream is then
-  // CU-masked and takes a hardware queue of its own
-  std::vector<uint32_t> static_mask;
-  if (!cu_mask.empty()) {
-    int cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    int k = 0;
-    if (const char* e = getenv("LB_PRIO_STATIC_CUS")) k = atoi(e);
-    if (k > 0 && k < ctx->prio_cus) {
-      static_mask.assign(cu_mask.size(), 0u);
-      for (int c = 0; c < cus - k; c++) static_mask[c / 32] |= 1u << (c % 32);
-    }
-  }
   if (!cu_mask.empty()) {
     const char* dy = getenv("LB_PRIO_DYN");
     ctx->prio_dyn = !dy || atoi(dy) != 0;
@@ -1300,8 +1285,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
     const bool one = ctx->prio_dyn && ctx->prio_dyn_slots < ctx->n_slots;
     for (int s = 0; s < ctx->n_slots; s++) {
       const int spp = ctx->streams_per_slot[s];
-      if (cu_mask.empty() || (ctx->prio_dyn && static_mask.empty())) plain += spp;
-      if (!static_mask.empty() && ctx->prio_dyn) masked += spp;  // (LB_PRIO_STATIC_CUS: the full streams too)
+      if (cu_mask.empty() || ctx->prio_dyn) plain += spp;
       if (!cu_mask.empty() && s < ctx->prio_dyn_slots) masked += one ? 1 : spp;
     }
     const char* tp = getenv("LB_TAIL_PRIO");
@@ -1341,11 +1325,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
           ok = hipExtStreamCreateWithCUMask(&sl.st_mask[i], (uint32_t)cu_mask.size(), cu_mask.data()) == hipSuccess;
         else if (one && i > 0)
           sl.st_mask[i] = sl.st_mask[0];
-        if (ok && ctx->prio_dyn)
-          ok = static_mask.empty()
-                   ? hipStreamCreateWithFlags(&sl.st_full[i], hipStreamNonBlocking) == hipSuccess
-                   : hipExtStreamCreateWithCUMask(&sl.st_full[i], (uint32_t)static_mask.size(), static_mask.data()) ==
-                         hipSuccess;
+        if (ok && ctx->prio_dyn) ok = hipStreamCreateWithFlags(&sl.st_full[i], hipStreamNonBlocking) == hipSuccess;
         sl.st[i] = ctx->prio_dyn ? sl.st_full[i] : sl.st_mask[i];
       } else {
         ok = hipStreamCreateWithFlags(&sl.st[i], hipStreamNonBlocking) == hipSuccess;
