@@ -161,3 +161,45 @@ def test_golden_verdict_scenarios_match_semantics_of_3set_batch():
         pk = O.g1_from_bytes(bytes.fromhex(st["pks"][0]))
         sets.append((pk, bytes.fromhex(st["msg"]), bytes.fromhex(st["sig"])))
     assert OB.verify_signature_sets_maybe_batch(sets) == v["expect"][0]
+
+
+def test_expand_message_zpad_state_constant():
+    """bls_hash.h expand_message_xmd_32 starts from the SHA-256 state after the all-zero
+    Z_pad block (a constant): that state, completed with the padding block of a 64-byte
+    message, must give hashlib's sha256(64 zero bytes)."""
+    import hashlib
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lodestar_amd", "csrc",
+                            "bls_hash.h")).read()
+    m = re.search(r"uint32_t st\[8\] = \{([^}]*)\};", src)
+    st = [int(x.strip().rstrip("u"), 16) for x in m.group(1).split(",")]
+    K = [int(x) for x in (
+        "1116352408 1899447441 3049323471 3921009573 961987163 1508970993 2453635748 2870763221 3624381080 "
+        "310598401 607225278 1426881987 1925078388 2162078206 2614888103 3248222580 3835390401 4022224774 "
+        "264347078 604807628 770255983 1249150122 1555081692 1996064986 2554220882 2821834349 2952996808 "
+        "3210313671 3336571891 3584528711 113926993 338241895 666307205 773529912 1294757372 1396182291 "
+        "1695183700 1986661051 2177026350 2456956037 2730485921 2820302411 3259730800 3345764771 3516065817 "
+        "3600352804 4094571909 275423344 430227734 506948616 659060556 883997877 958139571 1322822218 "
+        "1537002063 1747873779 1955562222 2024104815 2227730452 2361852424 2428436474 2756734187 3204031479 "
+        "3329325298").split()]
+    M = 0xFFFFFFFF
+
+    def rotr(x, n):
+        return ((x >> n) | (x << (32 - n))) & M
+
+    def compress(state, block):
+        w = list(block) + [0] * 48
+        for i in range(16, 64):
+            s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3)
+            s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10)
+            w[i] = (w[i - 16] + s0 + w[i - 7] + s1) & M
+        a, b, c, d, e, f, g, h = state
+        for i in range(64):
+            t1 = (h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i]) & M
+            t2 = ((rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c))) & M
+            h, g, f, e, d, c, b, a = g, f, e, (d + t1) & M, c, b, a, (t1 + t2) & M
+        return [(x + y) & M for x, y in zip(state, [a, b, c, d, e, f, g, h])]
+
+    digest = compress(st, [0x80000000] + [0] * 14 + [512])
+    assert b"".join(x.to_bytes(4, "big") for x in digest) == hashlib.sha256(bytes(64)).digest()
