@@ -334,9 +334,18 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
                     uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
   (void)pf;
-  (void)tid;
-  (void)stamps;
-  (void)r;
+  // stamps (diagnostic, tools/lp_probe.py; only in a -DLB_LP_STAMPS_ON build, which keeps them
+  // out of the product's register allocation): the ring build's points 0-5 (1, 2: no ring store)
+#ifndef LB_LP_STAMPS_ON
+  stamps = nullptr;
+#endif
+#define LB_LP_STAMP(k)                                                                     \
+  do {                                                                                     \
+    if (stamps && tid == 0) stamps[r * LB_LP_STAMPS + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  LB_LP_STAMP(0);
+  LB_LP_STAMP(1);
+  LB_LP_STAMP(2);
   const uint32_t cons_n = st.cons + bw;
   Desc dn;
   uint32_t bwn = 0, nun = 0;
@@ -350,12 +359,20 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
     for (int k = 0; k < 3; k++)
       dn.v[k] = 16u * k + lane < (uint32_t)RECW ? st.sp[cons_n + 4 + RECW * row + 16u * k + lane] : 0u;
   }
-  if (row < nu) run_unit(d, S, st.cons, lane, pj, st.sp);
+  LB_LP_STAMP(3);
+  if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+  if (row < nu)
+    run_unit(d, S, st.cons, lane, pj, st.sp,
+             stamps ? stamps + r * LB_LP_STAMPS + 6 + 2 * LB_LP_TPB / 64 + 4 * (tid >> 6) : nullptr);
+  if (stamps && (tid & 63u) == 0) stamps[r * LB_LP_STAMPS + 6 + LB_LP_TPB / 64 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+  LB_LP_STAMP(4);
   st.cons = cons_n;
   d = dn;
   bw = bwn;
   nu = nun;
   __syncthreads();
+  LB_LP_STAMP(5);
+#undef LB_LP_STAMP
 }
 #else
 LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
