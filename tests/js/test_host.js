@@ -429,6 +429,26 @@ test("index2pubkey objects mirrored by syncPubkeys ship as validator indices", a
   assert.deepStrictEqual(Array.from(st.backend.lastBatch.pubkeyIndices), [4]);
 });
 
+test("mirrored key objects: index as a hidden per-verifier property; frozen keys via the map", async () => {
+  const b = new TableBackend();
+  const v = new V.BlsGpuVerifier({backends: [b], seedSource: seed});
+  const keys = Array.from({length: 6}, (_, i) => new MockPublicKey(10 + i));
+  Object.freeze(keys[2]);  // (cannot take the property: the identity map serves)
+  const before = Object.keys(keys[0]);
+  await v.syncIndex2pubkey(keys);
+  assert.deepStrictEqual(Object.keys(keys[0]), before, "the index property must not be enumerable");
+  await v.verifySignatureSets([{type: "aggregate", pubkeys: [keys[5], keys[2], keys[0]], signingRoot: new Uint8Array(32), signature: GOOD}]);
+  assert.deepStrictEqual(Array.from(b.lastBatch.pubkeyIndices), [5, 2, 0]);
+  // a second verifier (its own table) maps the same objects to its own indices
+  const b2 = new TableBackend();
+  const v2 = new V.BlsGpuVerifier({backends: [b2], seedSource: seed});
+  await v2.syncPubkeys([keys[4], keys[3]], 48);
+  await v2.verifySignatureSets([{type: "aggregate", pubkeys: [keys[3], keys[4]], signingRoot: new Uint8Array(32), signature: GOOD}]);
+  assert.deepStrictEqual(Array.from(b2.lastBatch.pubkeyIndices), [1, 0]);
+  await v.close();
+  await v2.close();
+});
+
 test("packRequestsAsync (sliced, yielding) packs exactly what packRequests packs", async () => {
   const reqs = [];
   for (let r = 0; r < 40; r++) {
