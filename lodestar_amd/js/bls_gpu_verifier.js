@@ -187,12 +187,15 @@ function* packRequestsGen(requests, seed, keyMap, slice) {
       nSets++;
     }
   }
-  const keyIx = new Int32Array(nKeys);
+  // the final index words, written here: a table index, or a flagged row of the keys shipped
+  // by their encodings (LB_PK_ROW_FLAG | LB_PK_ROW48_FLAG for a compressed one | row)
+  const keyIx = new Uint32Array(nKeys);
   const rowKeys = []; // encodings of the keys shipped as rows, in order
   let nIdx = 0;
   let nComp = 0;
   let k = 0;
   let sinceYield = 0;
+  const sym = keyMap ? keyMap.lbIndexSymbol : undefined;
   const lookKey = (pk) => {
     const ix = keyIndex(pk, keyMap);
     if (ix >= 0) {
@@ -202,14 +205,22 @@ function* packRequestsGen(requests, seed, keyMap, slice) {
     }
     const b = keyBytes(pk);
     if (b.length === 48) nComp++;
-    keyIx[k++] = -1 - rowKeys.length;
+    keyIx[k++] = (LB_PK_ROW_FLAG | (b.length === 48 ? LB_PK_ROW48_FLAG : 0) | rowKeys.length) >>> 0;
     rowKeys.push(b);
   };
   for (const req of requests) {
     for (const s of req) {
       if (s.type === "aggregate") {
         const ks = s.pubkeys || [];
-        for (let q = 0; q < ks.length; q++) lookKey(ks[q]);
+        for (let q = 0; q < ks.length; q++) {
+          // (a mirrored key object: its index as a property read, no call)
+          const pk = ks[q];
+          const ix = sym !== undefined && pk !== null && typeof pk === "object" ? pk[sym] : undefined;
+          if (ix !== undefined) {
+            keyIx[k++] = ix;
+            nIdx++;
+          } else lookKey(pk);
+        }
       } else lookKey(s.pubkey);
     }
     if ((sinceYield += req.length) >= slice) {
@@ -227,18 +238,9 @@ function* packRequestsGen(requests, seed, keyMap, slice) {
   // shipped keys (LB_PK_ROW_FLAG, LB_PK_ROW48_FLAG for a compressed row); no index and no
   // compressed key: the 96-byte encodings
   const mixed = nIdx > 0 || nComp > 0;
-  const idx = mixed ? new Uint32Array(nKeys) : null;
+  const idx = mixed ? keyIx : null;
   const rows = rowKeys.length > 0 ? new Uint8Array(96 * rowKeys.length) : null;
   for (let r = 0; r < rowKeys.length; r++) rows.set(rowKeys[r], 96 * r);
-  if (idx)
-    for (let q = 0; q < nKeys; q++) {
-      const v = keyIx[q];
-      if (v >= 0) idx[q] = v;
-      else {
-        const row = -1 - v;
-        idx[q] = (LB_PK_ROW_FLAG | (rowKeys[row].length === 48 ? LB_PK_ROW48_FLAG : 0) | row) >>> 0;
-      }
-    }
   let i = 0;
   let so = 0;
   k = 0;
