@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 5 final: the whole GPU suite, smoke, JS host GPU tests, the driver's bench line
+set -o pipefail
+D=gpurun_out/${1:-r05ab}; mkdir -p $D
+timeout -k 10 450 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/gpu_tests.txt 2>&1 || exit 1
+timeout -k 10 60 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.txt 2>&1 || exit 2
+timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench_20.json 2> $D/bench_20.err || exit 3
