@@ -270,8 +270,12 @@ struct lb_ctx {
   // B/lane: 18.3 GB of traffic per launch, 13.9x the algorithmic bytes; now 2.6 GB, 2.0x), the
   // pipeline 3.55-3.62 vs 3.54-3.57 M sets/s, three interleaved runs each
   // (profiles/r04/step_ab/).  Round 3 had measured 2/2 ahead of 2/1 (profiles/ab_r03/ab_r03s).
-  int step_mode = 1;
-  int step_waves = 1;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
+  // Round 5, in the final pipeline (merged-check program, two-phase flow): one line at a time
+  // at 2 waves/SIMD again ahead -- 3.61-3.67 M (mean 3.650 over 5 runs) against the LDS build's
+  // 3.53-3.61 M (mean 3.569), although alone it takes 5.6-5.7 ms against 4.4-4.5
+  // (profiles/r05/knobs/): its second wave per SIMD overlaps the other calls' kernels
+  int step_mode = 2;
+  int step_waves = 2;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
   // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
   // submission; the N-API addon sets it, lb_last_stage_times is then empty)
   bool stage_events = true;
