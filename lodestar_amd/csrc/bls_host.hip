@@ -271,11 +271,14 @@ struct lb_ctx {
   // pipeline 3.55-3.62 vs 3.54-3.57 M sets/s, three interleaved runs each
   // (profiles/r04/step_ab/).  Round 3 had measured 2/2 ahead of 2/1 (profiles/ab_r03/ab_r03s).
   // Round 5, in the final pipeline (merged-check program, two-phase flow): one line at a time
-  // at 2 waves/SIMD again ahead -- 3.61-3.67 M (mean 3.650 over 5 runs) against the LDS build's
-  // 3.53-3.61 M (mean 3.569), although alone it takes 5.6-5.7 ms against 4.4-4.5
-  // (profiles/r05/knobs/): its second wave per SIMD overlaps the other calls' kernels
-  int step_mode = 2;
-  int step_waves = 2;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
+  // at 2 waves/SIMD (LB_STEP_MODE=2 LB_STEP_WAVES=2) measured ahead -- 3.61-3.67 M (mean 3.650
+  // over 5 runs) against the LDS build's 3.53-3.61 M (mean 3.569) -- but alone it takes 5.7 ms
+  // against 4.4-4.5 and moves 18.4 GB per launch (13.9x its algorithmic bytes: spills) against
+  // 2.6 GB (profiles/r05/knobs/, final/pmc_traffic_r05s3.json); the LDS build stays the default
+  // until a 2-wave build without the spills exists (half the accumulator in LDS: 18 KB a
+  // workgroup, 8 per CU)
+  int step_mode = 1;
+  int step_waves = 1;  // LB_STEP_WAVES: occupancy target of k_step_acc (1 or 2)
   // LB_STAGE_EVENTS=0: no per-stage timing events (two HIP calls per kernel of the
   // submission; the N-API addon sets it, lb_last_stage_times is then empty)
   bool stage_events = true;
