@@ -25,6 +25,8 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 // v_mad_u64_u32 at ~60% of the SIMD's rate); the per-request tails (one lane
 // per request, a long serial chain) and the Miller accumulation keep the
 // spill-free 1-wave budget.
+// Re-measured in round 5 (profiles/r05/occupancy/): hash_finish / decode at 1 wave cost
+// the pipeline 6-7 % (co-residency with other calls' kernels), at 3 waves 0.3-2.5 %.
 #ifndef LB_W_HASH
 #define LB_W_HASH 2
 #endif
