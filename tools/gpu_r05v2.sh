@@ -1,0 +1,8 @@
+#!/bin/bash
+# round 5 end: the committed tree's GPU suite, smoke and the driver's bench line
+set -o pipefail
+D=gpurun_out/${1:-r05s5}; mkdir -p $D
+timeout -k 10 450 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $D/gpu_tests.txt 2>&1 || exit 1
+timeout -k 10 60 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.txt 2>&1 || exit 2
+timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench_20.json 2> $D/bench_20.err || exit 3
+echo done
