@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the secondary legs (host API, same-message, ...)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the C3 / C4 shard / C5 / perf-suite size legs (config_legs)")
     ap.add_argument("--node-rounds", type=int, default=96,
                     help="node leg: rounds of 512 x 128-set jobs (one 65,536-set package each) queued at once "
                          "(enough packages past the 16 in flight that filling and draining the pipe is small)")
@@ -186,6 +188,7 @@ def main():
     # the node leg first, while this process holds no HIP queue (node_leg)
     node_res = None
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_legs:
+        _progress("node leg")
         node_res = node_leg(a.sets, a.node_rounds)
 
     import torch
@@ -298,6 +301,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    _progress("timed region")
     t0 = time.perf_counter()
     stage_acc = {}
     n_acc = [0]
@@ -493,10 +497,13 @@ def main():
     # iteration retires the oldest call and submits the next, so the load never drains
     loaded = None
     if a.latency_reps > 0 and world == 1:  # (one-phase background calls, after the timed region)
+        # (the window opens before the first background call is submitted and closes when the
+        # last retires: every one of the kk calls ran inside it, and all kk are counted --
+        # the window used to open after nbuf calls were already in flight)
+        t_load = time.perf_counter()
         pend = [submit(k) for k in range(nbuf)]
         kk = nbuf
         ll1, ll128 = [], []
-        t_load = time.perf_counter()
         for r in range(2 * a.latency_reps):
             t1 = time.perf_counter()
             if r % 2:
@@ -513,14 +520,20 @@ def main():
         el_load = time.perf_counter() - t_load
         loaded = {"p50_ms_1set": round(float(np.median(ll1)), 3),
                   "p50_ms_128set_batch": round(float(np.median(ll128)), 3),
-                  "calls_in_flight": nbuf, "background_sets_per_s": round(n * (kk - nbuf) / el_load, 1),
+                  "calls_in_flight": nbuf, "background_sets_per_s": round(n * kk / el_load, 1),
+                  "background_calls": kk, "window_s": round(el_load, 3),
                   "ratio_1set_vs_idle": round(float(np.median(ll1)) / p50_1, 2) if p50_1 else None,
                   "ratio_128set_vs_idle": round(float(np.median(ll128)) / p50, 2) if p50 else None,
                   "lane": "priority slot (highest-priority stream) + latency path"}
 
     legs = {}
     if world == 1 and not a.no_legs:
-        legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off)
+        _progress("secondary legs")
+        legs = secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off,
+                              (d_reqoff.data_ptr(), d_pk.data_ptr(), d_sig.data_ptr(), d_sigoff.data_ptr(),
+                               d_seed.data_ptr()))
+        if not a.no_configs:
+            legs.update(config_legs(a, dev, torch, cuda, sks, pks, msgs, sigs, nbuf))
         if node_res is not None:
             legs["node"] = node_res
 
@@ -535,6 +548,7 @@ def main():
     cpu = None
     c1 = None
     if not a.no_cpu_baseline and world == 1:
+        _progress("cpu baseline")
         # the box's CPU share is 16 threads per GPU (os.cpu_count() shows the whole host)
         threads = max(1, min(16, os.cpu_count() or 1))
         rate, done, el, variant = cpu_baseline_c(pks, msgs, sigs, a.cpu_seconds, threads, a.per_request)
@@ -760,7 +774,7 @@ def node_leg(n_sets: int, rounds: int = 4):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off):
+def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n_req, req_off, sig_off, dev_ptrs):
     legs = {}
     reps = max(4, a.steps // 2)
     # (1) host-buffer API (what BlsGpuVerifier calls): numpy inputs, pinned staging, PCIe both ways
@@ -819,6 +833,63 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
     legs["adversarial"] = {"sets_per_s": round(n * reps / el, 1), "calls": reps,
                            "case": "one wrong-message set per 65,536-set call: merged check fails, 512 per-request "
                                    "tails (worker.ts:74-85 retry)"}
+    # (2b) the same through the two-phase flow (what bench.py times and the multi-GPU path runs):
+    # the combined check fails for every call.  LB_TP_RELEASE=1 (default) re-verifies the
+    # shard as a one-phase call; LB_TP_RELEASE=0 keeps the slot and runs only the per-request
+    # tails on the products already computed (the cost of the release's re-run)
+    from lodestar_amd.native import Device
+
+    def two_phase_bad(d):
+        def one(k):
+            tk = d.verify_requests_device_async(n_req, n, d_reqoff_, d_pk_, None, d_bad.data_ptr(), d_sig_, d_sigoff_,
+                                                d_seed_, d_valid_[k % len(d_valid_)], d_err_[k % len(d_err_)],
+                                                partial=True)
+            return tk
+
+        def resolve(tk):
+            ok_ = d.gt_check([d.partial_wait_t(tk)])
+            assert not ok_
+            d.finish_t(tk, ok_)
+            d.wait(tk)
+        resolve(one(0))
+        t1_ = time.perf_counter()
+        pend_ = []
+        for k in range(reps):
+            pend_.append(one(k))
+            if len(pend_) >= nbuf:
+                resolve(pend_.pop(0))
+        for tk in pend_:
+            resolve(tk)
+        torch.cuda.synchronize()
+        return n * reps / (time.perf_counter() - t1_)
+    d_reqoff_, d_pk_, d_sig_, d_sigoff_, d_seed_ = dev_ptrs
+    keep_ =[torch.zeros(n_req, dtype=torch.uint8, device=cuda) for _ in range(2 * nbuf)]
+    d_valid_ = [x.data_ptr() for x in keep_[:nbuf]]
+    d_err_ = [x.data_ptr() for x in keep_[nbuf:]]
+    rel = two_phase_bad(dev)
+    bad_row = (n // 2) // a.per_request
+    got = keep_[0].cpu().numpy()
+    assert not got[bad_row] and got.sum() == n_req - 1, "two-phase adversarial verdicts"
+    saved = {k: os.environ.get(k) for k in ("LB_TP_RELEASE", "LB_PRIO_CUS")}
+    os.environ["LB_TP_RELEASE"] = "0"
+    os.environ["LB_PRIO_CUS"] = "0"
+    try:
+        legacy_dev = Device(dev.device)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        legacy = two_phase_bad(legacy_dev)
+    finally:
+        legacy_dev.close()
+    legs["adversarial_two_phase"] = {
+        "sets_per_s_release": round(rel, 1), "sets_per_s_legacy": round(legacy, 1), "calls": reps,
+        "case": "one wrong-message set per 65,536-set two-phase call: the combined check fails every time; "
+                "release (LB_TP_RELEASE=1, default): the shard re-verified as a one-phase call; legacy "
+                "(LB_TP_RELEASE=0, its own context): the slot held, only the per-request tails run"}
     # (3) same-message gossip jobs: 512 attestation-data groups x 128 validators per call, pubkeys by index
     from lodestar_amd.native import Device  # noqa: F401
     n_jobs, per_job = 512, 128
@@ -865,6 +936,284 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
                                      "api": f"lb_verify_same_message_batch_async, {nbuf} packages in flight "
                                             "(host buffers, validator indices)"}
     return legs
+
+
+def _progress(msg):
+    """A line on stderr per leg (a long run shows it is alive; stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _p50(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t1) * 1e3)
+    return float(np.median(ts))
+
+
+def _config_roof(oc_w, key, sets_per_s, keys_per_set):
+    """A config's whole-pipeline fraction of the mad peak: its own measured mads per set
+    (tools/opcount.py --workload, profiles/op_counts_workloads.json) x sets/s."""
+    c = (oc_w or {}).get(key)
+    if not c:
+        return None
+    tot = c["mads_per_set_total"]
+    return {"bound": "valu", "unit": "Tmad/s", "mads_per_set": round(tot), "keys_per_set": round(keys_per_set, 2),
+            "achieved": round(sets_per_s * tot / 1e12, 4), "peak": round(PEAK_MAD_PER_S / 1e12, 3),
+            "frac": round(sets_per_s * tot / PEAK_MAD_PER_S, 5),
+            "counts": "profiles/op_counts_workloads.json[%s] (counting build, this config's shape)" % key}
+
+
+def config_legs(a, dev, torch, cuda, sks, pks, msgs, sigs, nbuf):
+    """Every other BASELINE.json config and the reference's perf-suite sizes
+    (BNT/perf/bls/bls.test.ts:56-122), timed after the C2 measurement (reported, never
+    `value`):
+      c3       2048-key committee aggregation (PublicKey.aggregate, chain/bls/utils.ts:13) and
+               the 512-key sync-committee aggregate verify (one 1-set request);
+      c4_shard one GPU's 1/8 of the 1 M mixed gossip sets (125,000 sets: 112,712 attestations +
+               4,096 AggregateAndProof triples with 488-key aggregates, 977 requests of 128),
+               pubkeys by validator index, device-resident inputs, `nbuf` calls in flight; plus
+               the node leg's C4 package shape (220 x 128 singles + 1,024 triples) through the
+               Python host, the GPU-bound ceiling of node's c4_public_key_objects leg;
+      c5       the 32-block epoch of block import (147 sets per block: proposer, RANDAO, 128
+               aggregates of 488 keys, the 512-key sync aggregate, 16 exits; one request per
+               block, verifyBlocksSignatures.ts:38-55) with invalid sets injected at 1e-3 --
+               the blocks holding one are false, every other block true;
+      sizes    verifyMultipleSignatures {3, 8, 32, 64, 128} (one request), same-message
+               {3, ..., 128} (one job), aggregatePubkeys {32, 128}, deserializing 10k / 100k
+               signatures with validation."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import workloads as W
+    from lodestar_amd.native import pack_blobs
+    out = {}
+    reps = max(5, a.latency_reps)
+    nv = len(pks)
+    seed = hashlib.sha256(b"batch-rand").digest()
+    oc_w = None
+    p = os.path.join(ROOT, "profiles", "op_counts_workloads.json")
+    if os.path.exists(p):
+        oc_w = json.load(open(p))
+    # validator i's key at table index i (the secondary legs appended the C2 keys to a fresh table)
+    if dev.pubkey_table_size() == 0:
+        dev.pubkey_table_append(pks)
+    assert dev.pubkey_table_read(0, 1)[0] == pks[0] and dev.pubkey_table_size() >= nv
+    keys = W.Keys([int.from_bytes(s, "big") for s in sks], list(pks))
+    rng = np.random.default_rng(5)
+
+    _progress("config legs: C3")
+    # ---- C3 ------------------------------------------------------------------------------
+    t_gen = time.time()
+    com = rng.choice(nv, 2048, replace=False).astype(np.uint32)
+    com_b = [pks[int(i)] for i in com]
+    agg = dev.aggregate_pubkeys(com_b)
+    assert agg == dev.aggregate_pubkeys_indexed(com)
+    sync = rng.choice(nv, 512, replace=False).astype(np.uint32)
+    root = hashlib.sha256(b"sync-committee-c3").digest()
+    sync_sig = W.sign_many(dev, [sum(keys.sks[int(i)] for i in sync) % R_ORDER], [root])[0]
+    blob1, offs1 = pack_blobs([sync_sig])
+    req1, pko1 = np.array([0, 1], np.uint32), np.array([0, 512], np.uint32)
+    mg1 = np.frombuffer(root, np.uint8)
+
+    def sync_verify():
+        r = dev.verify_requests(req1, None, pko1, mg1, blob1, offs1, seed, pk_indices=sync)
+        assert bool(r.valid[0]) and not r.errors.any()
+    sync_verify()
+    sync_verify_b = np.frombuffer(b"".join(pks[int(i)] for i in sync), np.uint8)
+
+    def sync_verify_bytes():
+        r = dev.verify_requests(req1, sync_verify_b, pko1, mg1, blob1, offs1, seed)
+        assert bool(r.valid[0])
+    sync_verify_bytes()
+    out["c3"] = {"config": "C3: 2048-key committee aggregation + 512-key sync-committee aggregate verify",
+                 "aggregate_2048_bytes_p50_ms": round(_p50(lambda: dev.aggregate_pubkeys(com_b), reps), 3),
+                 "aggregate_2048_indexed_p50_ms": round(_p50(lambda: dev.aggregate_pubkeys_indexed(com), reps), 3),
+                 "sync_aggregate_512_verify_indexed_p50_ms": round(_p50(sync_verify, reps), 3),
+                 "sync_aggregate_512_verify_bytes_p50_ms": round(_p50(sync_verify_bytes, reps), 3),
+                 "sync_verify_stage_ms": {k: round(v, 3) for k, v in dev.last_stage_times()},
+                 "api": "lb_aggregate_pubkeys[_indexed]; lb_verify_requests (host buffers, one 1-set request of "
+                        "512 keys: the latency path)",
+                 "datagen_s": round(time.time() - t_gen, 2)}
+
+    _progress("config legs: C4 shard")
+    # ---- C4: one GPU's shard ---------------------------------------------------------------
+    t_gen = time.time()
+    c4 = W.c4_shard(dev, keys)
+    gen_c4 = time.time() - t_gen
+    blob4, offs4 = c4.blobs()
+    mg4 = c4.msg_array()
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).copy()).to(cuda)  # noqa: E731
+    d_req, d_pko, d_idx = t(c4.req_off.view(np.int32)), t(c4.pk_off.view(np.int32)), t(c4.idx.view(np.int32))
+    d_msg, d_sig, d_sigo, d_seed = t(mg4), t(blob4), t(offs4.view(np.int32)), t(np.frombuffer(seed, np.uint8))
+    nr4, ns4 = c4.n_req, c4.n_sets
+    outs = [(torch.zeros(nr4, dtype=torch.uint8, device=cuda), torch.zeros(nr4, dtype=torch.uint8, device=cuda))
+            for _ in range(nbuf)]
+    torch.cuda.synchronize()
+
+    def submit4(k):
+        v, e = outs[k % nbuf]
+        return dev.verify_requests_device_async(nr4, ns4, d_req.data_ptr(), 0, d_pko.data_ptr(), d_msg.data_ptr(),
+                                                d_sig.data_ptr(), d_sigo.data_ptr(), d_seed.data_ptr(), v.data_ptr(),
+                                                e.data_ptr(), d_pk_idx=d_idx.data_ptr())
+    for tk in [submit4(k) for k in range(nbuf)]:  # every slot's workspace sized for the shard
+        dev.wait(tk)
+    calls4 = max(nbuf, 2 * a.steps // 3)
+    t1 = time.perf_counter()
+    pend = []
+    for k in range(calls4):
+        pend.append(submit4(k))
+        if len(pend) >= nbuf:
+            dev.wait(pend.pop(0))
+    for tk in pend:
+        dev.wait(tk)
+    torch.cuda.synchronize()
+    el4 = time.perf_counter() - t1
+    ok4 = all(bool(v.cpu().numpy().all()) and not bool(e.cpu().numpy().any()) for v, e in outs)
+    lone4 = _p50(lambda: dev.verify_requests_device(nr4, ns4, d_req.data_ptr(), 0, d_pko.data_ptr(), d_msg.data_ptr(),
+                                                    d_sig.data_ptr(), d_sigo.data_ptr(), d_seed.data_ptr(),
+                                                    outs[0][0].data_ptr(), outs[0][1].data_ptr(),
+                                                    d_pk_idx=d_idx.data_ptr()), 3)
+    st4 = {k: round(v, 3) for k, v in dev.last_stage_times()}
+    host4 = _p50(lambda: dev.verify_requests(c4.req_off, None, c4.pk_off, mg4, blob4, offs4, seed, pk_indices=c4.idx),
+                 3)
+    rate4 = ns4 * calls4 / el4
+    kps4 = len(c4.idx) / ns4
+    # the node leg's C4 package shape through the Python host (bench_node.js c4Leg): 220 jobs of
+    # 128 single sets + 1,024 (selection proof, aggregator signature, 488-key aggregate) triples
+    n_agg = 1024
+    trip = [int(q) for q in np.nonzero(np.diff(c4.pk_off) > 1)[0][:n_agg]]
+    singles = [int(q) for q in np.nonzero(np.diff(c4.pk_off) == 1)[0][:220 * 128 + 2 * n_agg]]
+    sel = singles[:220 * 128]
+    rest = singles[220 * 128:]
+    order = sel + [q for a_ in range(n_agg) for q in (rest[2 * a_], rest[2 * a_ + 1], trip[a_])]
+    req_n = np.array([0] + [128 * (j + 1) for j in range(220)] + [220 * 128 + 3 * (a_ + 1) for a_ in range(n_agg)],
+                     np.uint32)
+    pk_n = np.zeros(len(order) + 1, np.uint32)
+    pk_n[1:] = np.cumsum([int(c4.pk_off[q + 1] - c4.pk_off[q]) for q in order])
+    idx_n = np.concatenate([c4.idx[c4.pk_off[q]:c4.pk_off[q + 1]] for q in order]).astype(np.uint32)
+    mg_n = np.frombuffer(b"".join(c4.msgs[q] for q in order), np.uint8)
+    blob_n, offs_n = pack_blobs([c4.sigs[q] for q in order])
+    pcs = [dev.verify_requests_async(req_n, None, pk_n, mg_n, blob_n, offs_n, seed, pk_indices=idx_n)
+           for _ in range(nbuf)]
+    assert all(bool(dev.wait_call(pc).valid.all()) for pc in pcs)
+    t1 = time.perf_counter()
+    pend, okn, calls_n = [], True, 2 * nbuf
+    for _ in range(calls_n):
+        pend.append(dev.verify_requests_async(req_n, None, pk_n, mg_n, blob_n, offs_n, seed, pk_indices=idx_n))
+        if len(pend) >= nbuf:
+            okn &= bool(dev.wait_call(pend.pop(0)).valid.all())
+    for pc in pend:
+        okn &= bool(dev.wait_call(pc).valid.all())
+    el_n = time.perf_counter() - t1
+    out["c4_shard"] = {
+        "config": "C4: one GPU's 1/8 of 1M mixed gossip sets (BASELINE.json configs[3])",
+        "sets": ns4, "requests": nr4, "pubkeys": int(len(c4.idx)), "keys_per_set": round(kps4, 2),
+        "sets_per_s": round(rate4, 1), "ms_per_call": round(el4 / calls4 * 1e3, 3), "calls": calls4,
+        "all_valid": ok4, "lone_call_ms": round(lone4, 3), "lone_call_stage_ms": st4,
+        "host_indexed_call_ms": round(host4, 3), "host_indexed_sets_per_s": round(ns4 / host4 * 1e3, 1),
+        "api": f"lb_verify_requests_device_async, validator indices, device-resident inputs, {nbuf} calls in flight",
+        "roofline": _config_roof(oc_w, "c4_shard", rate4, kps4),
+        "node_package_shape_python_host": {
+            "sets_per_call": len(order), "requests": len(req_n) - 1, "calls": calls_n,
+            "sets_per_s": round(len(order) * calls_n / el_n, 1), "all_valid": okn,
+            "api": f"lb_verify_requests_async, host buffers, validator indices, {nbuf} calls in flight: the "
+                   "package node's c4_public_key_objects leg sends, without JS"},
+        "datagen_s": round(gen_c4, 2)}
+    del d_req, d_pko, d_idx, d_msg, d_sig, d_sigo, outs
+
+    _progress("config legs: C5 epoch")
+    # ---- C5: block import, one 32-block epoch ----------------------------------------------
+    t_gen = time.time()
+    c5 = W.c5_epoch(dev, keys)
+    gen_c5 = time.time() - t_gen
+    blob5, offs5 = c5.blobs()
+    mg5 = c5.msg_array()
+    want = [k not in c5.expect_invalid_requests for k in range(c5.n_req)]
+
+    def c5_host():
+        r = dev.verify_requests(c5.req_off, None, c5.pk_off, mg5, blob5, offs5, seed, pk_indices=c5.idx)
+        assert [bool(v) for v in r.valid] == want, "C5 block verdicts"
+        return r
+    r5 = c5_host()
+    host5 = _p50(c5_host, reps)
+    st5_host = {k: round(v, 3) for k, v in dev.last_stage_times()}
+    d5 = [t(c5.req_off.view(np.int32)), t(c5.pk_off.view(np.int32)), t(c5.idx.view(np.int32)), t(mg5), t(blob5),
+          t(offs5.view(np.int32)), t(np.frombuffer(seed, np.uint8))]
+    v5 = torch.zeros(c5.n_req, dtype=torch.uint8, device=cuda)
+    e5 = torch.zeros(c5.n_req, dtype=torch.uint8, device=cuda)
+    torch.cuda.synchronize()
+
+    def c5_dev():
+        return dev.verify_requests_device(c5.n_req, c5.n_sets, d5[0].data_ptr(), 0, d5[1].data_ptr(), d5[3].data_ptr(),
+                                          d5[4].data_ptr(), d5[5].data_ptr(), d5[6].data_ptr(), v5.data_ptr(),
+                                          e5.data_ptr(), d_pk_idx=d5[2].data_ptr())
+    c5_dev()
+    dev5 = _p50(c5_dev, reps)
+    st5 = {k: round(v, 3) for k, v in dev.last_stage_times()}
+    assert [bool(v) for v in v5.cpu().numpy()] == want, "C5 block verdicts (device inputs)"
+    kps5 = len(c5.idx) / c5.n_sets
+    out["c5"] = {
+        "config": "C5: block import, 32-block epoch, 147 sets per block, invalid sets injected at 1e-3",
+        "blocks": c5.n_req, "sets": c5.n_sets, "pubkeys": int(len(c5.idx)), "keys_per_set": round(kps5, 2),
+        "invalid_blocks": sorted(c5.expect_invalid_requests), "verdicts_match": True,
+        "batch_retries": r5.batch_retries,
+        "epoch_ms_p50_device_inputs": round(dev5, 3), "sets_per_s": round(c5.n_sets / dev5 * 1e3, 1),
+        "epoch_ms_p50_host_indexed": round(host5, 3),
+        "stage_ms": st5, "stage_ms_host": st5_host,
+        "roofline": _config_roof(oc_w, "c5", c5.n_sets / dev5 * 1e3, kps5),
+        "api": "lb_verify_requests_device (one synchronous call per epoch, validator indices, inputs in HBM) and "
+               "lb_verify_requests (host buffers)",
+        "datagen_s": round(gen_c5, 2)}
+    # the same epoch before the injection: every block valid, no per-request failure path
+    b5v, o5v = pack_blobs(c5.clean_sigs)
+    m5v = np.frombuffer(b"".join(c5.clean_msgs), np.uint8)
+
+    def c5_valid():
+        r = dev.verify_requests(c5.req_off, None, c5.pk_off, m5v, b5v, o5v, seed, pk_indices=c5.idx)
+        assert r.valid.all()
+    c5_valid()
+    out["c5"]["all_valid_epoch_ms_p50_host_indexed"] = round(_p50(c5_valid, reps), 3)
+    out["c5"]["all_valid_stage_ms_host"] = {k: round(v, 3) for k, v in dev.last_stage_times()}
+    del d5, v5, e5
+
+    _progress("config legs: perf-suite sizes")
+    # ---- the reference's perf-suite sizes (bls.test.ts:56-122) ------------------------------
+    sizes = {}
+    lat1 = []
+    for nset in (1, 3, 8, 32, 64, 128):
+        ro = np.array([0, nset], np.uint32)
+        pk_h = np.frombuffer(b"".join(pks[:nset]), np.uint8)
+        mg_h = np.frombuffer(b"".join(msgs[:nset]), np.uint8)
+        bl, of = pack_blobs(sigs[:nset])
+
+        def one():
+            r = dev.verify_requests(ro, pk_h, None, mg_h, bl, of, seed)
+            assert bool(r.valid[0])
+        one()
+        ms = _p50(one, reps)
+        key = "verify_1" if nset == 1 else f"verifyMultipleSignatures_{nset}"
+        sizes[key] = {"p50_ms": round(ms, 3), "sets_per_s": round(nset / ms * 1e3, 1)}
+    root_sm = hashlib.sha256(b"same-message-perf").digest()
+    sm_sigs = W.sign_many(dev, keys.sks[:128], [root_sm] * 128)
+    for nset in (3, 8, 32, 64, 128):
+        def sm():
+            v, fast = dev.verify_same_message(pks[:nset], sm_sigs[:nset], root_sm, seed)
+            assert all(v) and fast
+        sm()
+        ms = _p50(sm, reps)
+        sizes[f"sameMessage_{nset}"] = {"p50_ms": round(ms, 3), "sets_per_s": round(nset / ms * 1e3, 1)}
+    for nk in (32, 128):
+        ks = pks[:nk]
+        sizes[f"aggregatePubkeys_{nk}"] = {"p50_ms": round(_p50(lambda: dev.aggregate_pubkeys(ks), reps), 3)}
+    for nsig in (10_000, 100_000):
+        bl, of = pack_blobs([sigs[i % 256] for i in range(nsig)])  # (getSet(i % 256), bls.test.ts:82)
+        buf = np.zeros(nsig * 192, np.uint8)
+        assert not dev.decode_signatures_packed(bl, of, buf).any()
+        ms = _p50(lambda: dev.decode_signatures_packed(bl, of, buf), reps)
+        sizes[f"deserializing_{nsig}"] = {"p50_ms": round(ms, 3), "signatures_per_s": round(nsig / ms * 1e3, 1)}
+    out["sizes"] = {"suite": "BNT/perf/bls/bls.test.ts:56-122 shapes (one call each, host buffers, synchronous; "
+                             "1..128-set calls take the latency path)", **sizes}
+    return out
 
 
 if __name__ == "__main__":

@@ -47,7 +47,8 @@ extern "C" {
 #define LB_ERR_DEVICE (-2)           /* HIP runtime failure (maps to Promise rejection, index.ts:503-512) */
 #define LB_ERR_NO_DEVICE (-3)        /* no GPU / bad ordinal                      */
 #define LB_ERR_OUT_OF_MEMORY (-4)
-#define LB_ERR_RESOURCES (-5)        /* lb_create: more hardware queues than the scratch reservation allows */
+#define LB_ERR_RESOURCES (-5)        /* lb_create: more hardware queues than the scratch reservation allows;
+                                        lb_verify_requests_partial_async: 256 unfinished two-phase calls */
 
 /* ---- per-request error codes (lb_verify_requests out_request_error) ----- */
 #define LB_REQ_OK 0
@@ -266,6 +267,24 @@ int lb_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_done);
  * A partial is 12 big-endian canonical Fp coefficients (c0.c0.c0 ... c1.c2.c1,
  * the lb_pairing order); an empty shard's partial is 1.  A two-phase call that
  * is waited for without lb_verify_requests_finish resumes with merged_ok = 0.
+ *
+ * Contract of the default flow (LB_TP_RELEASE=1: the call frees its slot once its
+ * partial is out, instead of holding it through the host's combine):
+ *   - the outputs are PROVISIONAL until lb_wait(ticket) returns LB_OK: the released
+ *     call writes "valid" for every request not already false before the combined
+ *     check has run (into device outputs at once, into host outputs when it
+ *     retires).  Only lb_wait's return makes them verdicts;
+ *   - every input buffer (host or device) must stay valid and unchanged until
+ *     lb_wait returns: a failed combined check (merged_ok = 0) re-verifies the shard
+ *     from the caller's buffers as a one-phase call into the same outputs;
+ *   - lb_wait returns an error, never verdicts, when that re-verification could not
+ *     be submitted (lb_verify_requests_finish returned the error first);
+ *   - at most 256 two-phase calls can be unfinished: the context keeps one record per
+ *     ticket in a 256-entry ring, and lb_verify_requests_partial_async refuses a call
+ *     with LB_ERR_RESOURCES (nothing enqueued) while its ring entry still holds a call
+ *     that is neither finished nor waited for, instead of overwriting it.
+ * LB_TP_RELEASE=0 (legacy): the call holds its slot until finish; its outputs are
+ * written only by the per-request tails or the verdict, i.e. never provisional.
  */
 #define LB_BATCH_DEVICE 1u
 int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* batch, uint32_t flags,

@@ -182,9 +182,14 @@ class ErrorText {
 // A released two-phase call (LB_TP_RELEASE): what lb_partial_wait, lb_verify_requests_finish
 // and lb_wait need once its slot has moved on -- the partial, and the call itself (the
 // caller's buffers stay valid until lb_wait returns) for a re-run when the combine fails.
+// Until its ticket is waited for, a released call's outputs hold provisional verdicts (every
+// request not already false valid), so a record is never overwritten while it can still
+// change them: lb_verify_requests_partial_async refuses a call whose ring entry is live
+// (tp_reusable).  `failed`: the re-run after a failed combined check could not be submitted;
+// lb_wait then returns that error instead of the provisional verdicts.
 struct TwoPhaseRec {
   uint64_t ticket = 0;
-  bool device = false, finished = false, have_partial = false;
+  bool device = false, finished = false, have_partial = false, failed = false, waited = false;
   uint64_t rerun = 0;  // the one-phase re-run's ticket (failed combine)
   lb_request_batch batch{};
   uint8_t *valid = nullptr, *err = nullptr, *sst = nullptr;
@@ -241,6 +246,7 @@ struct lb_ctx {
   // combine (-5..-7 % at N = 1); a failed combined check re-runs the shard
   // as a one-phase call.  One record per two-phase ticket (ring by ticket).
   bool tp_release = true;
+  bool fault_rerun = false;  // LB_FAULT_RERUN=1 (tests only): a failed combine's re-run fails to submit
   TwoPhaseRec tp[kTwoPhaseRing];
   ErrorText err;
   hipStream_t stream = nullptr;  // slot 0 stream 0 (synchronous helper calls)
@@ -323,6 +329,7 @@ struct lb_ctx {
   bool mtail_lp = true;
   bool gt_lp = true;  // lb_gt_check's final exponentiation as a round program (LB_GT_LP=0: one wave)
   int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
+  int q_plain = 0, q_high = 0, q_masked = 0;  // its streams in the process tally (g_q_*)
   bool lane = false;  // lb_create_lane: a latency-lane context (one slot, no CU-masked streams)
   int last_call_streams = 0;  // streams of the last submitted verify call (begin_call)
   unsigned long long lp_clk[4] = {};  // clock stamps of the last retired latency-path call
@@ -1171,6 +1178,22 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
   return lane * 64 * 32 * (size_t)cus;
 }
 
+// The streams of every live context of this process, by kind: HIP pools the
+// plain streams of one priority into at most GPU_MAX_HW_QUEUES queues PER PROCESS, so a
+// second context's plain and high-priority streams share the first one's queues (up to
+// that cap) while each CU-masked stream takes a queue of its own.  A latency-lane context
+// (lb_create_lane, optional: the addon runs without one) is priced on the process total
+// against kProcessQueueBudget, the largest process configuration seen to run: bench.py's
+// process and the node addon's, 16 plain + 2 CU-masked + 4 high-priority queues (the main
+// context's priority lane and aux stream, and the second context's two).
+static std::mutex g_q_mu;
+static int g_q_plain = 0, g_q_high = 0, g_q_masked = 0;
+static constexpr int kProcessQueueBudget = 22;
+
+static int pooled_queues(int plain, int high, int masked, int maxq) {
+  return (plain < maxq ? plain : maxq) + (high < maxq ? high : maxq) + masked;
+}
+
 static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (!out_ctx) return LB_ERR_INVALID_ARGUMENT;
   *out_ctx = nullptr;
@@ -1212,6 +1235,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = atoi(e) != 0;
+  if (const char* e = getenv("LB_FAULT_RERUN")) ctx->fault_rerun = atoi(e) != 0;
   if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_PRIO_KCOPY")) ctx->prio_kcopy = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_MAX")) {
@@ -1319,6 +1343,24 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
       delete ctx;
       return LB_ERR_RESOURCES;
     }
+    std::lock_guard<std::mutex> g(g_q_mu);
+    const int proc = pooled_queues(g_q_plain + plain, g_q_high + high, g_q_masked + masked, maxq);
+    if (lane && proc > kProcessQueueBudget) {
+      char msg[300];
+      snprintf(msg, sizeof msg,
+               "latency-lane context refused: the process would hold %d hardware queues (%d plain, %d high-priority "
+               "streams pooled into at most GPU_MAX_HW_QUEUES=%d each, %d CU-masked), above the %d that ran",
+               proc, g_q_plain + plain, g_q_high + high, maxq, g_q_masked + masked, kProcessQueueBudget);
+      g_create_err = msg;
+      delete ctx;
+      return LB_ERR_RESOURCES;
+    }
+    g_q_plain += plain;
+    g_q_high += high;
+    g_q_masked += masked;
+    ctx->q_plain = plain;
+    ctx->q_high = high;
+    ctx->q_masked = masked;
     ctx->hw_queues = queues;
   }
   for (int s = 0; ok && s <= ctx->n_slots; s++) {
@@ -1445,6 +1487,12 @@ int lb_destroy(lb_ctx* ctx) {
   if (ctx->d_aux) (void)hipFree(ctx->d_aux);
   if (ctx->h_aux) (void)hipHostFree(ctx->h_aux);
   if (ctx->d_lp) (void)hipFree(ctx->d_lp);
+  {
+    std::lock_guard<std::mutex> g(g_q_mu);
+    g_q_plain -= ctx->q_plain;
+    g_q_high -= ctx->q_high;
+    g_q_masked -= ctx->q_masked;
+  }
   delete ctx;
   return LB_OK;
 }
@@ -1531,10 +1579,14 @@ static void pick_streams(lb_ctx* ctx, Slot& sl) {
 static void tp_record(lb_ctx* ctx, uint64_t ticket, const lb_request_batch* b, bool device, uint8_t* valid,
                       uint8_t* err, uint8_t* sst) {
   if (!ctx->tp_release) return;
+  // (the ticket ring too: a finish of a ticket whose record was reused -- finished or waited
+  // for by then, tp_reusable -- is a no-op, not an error)
+  ctx->two_phase[ctx->two_phase_pos] = ticket;
+  ctx->two_phase_pos = (ctx->two_phase_pos + 1) % lb_ctx::kTwoPhaseRing;
   TwoPhaseRec& r = ctx->tp[ticket % lb_ctx::kTwoPhaseRing];
   r.ticket = ticket;
   r.device = device;
-  r.finished = r.have_partial = false;
+  r.finished = r.have_partial = r.failed = r.waited = false;
   r.rerun = 0;
   r.batch = *b;
   r.valid = valid;
@@ -1550,6 +1602,14 @@ static void tp_record(lb_ctx* ctx, uint64_t ticket, const lb_request_batch* b, b
 static TwoPhaseRec* tp_find(lb_ctx* ctx, uint64_t ticket) {
   TwoPhaseRec& r = ctx->tp[ticket % lb_ctx::kTwoPhaseRing];
   return (ticket && ctx->tp_release && r.ticket == ticket) ? &r : nullptr;
+}
+
+// A record may be overwritten once nothing about its call can change: it was waited for, or
+// it was finished (with a submitted re-run, if any, retired).  Before that its outputs hold
+// provisional verdicts that only its record turns into final ones.
+static bool tp_reusable(lb_ctx* ctx, const TwoPhaseRec& r) {
+  if (!r.ticket || r.waited) return true;
+  return r.finished && !r.failed && (!r.rerun || !slot_of_ticket(ctx, r.rerun));
 }
 
 static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t* d_valid, uint8_t* d_req_err,
@@ -1784,6 +1844,15 @@ int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* b, uin
   if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(sm_pump(ctx));
+  if (ctx->tp_release && !tp_reusable(ctx, ctx->tp[ctx->next_ticket % lb_ctx::kTwoPhaseRing])) {
+    // (the ticket this call would take is end_call_async's next_ticket: no ticket is issued
+    // in between)
+    ctx->err = "two-phase ring full: the call " +
+               std::to_string(ctx->tp[ctx->next_ticket % lb_ctx::kTwoPhaseRing].ticket) +
+               " is neither finished nor waited for (" + std::to_string(lb_ctx::kTwoPhaseRing) +
+               "-entry ring by ticket): finish or wait for older two-phase calls first";
+    return LB_ERR_RESOURCES;
+  }
   Slot& sl = next_async_slot(ctx);
   if (flags & LB_BATCH_DEVICE)
     return submit_device(ctx, sl, b, out_valid, out_req_err, out_set_status, true, out_ticket);
@@ -1858,14 +1927,24 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
     // the combined check failed: the shard again as a one-phase call -- its own merged check
     // fails and every request is verified alone (worker.ts:74-85) -- into the same outputs,
     // after the released call has retired (its verdicts must not land after the re-run's)
+    // (a failure from here on leaves the outputs provisional: the record says so, and
+    // lb_wait returns the error instead of them)
+    r->failed = true;
     if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
+    if (ctx->fault_rerun) {  // (fault injection for the tests: the re-run's submission fails)
+      ctx->err = "LB_FAULT_RERUN: the failed combine's re-verification was not submitted";
+      return LB_ERR_DEVICE;
+    }
     const lb_request_batch b = r->batch;
     uint8_t *v = r->valid, *e = r->err, *st = r->sst;
     const bool device = r->device;
     uint64_t t2 = 0;
     LB_TRY(device ? submit_device(ctx, next_async_slot(ctx), &b, v, e, st, false, &t2)
                   : submit_host(ctx, next_async_slot(ctx), &b, v, e, st, false, &t2));
-    if (TwoPhaseRec* r2 = tp_find(ctx, ticket)) r2->rerun = t2;
+    if (TwoPhaseRec* r2 = tp_find(ctx, ticket)) {
+      r2->rerun = t2;
+      r2->failed = false;
+    }
     return LB_OK;
   }
   Slot* sl = slot_of_ticket(ctx, ticket);
@@ -1971,8 +2050,25 @@ int lb_wait(lb_ctx* ctx, uint64_t ticket, lb_verify_stats* stats) {
   bool rerun = false;
   if (TwoPhaseRec* r = tp_find(ctx, ticket)) {
     // waited for without a combined verdict: as before, each request verified alone
-    if (!r->finished) LB_TRY(lb_verify_requests_finish(ctx, ticket, 0));
-    if (TwoPhaseRec* r2 = tp_find(ctx, ticket); r2 && r2->rerun) {
+    if (!r->finished) {
+      const int rc = lb_verify_requests_finish(ctx, ticket, 0);
+      if (rc != LB_OK) {
+        if (TwoPhaseRec* r2 = tp_find(ctx, ticket)) r2->waited = true;
+        return rc;
+      }
+    }
+    TwoPhaseRec* r2 = tp_find(ctx, ticket);
+    if (r2 && r2->failed) {  // the failed combine's re-run never ran: the outputs are not verdicts
+      const uint64_t own = ticket;
+      if (Slot* sl = slot_of_ticket(ctx, own)) LB_TRY(finish_slot(ctx, *sl));
+      r2->waited = true;
+      ctx->err = "two-phase call " + std::to_string(own) +
+                 ": the combined check failed and its re-verification could not be submitted; its outputs are not "
+                 "verdicts";
+      return LB_ERR_DEVICE;
+    }
+    if (r2) r2->waited = true;
+    if (r2 && r2->rerun) {
       ticket = r2->rerun;
       rerun = true;
     }

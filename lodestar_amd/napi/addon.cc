@@ -38,6 +38,7 @@
 #define NAPI_VERSION 8
 #include <node_api.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -294,6 +295,10 @@ struct Context {
   // (the reference's verifyOnMainThread / priority unshift,
   // BN/chain/bls/multithread/index.ts:174-187,544-555).  Its pubkey table mirrors ctx's.
   lb_ctx* lctx = nullptr;
+  // false once the lane's pubkey table failed to follow ctx's: from then on
+  // priority calls go back to ctx (the submission thread), never to a table that resolves
+  // indices differently
+  std::atomic<bool> lane_ok{true};
   std::thread lane;
   std::mutex lmu;
   std::condition_variable lcv;
@@ -332,16 +337,27 @@ void lane_loop(Context* c) {
       continue;
     }
     if (t->kind == Kind::SyncPubkeys) {
+      // (ctx's table, the authoritative one, already holds the keys: the task succeeds; a
+      // lane that cannot follow is retired instead of left out of sync)
       int32_t bad = -1;
       uint32_t n = 0;
-      const int rc = lb_pubkey_table_append(c->lctx, t->n_keys, t->pubkeys.data(), t->pk_len, &bad);
-      if (rc != LB_OK) {
-        fail(t, rc, c->lctx);
-      } else if (lb_pubkey_table_size(c->lctx, &n) != LB_OK || n != t->u32) {
-        t->rc = LB_ERR_DEVICE;
-        t->errmsg = "the latency lane's pubkey table is out of sync";
+      if (c->lane_ok && (lb_pubkey_table_append(c->lctx, t->n_keys, t->pubkeys.data(), t->pk_len, &bad) != LB_OK ||
+                         lb_pubkey_table_size(c->lctx, &n) != LB_OK || n != t->u32)) {
+        c->lane_ok = false;
+        fprintf(stderr, "lodestar_bls: latency lane retired (its pubkey table could not follow: %s); priority "
+                        "calls run on the main context\n", lb_last_error(c->lctx));
       }
       complete(c, t);
+      continue;
+    }
+    if (!c->lane_ok) {  // a priority call queued here before the lane retired: back to ctx
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        auto it = c->queue.begin();
+        while (it != c->queue.end() && (*it)->prio) ++it;
+        c->queue.insert(it, t);
+      }
+      c->cv.notify_all();
       continue;
     }
     t->t_start = now_ns();
@@ -519,8 +535,13 @@ void worker_loop(Context* c) {
           break;
         }
         t->target = it->second;
-        // a call whose slot was reused meanwhile has already resumed with merged_ok = 0
-        (void)lb_verify_requests_finish(c->ctx, t->target->ticket, t->merged_ok);
+        // (a released call -- LB_TP_RELEASE, the default -- holds provisional verdicts until this
+        // finish; a failed finish, e.g. the failed combine's re-run not submitted, rejects the
+        // promise: the call still retires through lb_wait below, whose error is kept)
+        {
+          const int rc = lb_verify_requests_finish(c->ctx, t->target->ticket, t->merged_ok);
+          if (rc != LB_OK) fail(t, rc, c->ctx);
+        }
         inflight.push_back(t);
         break;
       }
@@ -557,7 +578,7 @@ void worker_loop(Context* c) {
           if (bad >= 0) t->errmsg += " (pubkey " + std::to_string(bad) + ")";
         } else {
           lb_pubkey_table_size(c->ctx, &t->u32);
-          if (c->lctx) {  // the same keys into the latency lane's table, then resolve
+          if (c->lctx && c->lane_ok) {  // the same keys into the latency lane's table, then resolve
             {
               std::lock_guard<std::mutex> lk(c->lmu);
               c->lqueue.push_back(t);
@@ -663,6 +684,7 @@ napi_value make_error(napi_env env, int rc, const std::string& msg) {
                      : rc == LB_ERR_DEVICE         ? "LB_ERR_DEVICE"
                      : rc == LB_ERR_NO_DEVICE      ? "LB_ERR_NO_DEVICE"
                      : rc == LB_ERR_OUT_OF_MEMORY  ? "LB_ERR_OUT_OF_MEMORY"
+                     : rc == LB_ERR_RESOURCES      ? "LB_ERR_RESOURCES"
                                                    : "LB_ERR";
   napi_value c, m, e;
   napi_create_string_utf8(env, code, NAPI_AUTO_LENGTH, &c);
@@ -779,7 +801,7 @@ napi_value submit(napi_env env, Context* c, Task* t) {
       return promise;
     }
     if (t->kind == Kind::Close) c->closing = true;
-    if (t->prio && t->kind == Kind::Verify && c->lctx) {
+    if (t->prio && t->kind == Kind::Verify && c->lctx && c->lane_ok) {
       // the latency lane: its own thread and context; the throughput context's calls
       // submitted from now on leave the reserved CUs free (lb_mark_priority)
       lb_mark_priority(c->ctx);

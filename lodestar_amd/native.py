@@ -698,6 +698,19 @@ class Device:
                     "lb_decode_signatures")
         return [int(x) for x in st[:n]], [out[i * 192:(i + 1) * 192].tobytes() for i in range(n)]
 
+    def decode_signatures_packed(self, blob: np.ndarray, offs: np.ndarray, out: Optional[np.ndarray] = None
+                                 ) -> np.ndarray:
+        """lb_decode_signatures on an already packed blob (pack_blobs): the per-signature
+        statuses (0 = valid: Signature.fromBytes(bytes, affine, validate=true) accepts it);
+        the affine points land in `out` (n x 192 bytes) when given."""
+        n = len(offs) - 1
+        st = np.zeros(max(n, 1), np.uint8)
+        if out is None or len(out) < max(n, 1) * 192:
+            out = np.zeros(max(n, 1) * 192, np.uint8)
+        self._check(self.lib.lb_decode_signatures(self._h, n, _ptr(blob), _ptr(offs), _ptr(st), _ptr(out)),
+                    "lb_decode_signatures")
+        return st[:n]
+
     def pairing(self, g1s: Sequence[bytes], g2s: Sequence[bytes]) -> List[bytes]:
         n = len(g1s)
         a = _u8(b"".join(g1s))

@@ -238,7 +238,8 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   // slot under gossip load.  A priority call's workgroups cannot preempt the throughput
   // waves already on the GPU, so it waits for CUs to drain (DESIGN.md §7).
   const onset1 = [];
-  for (let r = 0; r < 5; r++) {
+  const onsetSamples = parseInt(process.env.LB_NODE_ONSET_SAMPLES || "20", 10);
+  for (let r = 0; r < onsetSamples; r++) {
     await new Promise((res) => setTimeout(res, 600));
     const t = ms();
     ok = ok && (await v.verifySignatureSets([set(r + 3)], {verifyOnMainThread: true})) === true;
@@ -327,7 +328,10 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
       lane_1set_clocks: {fresh: clockSummary(clkPre), after_throughput: clockSummary(clkAfter)},
       // while every slot is busy with a 65,536-set package (priority lane)
       under_load_onset: {ms_1set: onset1.map((x) => +x.toFixed(2)), p50_ms_1set: +median(onset1).toFixed(3),
-                         gap_ms: 600},
+                         max_ms_1set: +Math.max(...onset1).toFixed(3),
+                         ratio_p50_vs_idle: +(median(onset1) / median(pre1)).toFixed(2),
+                         ratio_max_vs_idle: +(Math.max(...onset1) / median(pre1)).toFixed(2),
+                         samples: onset1.length, gap_ms: 600},
       under_load: {
         p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
         p50_ms_128set_priority: load128.length ? +median(load128).toFixed(3) : null,

@@ -1,9 +1,11 @@
 #!/bin/bash
-# round 5 profiles: rocprofv3 kernel stats of the bench (every call alone: --sync, and the
-# pipelined timed region), HBM traffic PMC passes of one C2 call
+# Profiles of the bench: rocprofv3 kernel stats with every call alone (--sync,
+# LB_DAG=0: the iso timings the roofline is priced on) and of the pipelined timed region, then
+# the HBM-traffic PMC passes of one C2 call (tools/pmc.sh; summarise with tools/pmc_summarize.py).
+# usage (via gpurun): tools/gpu_profile.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
-D=gpurun_out/${1:-prof_r05}; mkdir -p $D
+D=gpurun_out/${1:-prof}; mkdir -p $D
 LB_DAG=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/sync -o run --output-format csv -- \
   python3 bench.py --sync --steps 10 --warmup 2 --no-cpu-baseline --no-legs --latency-reps 0 --iso-reps 3 \
   > $D/sync_line.json 2> $D/sync.err || exit 1

@@ -31,12 +31,18 @@ def main():
     ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--per-request", type=int, default=128)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "op_counts.json"))
+    ap.add_argument("--workloads", action="store_true",
+                    help="count BASELINE.json's C4 shard (at 1/8 scale, same proportions) and C5 epoch shapes in "
+                         "the default organisation -> profiles/op_counts_workloads.json (bench.py config_legs)")
+    ap.add_argument("--wl-out", default=os.path.join(ROOT, "profiles", "op_counts_workloads.json"))
     a = ap.parse_args()
     from lodestar_amd import build as b
     if a.build:
         print(b.build_opcount(OUT_DIR))
     if not a.run:
         return
+    if a.workloads:
+        return count_workloads(a.wl_out)
     import numpy as np
     # the bench's organisation (stored lines + multi-pair accumulation, merged check)
     os.environ["LB_MILLER"] = "lines"
@@ -97,6 +103,50 @@ def main():
            "lone_call_stages": {k: {"mads_per_set": v["mads_per_set"]} for k, v in lone.items()}}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+def count_workloads(out_path=os.path.join(ROOT, "profiles", "op_counts_workloads.json")):
+    """Every Fp product of one call of each config shape (tools/workloads.py), in the
+    organisation the library picks for it (no LB_MILLER override), pubkeys by validator
+    index from a 65,536-key table: the mads per set bench.py's config legs price."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import workloads as W
+    from lodestar_amd import native
+    native.library_path = lambda: os.path.join(OUT_DIR, "liblodestar_bls_count.so")
+    native._lib = None
+    lib = native.load_library()
+    lib.lb_opcount_stages.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    dev = native.Device(0)
+    keys = W.make_keys(dev, 65536)
+    assert dev.pubkey_table_append(keys.pks) == 65536
+    shapes = {"c4_shard": lambda: W.c4_shard(dev, keys, singles=112712 // 8, aggregates=4096 // 8),
+              "c5": lambda: W.c5_epoch(dev, keys, invalid_rate=0.0)}
+    out = {"mads_per_fp_mul": MADS_PER_FPMUL, "mads_per_fp_sqr": MADS_PER_FPSQR,
+           "note": "counting build (-DLB_COUNT_OPS), one call per shape, default organisation, all sets valid; "
+                   "c4_shard at 1/8 scale (14,089 singles + 512 AggregateAndProof triples of 488 keys)"}
+    for name, make in shapes.items():
+        p = make()
+        blob, offs = p.blobs()
+        r = dev.verify_requests(p.req_off, None, p.pk_off, p.msg_array(), blob, offs, bytes(32), pk_indices=p.idx)
+        assert r.valid.all(), name
+        names = [nm for nm, _ in dev.last_stage_times()]
+        buf = (ctypes.c_ulonglong * 32)()
+        k = lib.lb_opcount_stages(dev._h, buf, 32)
+        per, tm, ts = {}, 0, 0
+        for i in range(k):
+            muls, sqrs = (int(buf[i]) & 0xFFFFFFFF) / 2, int(buf[i]) >> 32
+            tm += muls
+            ts += sqrs
+            per[names[i]] = {"mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / p.n_sets}
+        out[name] = {"sets": p.n_sets, "requests": p.n_req, "pubkeys": int(len(p.idx)),
+                     "keys_per_set": len(p.idx) / p.n_sets, "stages": per,
+                     "mads_per_set_total": (tm * MADS_PER_FPMUL + ts * MADS_PER_FPSQR) / p.n_sets}
+        print(name, out[name]["mads_per_set_total"], flush=True)
+    dev.close()
+    with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 

@@ -1,5 +1,5 @@
 """Synthetic workloads of BASELINE.json configs C4 and C5 (shared by the GPU
-parity tests, tools/bench_workloads.py and bench.py's secondary legs).
+parity tests, bench.py's config legs and tools/opcount.py --workloads).
 
 Keys are the interop keys sk_i = LE(sha256(LE32(i))) mod r
 (packages/state-transition/src/util/interop.ts:19-23); signatures come from the
@@ -69,6 +69,8 @@ class Packed:
     msgs: List[bytes]
     sigs: List[bytes]
     expect_invalid_requests: Set[int] = field(default_factory=set)
+    clean_msgs: Optional[List[bytes]] = None  # (c5_epoch: messages / signatures before the injection)
+    clean_sigs: Optional[List[bytes]] = None
 
     @property
     def n_sets(self) -> int:
@@ -170,6 +172,9 @@ def c5_epoch(dev, keys: Keys, blocks: int = 32, committee: int = 488, seed: int 
     sigs = sign_many(dev, [sum(keys.sks[i] for i in ix) % R_ORDER for ix, _ in plan], [m for _, m in plan])
     req_off = np.arange(0, len(plan) + 1, per_block, dtype=np.uint32)
     p = _pack([(ix, m, s) for (ix, m), s in zip(plan, sigs)], None, req_off)
+    p.clean_msgs, p.clean_sigs = list(p.msgs), list(p.sigs)  # (the same epoch before the injection)
+    if invalid_rate <= 0:
+        return p
     n_bad = max(2, int(round(len(plan) * invalid_rate)))
     pos = rng.choice(len(plan), n_bad, replace=False)
     # only the two kinds the reference's bls.test.ts uses for block import (wrong root, malformed)
