@@ -870,26 +870,29 @@ def secondary_legs(a, dev, torch, cuda, pks, msgs, sigs, sks, submit, nbuf, n, n
     bad_row = (n // 2) // a.per_request
     got = keep_[0].cpu().numpy()
     assert not got[bad_row] and got.sum() == n_req - 1, "two-phase adversarial verdicts"
-    saved = {k: os.environ.get(k) for k in ("LB_TP_RELEASE", "LB_PRIO_CUS")}
-    os.environ["LB_TP_RELEASE"] = "0"
-    os.environ["LB_PRIO_CUS"] = "0"
-    try:
-        legacy_dev = Device(dev.device)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    try:
-        legacy = two_phase_bad(legacy_dev)
-    finally:
-        legacy_dev.close()
+    other = {}
+    for name, env in (("release_only", {"LB_TP_PAUSE": "0"}), ("legacy", {"LB_TP_RELEASE": "0"})):
+        saved = {k: os.environ.get(k) for k in list(env) + ["LB_PRIO_CUS"]}
+        os.environ.update(env, LB_PRIO_CUS="0")
+        try:
+            od = Device(dev.device)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        try:
+            other[name] = two_phase_bad(od)
+        finally:
+            od.close()
     legs["adversarial_two_phase"] = {
-        "sets_per_s_release": round(rel, 1), "sets_per_s_legacy": round(legacy, 1), "calls": reps,
-        "case": "one wrong-message set per 65,536-set two-phase call: the combined check fails every time; "
-                "release (LB_TP_RELEASE=1, default): the shard re-verified as a one-phase call; legacy "
-                "(LB_TP_RELEASE=0, its own context): the slot held, only the per-request tails run"}
+        "sets_per_s": round(rel, 1), "sets_per_s_release_only": round(other["release_only"], 1),
+        "sets_per_s_legacy": round(other["legacy"], 1), "calls": reps,
+        "case": "one wrong-message set per 65,536-set two-phase call: the combined check fails every time. "
+                "Default context: released calls, and after a failed combine the next 32 two-phase calls in the "
+                "legacy mode (LB_TP_PAUSE); release_only (LB_TP_PAUSE=0): every failed shard re-verified as a "
+                "one-phase call; legacy (LB_TP_RELEASE=0): the slot held, only the per-request tails run"}
     # (3) same-message gossip jobs: 512 attestation-data groups x 128 validators per call, pubkeys by index
     from lodestar_amd.native import Device  # noqa: F401
     n_jobs, per_job = 512, 128

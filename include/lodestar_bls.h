@@ -285,6 +285,10 @@ int lb_poll(lb_ctx* ctx, uint64_t ticket, int32_t* out_done);
  *     that is neither finished nor waited for, instead of overwriting it.
  * LB_TP_RELEASE=0 (legacy): the call holds its slot until finish; its outputs are
  * written only by the per-request tails or the verdict, i.e. never provisional.
+ * After a failed combined check (merged_ok = 0) the context submits its next 32
+ * two-phase calls (LB_TP_PAUSE) in the legacy mode: a re-run repeats the whole shard,
+ * the legacy mode only its per-request tails, so a stream of failing batches costs
+ * the tails alone while a clean stream keeps the release.
  */
 #define LB_BATCH_DEVICE 1u
 int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* batch, uint32_t flags,

@@ -245,7 +245,15 @@ struct lb_ctx {
   // frees its slot when its partial is out, instead of holding the slot through the host's
   // combine (-5..-7 % at N = 1); a failed combined check re-runs the shard
   // as a one-phase call.  One record per two-phase ticket (ring by ticket).
-  bool tp_release = true;
+  bool tp_release = true;  // the mode of the two-phase call being submitted
+  // LB_TP_RELEASE as configured; after a failed combined check the next tp_pause_calls two-phase
+  // calls take the legacy mode: a re-run repeats the whole shard (one wrong set per C2 call:
+  // 1.07 M sets/s released against 1.98 M legacy, bench.py adversarial_two_phase), the legacy
+  // mode runs only the per-request tails, so a stream of failing batches (invalid gossip)
+  // costs the tails alone while a clean stream keeps the release
+  bool tp_release_cfg = true;
+  uint32_t tp_pause = 0;
+  uint32_t tp_pause_calls = 32;  // (LB_TP_PAUSE; 0: always release)
   bool fault_rerun = false;  // LB_FAULT_RERUN=1 (tests only): a failed combine's re-run fails to submit
   TwoPhaseRec tp[kTwoPhaseRing];
   ErrorText err;
@@ -601,7 +609,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // stream 0 beside stream 1's hash/lines (lines_all), and k_tail multiplies it in
   const bool fold = use_msm && by_lines && !split && !steps;
   // merged check as a round program (k_lp_mtail): S_all, its Miller value and the final
-  // exponentiation from the MSM's bit sums and the level products' Horner value
+  // exponentiation from the MSM's bit sums and the 63 level products (their Horner chain folded in)
   const bool mtail = steps && use_msm && merged && ctx->mtail_lp;
   if (mtail) LB_TRY(lp_ensure(ctx));
   // (steps + merged: the merged pair's lines come from a one-lane kernel before the
@@ -771,7 +779,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       // (mtail: the merged pair's Miller value comes from the round program, not as lines)
       LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, mtail ? 0xffffffffu : n_sets + n_req,
                rows, d_req_off, (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
-      LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
+      // (mtail: the round program runs the Horner chain over the level products itself, on the
+      // Miller loop's squarings of (-g1, S_all): no one-wave k_horner_all)
+      if (!mtail) LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
     } else {
       LB_STAGE("req_horner", 0, k_req_horner, n_req, TPB, n_req, n_sets, rows, d_req_off, (const uint32_t*)d_G,
                (const uint8_t*)d_bad, d_F, (const uint8_t*)nullptr);
@@ -858,7 +868,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     }
     const uint32_t* merged_lines = (fold || steps) ? nullptr : (const uint32_t*)d_lines;
     if (mtail) {
-      hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Fall, (const g2j*)d_mG, d_mt_in);
+      hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Pl, (const g2j*)d_mG, d_mt_in);
       LB_HIP(hipGetLastError());
       if (partial) {  // F_all * Miller(-g1, S_all) back into d_Fall, encoded by k_partial below
         LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_PARTIAL].off,
@@ -1233,8 +1243,11 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_TAIL")) ctx->tail_wave = strcmp(e, "lane") != 0;
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_LINES_MIN")) ctx->lines_min_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
-  if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = atoi(e) != 0;
+  if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = ctx->tp_release_cfg = atoi(e) != 0;
+  if (const char* e = getenv("LB_TP_PAUSE")) ctx->tp_pause_calls = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_FAULT_RERUN")) ctx->fault_rerun = atoi(e) != 0;
   if (const char* e = getenv("LB_GT_LP")) ctx->gt_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_PRIO_KCOPY")) ctx->prio_kcopy = atoi(e) != 0;
@@ -1601,7 +1614,8 @@ static void tp_record(lb_ctx* ctx, uint64_t ticket, const lb_request_batch* b, b
 
 static TwoPhaseRec* tp_find(lb_ctx* ctx, uint64_t ticket) {
   TwoPhaseRec& r = ctx->tp[ticket % lb_ctx::kTwoPhaseRing];
-  return (ticket && ctx->tp_release && r.ticket == ticket) ? &r : nullptr;
+  // (records exist only for calls submitted in the release mode, whatever the mode now)
+  return (ticket && r.ticket == ticket) ? &r : nullptr;
 }
 
 // A record may be overwritten once nothing about its call can change: it was waited for, or
@@ -1844,6 +1858,8 @@ int lb_verify_requests_partial_async(lb_ctx* ctx, const lb_request_batch* b, uin
   if (!out_valid || !out_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(sm_pump(ctx));
+  ctx->tp_release = ctx->tp_release_cfg && ctx->tp_pause == 0;
+  if (ctx->tp_pause) ctx->tp_pause--;
   if (ctx->tp_release && !tp_reusable(ctx, ctx->tp[ctx->next_ticket % lb_ctx::kTwoPhaseRing])) {
     // (the ticket this call would take is end_call_async's next_ticket: no ticket is issued
     // in between)
@@ -1930,6 +1946,7 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
     // (a failure from here on leaves the outputs provisional: the record says so, and
     // lb_wait returns the error instead of them)
     r->failed = true;
+    ctx->tp_pause = ctx->tp_pause_calls;  // (the next two-phase calls: legacy mode)
     if (Slot* sl = slot_of_ticket(ctx, ticket)) LB_TRY(finish_slot(ctx, *sl));
     if (ctx->fault_rerun) {  // (fault injection for the tests: the re-run's submission fails)
       ctx->err = "LB_FAULT_RERUN: the failed combine's re-verification was not submitted";
@@ -1961,6 +1978,7 @@ int lb_verify_requests_finish(lb_ctx* ctx, uint64_t ticket, int merged_ok) {
     ctx->err = "ticket is not a two-phase call";
     return LB_ERR_INVALID_ARGUMENT;
   }
+  if (!merged_ok && ctx->tp_release_cfg) ctx->tp_pause = ctx->tp_pause_calls;  // (failures go on: stay legacy)
   return finish_partial(ctx, *sl, merged_ok != 0);
 }
 

@@ -17,6 +17,9 @@
 #define LB_LP_VERIFY_WPE 4
 #endif
 #define LB_LP_MAX_REGS 1024               // LDS registers (64 B each)
+// the merged-check programs (k_lp_mtail, one workgroup per call) hold the call's 63 level
+// products as inputs (k_horner_all folded in): a larger register file, 96 KB of LDS
+#define LB_LP_MTAIL_REGS 1536
 #define LB_LP_MAX_FLAGS 512
 #define LB_LP_STAMPS (6 + 6 * LB_LP_TPB / 64)  // diagnostic s_memtime points per round (k_lp_program stamps): 6 of
                                               // the workgroup, run_unit start / end of every wave, 4 inside its unit
@@ -47,7 +50,9 @@
 #define LB_LP_PROG_MTAIL_PARTIAL 5  // ... its two-phase form: the shard's partial
 #define LB_LP_PROG_FINAL_LANE 6     // final exponentiation == 1 of a one-lane Fp12 (lb_gt_check)
 #define LB_LP_NPROGS 7
-#define LB_MTAIL_NIN (12 + 6 * LB_MSM_POS)  // mtail inputs: the Horner value, the MSM's 33 bit sums
+#define LB_MTAIL_LEVELS 63                  // the step-major accumulation's Horner levels (k_steps.hip)
+#define LB_MTAIL_NIN (12 * LB_MTAIL_LEVELS + 6 * LB_MSM_POS)  // mtail inputs: the 63 level products, the MSM's
+                                                              // 33 bit sums
 
 namespace lb {
 // k_lp.hip: instance b (one workgroup of LB_LP_TPB threads) runs the round program at
@@ -102,8 +107,8 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restri
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,
                                                              uint8_t* __restrict__ out);
-// in16 of the merged check: the Horner value F (one-lane fp12) and the MSM's bit sums G
-__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ F, const g2j* __restrict__ G,
+// in16 of the merged check: the 63 level products P_l (one-lane fp12) and the MSM's bit sums G
+__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ Pl, const g2j* __restrict__ G,
                                                     uint32_t* __restrict__ in16);
 // 12 records of one-lane limbs -> fp12
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F);

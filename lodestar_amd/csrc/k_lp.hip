@@ -40,13 +40,16 @@ using namespace co;
 
 namespace {
 
-struct LpShared {
-  uint32_t reg[LB_LP_MAX_REGS * 16];
+template <int NREGS>
+struct LpSharedT {
+  uint32_t reg[NREGS * 16];
   uint32_t flag[LB_LP_MAX_FLAGS];
 #ifndef LB_LP_DIRECT
   uint32_t ring[LB_LP_RING];
 #endif
 };
+using LpShared = LpSharedT<LB_LP_MAX_REGS>;
+using LpSharedMtail = LpSharedT<LB_LP_MTAIL_REGS>;  // (k_lp_mtail: the level products as inputs)
 constexpr uint32_t RMASK = LB_LP_RING - 1;
 #ifndef LB_LP_DIRECT
 static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
@@ -58,6 +61,7 @@ constexpr int NT = 16;                        // inline terms per operand
 constexpr int RECW = 4 + 2 * NT;              // fixed unit record (lpgen/compile.py)
 constexpr int YT = 3 + NT;                    // first y term word
 static constexpr uint32_t INV_FIX_RAW[13] = LB_LP_INV_FIX_RAW_LIMBS;
+__device__ __constant__ const uint32_t LB_LP_R416_RAW[12] = LB_LP_R416_RAW_LIMBS;
 
 // A row's unit record, spread over the row: lane j holds words j, 16 + j and 32 + j;
 // a word reaches the whole row by a DPP broadcast (row_newbcast).  Every lane loading
@@ -174,7 +178,8 @@ template <class R>
 LB_CO void skip_form(const R& rec, int& o) { o += 1 + (int)(rec[o] & 255u); }
 
 // the one-operand units on a normalized value x; returns true when it wrote a flag
-LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_t lane, uint32_t pj, uint32_t& v) {
+template <class SH>
+LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, SH& S, uint32_t lane, uint32_t pj, uint32_t& v) {
   if (op == LB_LP_OP_LIN) {
     v = x;
     return false;
@@ -208,8 +213,8 @@ LB_CO bool single_op(uint32_t op, uint32_t dst, uint32_t x, LpShared& S, uint32_
   return true;
 }
 
-template <class R>
-LB_CO void ext_unit(const R& rec, LpShared& S, uint32_t lane, uint32_t pj) {
+template <class R, class SH>
+LB_CO void ext_unit(const R& rec, SH& S, uint32_t lane, uint32_t pj) {
   const uint32_t w0 = rec[0];
   const uint32_t op = w0 & 15u, nops = (w0 >> 4) & 7u, nfl = (w0 >> 7) & 7u, dst = w0 >> 16;
   int o = 1 + (int)nfl;
@@ -233,7 +238,8 @@ LB_CO void ext_unit(const R& rec, LpShared& S, uint32_t lane, uint32_t pj) {
 }
 
 // one unit from its prefetched record; every lane of the row calls it
-LB_CO void run_unit(const Desc& d, LpShared& S, uint32_t cons, uint32_t lane, uint32_t pj,
+template <class SH>
+LB_CO void run_unit(const Desc& d, SH& S, uint32_t cons, uint32_t lane, uint32_t pj,
                     const uint32_t* __restrict__ gsp, unsigned long long* ustamp = nullptr) {
   // ustamp (diagnostic): s_memtime after the register reads / x form / y form / product
 #define LB_LP_USTAMP(k)                                                       \
@@ -330,7 +336,8 @@ struct Stream {
 // from the program stream (global memory; every workgroup running the program reads the
 // same blocks, so L2), issued one round ahead like the ring's prefetch and waited for only
 // where the next round uses them; extended records are read from the stream in place.
-LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
+template <class SH>
+LB_CO void lp_round(SH& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
                     uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
   (void)pf;
@@ -375,7 +382,8 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
 #undef LB_LP_STAMP
 }
 #else
-LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
+template <class SH>
+LB_CO void lp_round(SH& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu, uint4& pf,
                     uint32_t tid, uint32_t lane, uint32_t row, uint32_t pj,
                     unsigned long long* stamps, uint32_t r) {
   // stamps (diagnostic): LB_LP_STAMPS s_memtime points per round, lane 0 of the workgroup
@@ -455,7 +463,8 @@ LB_CO void lp_round(LpShared& S, Stream& st, Desc& d, uint32_t& bw, uint32_t& nu
 // Miller values); in_flags: n_inflag words; out: n_out 16-word records;
 // out_flags: n_outflag words.  stamps (diagnostic, usually nullptr): s_memtime
 // after every round's barrier.
-LB_DEV void lp_run(LpShared& S, const uint32_t* __restrict__ prog, const uint32_t* __restrict__ in_a, uint32_t split,
+template <class SH>
+LB_DEV void lp_run(SH& S, const uint32_t* __restrict__ prog, const uint32_t* __restrict__ in_a, uint32_t split,
                    const uint32_t* __restrict__ in_b, const uint32_t* __restrict__ in_flags,
                    uint32_t* __restrict__ out, uint32_t* __restrict__ out_flags,
                    unsigned long long* __restrict__ stamps = nullptr) {
@@ -774,7 +783,7 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCal
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restrict__ prog,
                                                         const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
                                                         uint32_t* __restrict__ out16) {
-  __shared__ LpShared S;
+  __shared__ LpSharedMtail S;
   __shared__ uint32_t s_fl[4];
   lp_run(S, prog, in16, 0xffffffffu, in16, nullptr, out16, s_fl);
   __syncthreads();
@@ -791,16 +800,28 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __r
   if (threadIdx.x == 0) out[0] = s_fl[0] ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ F, const g2j* __restrict__ G,
+// The merged-check program's inputs as 16-word records: the 63 level products P_l (k_level_prod)
+// in the program's domain (R = 2^416: x 2^416 / 2^384, one product by the raw constant 2^416 mod
+// p -- lpgen/bls.py mtail_program takes them as raw inputs), then the MSM's 33 bit sums in the
+// one-lane form (converted by the program).  fp12: 12 fp in the order c0.c0.c0 ... c1.c2.c1;
+// g2j: X.c0, X.c1, Y.c0, Y.c1, Z.c0, Z.c1.
+__global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ Pl, const g2j* __restrict__ G,
                                                     uint32_t* __restrict__ in16) {
-  const uint32_t i = threadIdx.x;
-  if (i >= LB_MTAIL_NIN) return;
-  // (fp12: 12 fp in the order c0.c0.c0 ... c1.c2.c1; g2j: X.c0, X.c1, Y.c0, Y.c1, Z.c0, Z.c1)
-  const fp v = i < 12 ? (&F->c0.c0.c0)[i] : (&G[(i - 12) / 6].X.c0)[(i - 12) % 6];
+  constexpr uint32_t NP = 12 * LB_MTAIL_LEVELS;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)LB_MTAIL_NIN; i += blockDim.x) {
+    fp v;
+    if (i < NP) {
+      fp k;
+      fp_set(k, LB_LP_R416_RAW);
+      fp_mul(v, (&Pl[i / 12].c0.c0.c0)[i % 12], k);
+    } else {
+      v = (&G[(i - NP) / 6].X.c0)[(i - NP) % 6];
+    }
 #pragma unroll
-  for (int j = 0; j < 12; j++) in16[16 * i + j] = v.l[j];
+    for (int j = 0; j < 12; j++) in16[16 * i + j] = v.l[j];
 #pragma unroll
-  for (int j = 12; j < 16; j++) in16[16 * i + j] = 0u;
+    for (int j = 12; j < 16; j++) in16[16 * i + j] = 0u;
+  }
 }
 
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {

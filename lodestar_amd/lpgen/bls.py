@@ -746,26 +746,54 @@ def msm_sum(pts) -> Proj:
     return acc
 
 
-MTAIL_INPUTS = ["h%d" % k for k in range(12)] + ["G%d_%s" % (p, c) for p in range(MSM_POS)
-                                                 for c in ("X0", "X1", "Y0", "Y1", "Z0", "Z1")]
+def miller1_levels(q: Proj, void: Flag, P) -> Fp12:
+    """conj(prod_l (P_l * lines_l)^(2^(62 - l))): the call's 63 level products P_l
+    (k_level_prod: the good requests' lane values of level l) folded into the Miller loop
+    of the one pair (-g1, Q) -- the value k_horner_all's Horner chain times miller1(q,
+    void), with ONE squaring chain for both (conj is multiplicative).  P_l times its
+    level's lines is formed beside the chain (the lines depend on the T-chain only), so
+    a level costs the chain one squaring and one product."""
+    g = q.X.g
+    P1 = g1_line_point(Jac(g.const(C["LB_G1_X"]), g.const(C["LB_G1_NEG_Y"]), g.one()))
+    Q = g2_homogeneous(q)
+    T = Q
+    f = None
+    for lvl, i in enumerate(range(62, -1, -1)):
+        T, ln = miller_dbl_step(T, P1)
+        m = P[lvl].mul_line(*unit_line(g, void, ln)).mat()
+        if (X_ABS >> i) & 1:
+            T, ln = miller_add_step(T, Q, P1)
+            m = m.mul_line(*unit_line(g, void, ln)).mat()
+        f = m if f is None else (f.sqr().mat() * m).mat()
+    return f.conj()
+
+
+MTAIL_LEVELS = 63  # k_steps.hip: the Horner levels of the step-major accumulation
+MTAIL_INPUTS = ["P%d_%d" % (lvl, k) for lvl in range(MTAIL_LEVELS) for k in range(12)] + [
+    "G%d_%s" % (p, c) for p in range(MSM_POS) for c in ("X0", "X1", "Y0", "Y1", "Z0", "Z1")]
 
 
 def mtail_program(partial: bool) -> Graph:
-    """inputs: the call's Horner value conj(prod_l P_l^(2^(62-l))) over its good requests'
-    lane values (k_horner_all) and the MSM's 33 bit sums G_p (Jacobian G2, one-lane
-    Montgomery form); S_all = sum 2^p G_p; f = Horner value * Miller(-g1, S_all).
+    """inputs: the call's 63 level products P_l over its good requests' lane values
+    (k_level_prod) and the MSM's 33 bit sums G_p (Jacobian G2, one-lane Montgomery form);
+    S_all = sum 2^p G_p; f = conj(Horner over l of P_l) * Miller(-g1, S_all), the Horner
+    chain and the Miller loop's squarings shared (miller1_levels: k_horner_all folded in).
     check: output flag is_one = (final_exp(f) == 1).  partial: f as 12 canonical Fp in
     the one-lane form (R = 2^384), the shard's 576-byte partial before encoding."""
     g = Graph("mtail_partial" if partial else "mtail_check")
-    v = [g.input(n) for n in MTAIL_INPUTS]
-    h = Fp12.from_fps(v[:12])
+    # (the level products come converted to this domain by k_mtail_prep: no conversion unit
+    # per input, and no register held by a raw input until its conversion)
+    n_p = 12 * MTAIL_LEVELS
+    v = [g.input_raw(n) if k < n_p else g.input(n) for k, n in enumerate(MTAIL_INPUTS)]
+    P = [Fp12.from_fps(v[12 * lvl:12 * lvl + 12]) for lvl in range(MTAIL_LEVELS)]
+    o = 12 * MTAIL_LEVELS
     pts = []
     zero, one = Fp2.zero(g), Fp2.one(g)
     for p in range(MSM_POS):
-        X, Y, Z = (Fp2(v[12 + 6 * p + 2 * c], v[12 + 6 * p + 2 * c + 1]) for c in range(3))
+        X, Y, Z = (Fp2(v[o + 6 * p + 2 * c], v[o + 6 * p + 2 * c + 1]) for c in range(3))
         pts.append(select(Z.is_zero(), Proj(zero, one, zero), proj_from_jac(Jac(X, Y, Z))))
     S = msm_sum(pts)
-    f = (h * miller1(S, S.Z.is_zero())).mat()
+    f = miller1_levels(S, S.Z.is_zero(), P).mat()
     if partial:
         r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
         for k, x in enumerate(f.fps()):

@@ -90,39 +90,55 @@ def test_ring_refuses_the_257th_unfinished_call():
         dev.close()
 
 
+def _device_call(dev, args, torch, cuda):
+    req, pk, _, mg, blob, offs, seed = args
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).copy()).to(cuda)  # noqa: E731
+    d = [t(req.view(np.int32)), t(pk), t(mg), t(blob), t(offs.view(np.int32)), t(np.frombuffer(seed, np.uint8))]
+    d_valid = torch.zeros(len(req) - 1, dtype=torch.uint8, device=cuda)
+    d_err = torch.zeros(len(req) - 1, dtype=torch.uint8, device=cuda)
+    torch.cuda.synchronize()
+    tk = dev.verify_requests_device_async(len(req) - 1, int(req[-1]), d[0].data_ptr(), d[1].data_ptr(), None,
+                                          d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr(), d[5].data_ptr(),
+                                          d_valid.data_ptr(), d_err.data_ptr(), partial=True)
+    ok = dev.gt_check([dev.partial_wait_t(tk)])
+    dev.finish_t(tk, ok)
+    dev.wait(tk)
+    return ok, [bool(v) for v in d_valid.cpu().numpy()], d_err.cpu().numpy()
+
+
 def test_failed_combine_after_release_host_and_device():
+    """A failed combine gives per-request false after the release (host buffers, then device
+    buffers on a fresh context: the provisional outputs are overwritten by the re-run); the
+    call after a failed combine takes the legacy mode (kTpPause) with the same verdicts."""
     import torch
     from lodestar_amd.native import Device
+    cuda = torch.device("cuda", 0)
     dev = Device(0)
     try:
         pks, msgs, sigs, expect = _sets(dev, 8, bad={5})
         want = [all(expect[0:4]), all(expect[4:8])]
         assert want == [True, False]
         args = _args(pks, msgs, sigs, 4)
-        # host buffers
+        # host buffers, release mode (a fresh context)
         pc = dev.verify_requests_async(*args, partial=True)
         ok = dev.gt_check([dev.partial_wait(pc)])
         assert not ok
         dev.verify_finish(pc, ok)
         r = dev.wait_call(pc)
         assert [bool(v) for v in r.valid] == want and r.batch_retries == 1
-        # device buffers: the provisional outputs are overwritten by the re-run
-        cuda = torch.device("cuda", 0)
-        req, pk, _, mg, blob, offs, seed = args
-        t = lambda x: torch.from_numpy(np.ascontiguousarray(x).copy()).to(cuda)  # noqa: E731
-        d = [t(req.view(np.int32)), t(pk), t(mg), t(blob), t(offs.view(np.int32)), t(np.frombuffer(seed, np.uint8))]
-        d_valid = torch.zeros(2, dtype=torch.uint8, device=cuda)
-        d_err = torch.zeros(2, dtype=torch.uint8, device=cuda)
-        torch.cuda.synchronize()
-        tk = dev.verify_requests_device_async(2, 8, d[0].data_ptr(), d[1].data_ptr(), None, d[2].data_ptr(),
-                                              d[3].data_ptr(), d[4].data_ptr(), d[5].data_ptr(), d_valid.data_ptr(),
-                                              d_err.data_ptr(), partial=True)
-        ok = dev.gt_check([dev.partial_wait_t(tk)])
-        assert not ok
-        dev.finish_t(tk, ok)
-        dev.wait(tk)
-        assert [bool(v) for v in d_valid.cpu().numpy()] == want
-        assert not d_err.cpu().numpy().any()
+        # the next calls after the failure: legacy mode, same verdicts (device, then host)
+        ok, got, err = _device_call(dev, args, torch, cuda)
+        assert not ok and got == want and not err.any()
+        pc = dev.verify_requests_async(*args, partial=True)
+        ok = dev.gt_check([dev.partial_wait(pc)])
+        dev.verify_finish(pc, ok)
+        assert [bool(v) for v in dev.wait_call(pc).valid] == want
+    finally:
+        dev.close()
+    dev = Device(0)
+    try:  # device buffers, release mode
+        ok, got, err = _device_call(dev, args, torch, cuda)
+        assert not ok and got == want and not err.any()
     finally:
         dev.close()
 

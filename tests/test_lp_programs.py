@@ -194,13 +194,30 @@ def _jac_inputs(pt, z):
     return [x0 * z2 % P, x1 * z2 % P, y0 * z3 % P, y1 * z3 % P, z, 0]
 
 
-def _mtail_inputs(h, pts, seed=7):
+def _mtail_inputs(levels, pts, seed=7):
+    """levels: the 63 level products P_l (raw inputs, this domain: k_mtail_prep converts);
+    pts: the 33 bit sums (one-lane Montgomery inputs)"""
     import random
     rnd = random.Random(seed)
-    vals = f12_fps(h)
+    vals = [mont416(v) for lv in levels for v in f12_fps(lv)]
+    g = []
     for pt in pts:
-        vals += _jac_inputs(pt, rnd.randrange(1, P))
-    return [mont(v) for v in vals]
+        g += _jac_inputs(pt, rnd.randrange(1, P))
+    return vals + [mont(v) for v in g]
+
+
+def _levels_for(h):
+    """level products whose value conj(prod_l P_l^(2^(62 - l))) is h: P_62 = conj(h), the rest 1"""
+    one = O.f12_mul(O.f12_inv(h), h)
+    return [one] * (bls.MTAIL_LEVELS - 1) + [O.f12_conj(h)]
+
+
+def _horner_value(levels):
+    """conj(prod_l P_l^(2^(62 - l))) by the oracle (k_horner_all's value)"""
+    acc = levels[0]
+    for lv in levels[1:]:
+        acc = O.f12_mul(O.f12_sqr(acc), lv)
+    return O.f12_conj(acc)
 
 
 def _msm_points(n_inf=3):
@@ -224,9 +241,9 @@ def test_mtail_programs_against_oracle():
     good = O.miller_loop(O.G1, S)      # e(g1, S) e(-g1, S) = 1
     bad = O.miller_loop(O.G1, O.g2_add(S, O.G2))
     for h, want in ((good, 1), (bad, 0)):
-        _, fl = mtail_prog(False).run(_mtail_inputs(h, pts), [])
+        _, fl = mtail_prog(False).run(_mtail_inputs(_levels_for(h), pts), [])
         assert fl == [want]
-        outs, _ = mtail_prog(True).run(_mtail_inputs(h, pts), [])
+        outs, _ = mtail_prog(True).run(_mtail_inputs(_levels_for(h), pts), [])
         f = tuple(tuple((outs[6 * a + 2 * b] * pow(1 << 384, -1, P) % P,
                          outs[6 * a + 2 * b + 1] * pow(1 << 384, -1, P) % P) for b in range(3)) for a in range(2))
         assert all(o < P for o in outs)  # canonical one-lane form
@@ -234,10 +251,26 @@ def test_mtail_programs_against_oracle():
     # S_all = O (every bit sum infinite): the Miller factor is 1
     inf_pts = [None] * bls.MSM_POS
     one = O.f12_mul(O.miller_loop(O.G1, O.G2), O.miller_loop(O.E1.neg(O.G1), O.G2))
-    _, fl = mtail_prog(False).run(_mtail_inputs(one, inf_pts), [])
+    _, fl = mtail_prog(False).run(_mtail_inputs(_levels_for(one), inf_pts), [])
     assert fl == [1]
-    _, fl = mtail_prog(False).run(_mtail_inputs(O.miller_loop(O.G1, O.G2), inf_pts), [])
+    _, fl = mtail_prog(False).run(_mtail_inputs(_levels_for(O.miller_loop(O.G1, O.G2)), inf_pts), [])
     assert fl == [0]
+
+
+def test_mtail_horner_over_levels():
+    """The folded Horner chain: 63 distinct level products (Miller values of small multiples
+    of the generators) -- the partial equals conj(Horner over the P_l) * Miller(-g1, S_all)
+    up to the factors the final exponentiation kills, and the check passes exactly when
+    that product is 1 after the final exponentiation."""
+    pts, S = _msm_points()
+    levels = [O.miller_loop(O.g1_mul(O.G1, 3 + lv), O.g2_mul(O.G2, 5 + 2 * lv)) for lv in range(bls.MTAIL_LEVELS)]
+    want_f = O.f12_mul(_horner_value(levels), O.miller_loop(O.E1.neg(O.G1), S))
+    outs, _ = mtail_prog(True).run(_mtail_inputs(levels, pts), [])
+    f = tuple(tuple((outs[6 * a + 2 * b] * pow(1 << 384, -1, P) % P,
+                     outs[6 * a + 2 * b + 1] * pow(1 << 384, -1, P) % P) for b in range(3)) for a in range(2))
+    assert O.f12_eq(O.final_exp(f), O.final_exp(want_f))
+    _, fl = mtail_prog(False).run(_mtail_inputs(levels, pts), [])
+    assert fl == [int(O.f12_is_one(O.final_exp(want_f)))]
 
 
 def test_final_lane_program():
