@@ -84,6 +84,9 @@ struct PipeState {
   bool steps = false;
   Rows rows{};
   const uint32_t* d_G = nullptr;
+  // the failed merged check's per-request tails as round programs (k_lp_rtail): staged inputs
+  uint32_t* d_rt_in = nullptr;
+  uint32_t* d_rt_fl = nullptr;
 };
 
 // A same-message package in flight (lb_verify_same_message_batch[_async]):
@@ -335,6 +338,10 @@ struct lb_ctx {
   // MSM's bit sums, Miller(-g1, S_all), final exponentiation on one workgroup) instead of
   // msm_final + lines of S_all + the one-wave k_tail (LB_MTAIL=0: the one-wave chain)
   bool mtail_lp = true;
+  // LB_RTAIL (default 1): a failed merged check's per-request tails (Miller(-g1, S_k), F_k times
+  // it, final exponentiation) as one round program per request (k_lp_rtail) instead of one-lane
+  // lines of S_k (k_lines_S) + the one-wave chain (k_tail)
+  bool rtail_lp = true;
   bool gt_lp = true;  // lb_gt_check's final exponentiation as a round program (LB_GT_LP=0: one wave)
   int hw_queues = 0;  // hardware queues this context opens (priced by lb_create's guard)
   int q_plain = 0, q_high = 0, q_masked = 0;  // its streams in the process tally (g_q_*)
@@ -541,13 +548,23 @@ int run_tails(lb_ctx* ctx, Slot& sl) {
       LB_STAGE("sum_tree", 0, k_sum_tree, p.n_req, TPB, p.n_req, p.d_req_off, (const g2j*)p.d_rsig, p.d_S,
                (const uint8_t*)p.d_mflag);
     }
-    LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
-             p.d_lines, (const uint8_t*)p.d_mflag);
+    if (!p.d_rt_in)
+      LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
+               p.d_lines, (const uint8_t*)p.d_mflag);
     if (p.steps)
       LB_STAGE("req_horner", 0, k_req_horner, p.n_req, TPB, p.n_req, p.n_sets, p.rows, p.d_req_off, p.d_G,
                (const uint8_t*)p.d_bad, p.d_F, (const uint8_t*)p.d_mflag);
-    LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
-             (const fp12*)p.d_F, (const uint8_t*)p.d_bad, p.d_valid, (const uint8_t*)p.d_mflag);
+    if (p.d_rt_in) {
+      hipLaunchKernelGGL(k_rtail_prep, dim3((p.n_req * LB_RTAIL_NIN + 255) / 256), dim3(256), 0, sl.st[0], p.n_req,
+                         (const fp12*)p.d_F, (const g2a*)p.d_S, p.d_rt_in, p.d_rt_fl);
+      LB_HIP(hipGetLastError());
+      LB_STAGE("rtail", 0, k_lp_rtail, p.n_req, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_RTAIL].off, p.n_req,
+               (const uint32_t*)p.d_rt_in, (const uint32_t*)p.d_rt_fl, (const uint8_t*)p.d_bad, p.d_valid,
+               (const uint8_t*)p.d_mflag);
+    } else {
+      LB_STAGE("tail", 0, k_tail, p.n_req, TPB, p.n_req, p.n_pairs, p.n_sets, (const uint32_t*)p.d_lines,
+               (const fp12*)p.d_F, (const uint8_t*)p.d_bad, p.d_valid, (const uint8_t*)p.d_mflag);
+    }
     hipLaunchKernelGGL(k_merge_stats, dim3(1), dim3(TPB), 0, sl.st[0], p.n_req, p.d_req_off, (const uint8_t*)p.d_bad,
                        (const uint8_t*)p.d_mflag, p.d_mstats);
     LB_HIP(hipGetLastError());
@@ -623,6 +640,11 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2a* d_S = ws.take<g2a>(n_req);
   fp12* d_fS = ws.take<fp12>(n_req);
   fp12* d_F = ws.take<fp12>(n_req);
+  // (a merged call's failure path: the per-request tails' round-program inputs, k_lp_rtail)
+  const bool rtail = merged && tail_wave && ctx->rtail_lp;
+  if (rtail) LB_TRY(lp_ensure(ctx));
+  uint32_t* d_rt_in = rtail ? ws.take<uint32_t>((size_t)(n_req ? n_req : 1) * LB_RTAIL_NIN * 16) : nullptr;
+  uint32_t* d_rt_fl = rtail ? ws.take<uint32_t>(n_req ? n_req : 1) : nullptr;
   uint8_t* d_bad = ws.take<uint8_t>(n_req);
   g2a* d_Sall = ws.take<g2a>(1);
   fp12* d_Fall = ws.take<fp12>(1);
@@ -840,6 +862,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   ps.d_lines = d_lines;
   ps.d_S = d_S;
   ps.d_F = d_F;
+  ps.d_rt_in = d_rt_in;
+  ps.d_rt_fl = d_rt_fl;
   ps.d_bad = d_bad;
   ps.d_valid = d_valid;
   ps.d_mflag = d_mflag;
@@ -919,7 +943,8 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 + 16 + 576 +
                    (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 + (2 * LB_MSM_W * sizeof(g2j)) / LB_MSM_T + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
-  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4;
+  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
+                   (size_t)LB_RTAIL_NIN * 64 + 4 + 2 * 256 / 64;  // (+ k_lp_rtail's records and flag)
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
                            8 * 256;
   // (+ the merged check's round-program records, k_lp_mtail)
@@ -1176,6 +1201,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
+                           (const void*)k_lp_rtail,
                            (const void*)k_msm_buckets, (const void*)k_decode_sigs, (const void*)k_scalar_pk};
   size_t lane = 0;
   for (const void* k : kernels) {
@@ -1246,6 +1272,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LINES_MIN")) ctx->lines_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_RTAIL")) ctx->rtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_TP_RELEASE")) ctx->tp_release = ctx->tp_release_cfg = atoi(e) != 0;
   if (const char* e = getenv("LB_TP_PAUSE")) ctx->tp_pause_calls = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_FAULT_RERUN")) ctx->fault_rerun = atoi(e) != 0;
@@ -1423,7 +1450,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   // the latency path's round programs (2.6 MB) are uploaded here, before any call is in
   // flight: a synchronous copy on the first latency-path call would wait for the
   // throughput calls already running on blocking (CU-masked) streams
-  if (ok && (ctx->lp_max_sets || ctx->mtail_lp || ctx->gt_lp) && lp_ensure(ctx) != LB_OK) ok = false;
+  if (ok && (ctx->lp_max_sets || ctx->mtail_lp || ctx->gt_lp || ctx->rtail_lp) && lp_ensure(ctx) != LB_OK) ok = false;
   // the priority slot's staging and workspace sized here for a latency-path call of
   // lp_max_sets sets (16 keys each by bytes): growing them later frees the old buffers,
   // and hipFree / hipHostFree synchronize the device -- the call would wait for every

@@ -49,7 +49,10 @@
 #define LB_LP_PROG_MTAIL_CHECK 4    // the throughput pipeline's merged check (lpgen/bls.py mtail_program)
 #define LB_LP_PROG_MTAIL_PARTIAL 5  // ... its two-phase form: the shard's partial
 #define LB_LP_PROG_FINAL_LANE 6     // final exponentiation == 1 of a one-lane Fp12 (lb_gt_check)
-#define LB_LP_NPROGS 7
+#define LB_LP_PROG_RTAIL 7          // one request's tail after a failed merged check (k_lp_rtail)
+#define LB_LP_NPROGS 8
+#define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf
+#define LB_LP_RTAIL_REGS 512            // (its program holds ~240 registers: 32 KB of LDS)
 #define LB_MTAIL_LEVELS 63                  // the step-major accumulation's Horner levels (k_steps.hip)
 #define LB_MTAIL_NIN (12 * LB_MTAIL_LEVELS + 6 * LB_MSM_POS)  // mtail inputs: the 63 level products, the MSM's
                                                               // 33 bit sums
@@ -110,6 +113,20 @@ __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __r
 // in16 of the merged check: the 63 level products P_l (one-lane fp12) and the MSM's bit sums G
 __global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ Pl, const g2j* __restrict__ G,
                                                     uint32_t* __restrict__ in16);
+// k_lp_rtail's inputs: LB_RTAIL_NIN 16-word records and one input flag per request
+__global__ void __launch_bounds__(256) k_rtail_prep(uint32_t n_req, const fp12* __restrict__ F,
+                                                    const g2a* __restrict__ S, uint32_t* __restrict__ in16,
+                                                    uint32_t* __restrict__ inflag);
+// the per-request tails of a failed merged check as round programs, one workgroup per request:
+// valid[k] = final_exp(F_k * Miller(-g1, S_k)) == 1; requests already false or a passed merged
+// check (skip) are settled without arithmetic, as k_tail does
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_rtail(const uint32_t* __restrict__ prog,
+                                                                          uint32_t n_req,
+                                                                          const uint32_t* __restrict__ in16,
+                                                                          const uint32_t* __restrict__ inflag,
+                                                                          const uint8_t* __restrict__ req_bad,
+                                                                          uint8_t* __restrict__ valid,
+                                                                          const uint8_t* __restrict__ skip);
 // 12 records of one-lane limbs -> fp12
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F);
 }  // namespace lb

@@ -50,6 +50,7 @@ struct LpSharedT {
 };
 using LpShared = LpSharedT<LB_LP_MAX_REGS>;
 using LpSharedMtail = LpSharedT<LB_LP_MTAIL_REGS>;  // (k_lp_mtail: the level products as inputs)
+using LpSharedRtail = LpSharedT<LB_LP_RTAIL_REGS>;  // (k_lp_rtail: a small program, two workgroups per CU)
 constexpr uint32_t RMASK = LB_LP_RING - 1;
 #ifndef LB_LP_DIRECT
 static_assert((LB_LP_RING & (LB_LP_RING - 1)) == 0, "ring size: power of two");
@@ -822,6 +823,42 @@ __global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ Pl,
 #pragma unroll
     for (int j = 12; j < 16; j++) in16[16 * i + j] = 0u;
   }
+}
+
+__global__ void __launch_bounds__(256) k_rtail_prep(uint32_t n_req, const fp12* __restrict__ F,
+                                                    const g2a* __restrict__ S, uint32_t* __restrict__ in16,
+                                                    uint32_t* __restrict__ inflag) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_req * (uint32_t)LB_RTAIL_NIN) return;
+  const uint32_t k = t / LB_RTAIL_NIN, i = t % LB_RTAIL_NIN;
+  const fp v = i < 12 ? (&F[k].c0.c0.c0)[i]
+                      : i == 12 ? S[k].x.c0 : i == 13 ? S[k].x.c1 : i == 14 ? S[k].y.c0 : S[k].y.c1;
+#pragma unroll
+  for (int j = 0; j < 12; j++) in16[16 * t + j] = v.l[j];
+#pragma unroll
+  for (int j = 12; j < 16; j++) in16[16 * t + j] = 0u;
+  if (i == 0) inflag[k] = S[k].inf ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_rtail(const uint32_t* __restrict__ prog,
+                                                                          uint32_t n_req,
+                                                                          const uint32_t* __restrict__ in16,
+                                                                          const uint32_t* __restrict__ inflag,
+                                                                          const uint8_t* __restrict__ req_bad,
+                                                                          uint8_t* __restrict__ valid,
+                                                                          const uint8_t* __restrict__ skip) {
+  __shared__ LpSharedRtail S;
+  __shared__ uint32_t s_fl[4];
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req) return;
+  if (req_bad[k] || (skip && *skip)) {  // (uniform per workgroup)
+    if (threadIdx.x == 0) valid[k] = req_bad[k] ? 0 : 1;
+    return;
+  }
+  const uint32_t* in = in16 + (size_t)k * LB_RTAIL_NIN * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, inflag + k, nullptr, s_fl);
+  __syncthreads();
+  if (threadIdx.x == 0) valid[k] = s_fl[0] ? 1 : 0;
 }
 
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {

@@ -803,6 +803,25 @@ def mtail_program(partial: bool) -> Graph:
     return g
 
 
+RTAIL_INPUTS = ["F%d" % k for k in range(12)] + ["S_x0", "S_x1", "S_y0", "S_y1"]
+
+
+def rtail_program() -> Graph:
+    """One request's tail after a failed merged check (the per-request re-verification,
+    worker.ts:74-85): inputs F_k (its Miller value, one-lane fp12) and S_k = sum r_i sigma_i
+    (affine G2, one-lane form; input flag S_inf: S_k = O); output flag is_one =
+    (final_exp(F_k * Miller(-g1, S_k)) == 1) -- k_lines_S + k_tail's one-wave chain as one
+    round program per request (k_lp_rtail)."""
+    g = Graph("rtail_check")
+    v = [g.input(n) for n in RTAIL_INPUTS]
+    s_inf = g.input_flag("S_inf")
+    F = Fp12.from_fps(v[:12])
+    S = Proj(Fp2(v[12], v[13]), Fp2(v[14], v[15]), Fp2.one(g))
+    f = (F * miller1(S, s_inf)).mat()
+    g.output_flag("is_one", final_exp(f).is_one())
+    return g
+
+
 def final_lane_program() -> Graph:
     """final exponentiation == 1 of a one-lane Fp12 (canonical, R = 2^384)"""
     g = Graph("final_exp_lane")

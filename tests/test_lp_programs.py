@@ -279,3 +279,22 @@ def test_final_lane_program():
     for f, want in ((one, 1), (O.miller_loop(O.G1, O.G2), 0)):
         _, fl = g.run([mont(v) for v in f12_fps(f)], [])
         assert fl == [want]
+
+
+def test_rtail_program_against_oracle():
+    """One request's tail of a failed merged check (k_lp_rtail): final_exp(F_k * Miller(-g1,
+    S_k)) == 1 exactly when F_k cancels e(-g1, S_k); S_k = O (input flag): the Miller factor
+    is 1."""
+    g = lpc.compile_graph(bls.rtail_program(), rows=32)
+    S = O.g2_mul(O.G2, 12345)
+    good = O.miller_loop(O.G1, S)
+    bad = O.miller_loop(O.G1, O.g2_add(S, O.G2))
+    (x0, x1), (y0, y1) = S
+    for f, want in ((good, 1), (bad, 0)):
+        _, fl = g.run([mont(v) for v in f12_fps(f) + [x0, x1, y0, y1]], [0])
+        assert fl == [want]
+    one = O.f12_mul(O.miller_loop(O.G1, O.G2), O.miller_loop(O.E1.neg(O.G1), O.G2))
+    _, fl = g.run([mont(v) for v in f12_fps(one) + [0, 0, 0, 0]], [1])
+    assert fl == [1]
+    _, fl = g.run([mont(v) for v in f12_fps(good) + [0, 0, 0, 0]], [1])
+    assert fl == [0]
