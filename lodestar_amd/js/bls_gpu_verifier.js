@@ -161,8 +161,7 @@ function packRequests(requests, seed, keyMap) {
 
 /** packRequests in slices of `slice` sets with the event loop turning between them: a
  * 65,536-set package is ~4 ms of main-thread work, and a priority call's completion
- * (or a gossip handler) must not wait for all of it (VERDICT r4 #2). */
-/** packRequests in slices of `slice` sets, the event loop turning between them.  `timing`
+ * (or a gossip handler) must not wait for all of it (VERDICT r4 #2).  `timing`
  * (optional): timing.mainThreadS receives the sum of the synchronous slices alone -- the
  * main thread's own share, without the turns spent on other work in between (ADVICE r5). */
 async function packRequestsAsync(requests, seed, keyMap, slice = 8192, timing = null) {
