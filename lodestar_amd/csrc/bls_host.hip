@@ -1233,6 +1233,7 @@ static int pooled_queues(int plain, int high, int masked, int maxq) {
 static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (!out_ctx) return LB_ERR_INVALID_ARGUMENT;
   *out_ctx = nullptr;
+  const bool lane_ctx = lane;  // (the queue guard's block below has a `lane` of its own: bytes per lane)
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || device < 0 || device >= n) return LB_ERR_NO_DEVICE;
   lb_ctx* ctx = new lb_ctx();
@@ -1385,7 +1386,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
     }
     std::lock_guard<std::mutex> g(g_q_mu);
     const int proc = pooled_queues(g_q_plain + plain, g_q_high + high, g_q_masked + masked, maxq);
-    if (lane && proc > kProcessQueueBudget) {
+    if (lane_ctx && proc > kProcessQueueBudget) {
       char msg[300];
       snprintf(msg, sizeof msg,
                "latency-lane context refused: the process would hold %d hardware queues (%d plain, %d high-priority "

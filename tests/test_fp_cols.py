@@ -1,0 +1,57 @@
+"""The carry-free column products (lodestar_amd/csrc/bls_fp_cols.h: 13 digits of 30 bits,
+Montgomery radix 2^384) against Python big integers, on the host (g++ build of the same
+header): mul / sqr (a, b < p -> a b 2^-384 mod p, fully reduced), mulw (a, b < 2^384 -> the
+exact 768-bit product) and redc (w < p 2^384 -> w 2^-384 mod p, fully reduced), on edge values
+(0, 1, p - 1, 2^384 - 1 for mulw, p 2^384 - 1 for redc, all-ones limbs) and random ones.  The
+GPU build of the same functions is exercised by the field self-test (tests/test_gpu_field.py)
+and every parity test when the library is built with them."""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+R = 1 << 384
+RINV = pow(R, -1, P)
+
+
+@pytest.fixture(scope="module")
+def lib(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("cols") / "libfp_cols_host.so")
+    src = os.path.join(ROOT, "tests", "native", "fp_cols_host.cpp")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out, src])
+    return ctypes.CDLL(out)
+
+
+def _arr(v, n):
+    return (ctypes.c_uint32 * n)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)])
+
+
+def _val(a, n):
+    return sum(int(a[i]) << (32 * i) for i in range(n))
+
+
+def test_columns_against_big_ints(lib):
+    rnd = random.Random(11)
+    edge_p = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, 2 ** 380, sum(0xFFFFFFFF << (32 * i) for i in range(11))]
+    vals = edge_p + [rnd.randrange(P) for _ in range(400)]
+    r = (ctypes.c_uint32 * 12)()
+    w = (ctypes.c_uint32 * 24)()
+    for k, a in enumerate(vals):
+        b = vals[(7 * k + 3) % len(vals)]
+        lib.cols_mul(r, _arr(a, 12), _arr(b, 12))
+        assert _val(r, 12) == a * b * RINV % P, (a, b)
+        lib.cols_sqr(r, _arr(a, 12))
+        assert _val(r, 12) == a * a * RINV % P, a
+    wide = [0, 1, R - 1, R - 2, P, 2 * P, 2 * P - 1] + [rnd.randrange(R) for _ in range(300)]
+    for k, a in enumerate(wide):
+        b = wide[(5 * k + 1) % len(wide)]
+        lib.cols_mulw(w, _arr(a, 12), _arr(b, 12))
+        assert _val(w, 24) == a * b, (a, b)
+    reds = [0, 1, P * R - 1, P * R // 2, (P - 1) * (P - 1), 4 * P * P] + [rnd.randrange(P * R) for _ in range(300)]
+    for x in reds:
+        lib.cols_redc(r, _arr(x, 24))
+        assert _val(r, 12) == x * RINV % P, x

@@ -1,6 +1,7 @@
 // Fp2 / Fp12 product microbenchmark on gfx950 at 1-4 waves per SIMD: the lazy-reduction
 // Fp2 product (bls_field.h, default) vs -DLB_NO_LAZY (three Montgomery products).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DLB_NO_LAZY] -o fp2_bench fp2_bench.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DLB_NO_LAZY] [-DLB_FP_COLS=15] -o fp2_bench fp2_bench.hip
+// (LB_FP_COLS: the carry-free column bodies of bls_fp_cols.h, a bit per product kind)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +24,8 @@ __global__ void __launch_bounds__(64, 1) k_fp2(uint32_t* out, int iters) {
     if (V == 0) { fp2_mul(a, a, b); fp2_mul(c, c, b); }
     if (V == 1) { fp12_sqr(f, f); }
     if (V == 2) { fp12_mul_line(f, f, a, b, c); }
+    if (V == 3) { fp_mul(a.c0, a.c0, b.c0); fp_mul(c.c1, c.c1, b.c1); }
+    if (V == 4) { fp_sqr(a.c0, a.c0); fp_sqr(c.c1, c.c1); }
   }
   uint32_t s = 0;
   for (int j = 0; j < 12; j++) s ^= a.c0.l[j] ^ c.c1.l[j] ^ f.c0.c0.c0.l[j] ^ f.c1.c2.c1.l[j];
@@ -46,7 +49,7 @@ int main() {
 #ifdef LB_NO_LAZY
   printf("variant: LB_NO_LAZY\n");
 #else
-  printf("variant: lazy\n");
+  printf("variant: lazy, LB_FP_COLS=%d\n", LB_FP_COLS);
 #endif
   for (int occ : {1, 2, 4}) {
     const int blocks = 1024 * occ;
@@ -55,6 +58,8 @@ int main() {
     run(k_fp2<0>, buf, blocks, 64, 2, "fp2_mul", lds);
     run(k_fp2<1>, buf, blocks, 16, 1, "fp12_sqr", lds);
     run(k_fp2<2>, buf, blocks, 16, 1, "fp12_line", lds);
+    run(k_fp2<3>, buf, blocks, 256, 2, "fp_mul", lds);
+    run(k_fp2<4>, buf, blocks, 256, 2, "fp_sqr", lds);
   }
   return 0;
 }
