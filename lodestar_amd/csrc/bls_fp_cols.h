@@ -8,7 +8,11 @@
 // column) before the Montgomery reduction adds its 13 m_i p terms to the same columns.  The
 // reduction takes 12 digits of 30 bits and a last one of 24 (30 x 12 + 24 = 384), so the
 // Montgomery radix stays R = 2^384 and these bodies are drop-in replacements of the asm ones
-// (same arguments, same bounds, same results): microbenchmark tools/microbench/fp_cols_bench.hip.
+// (same arguments and results; operands up to 2^384 give a result < 2^384, canonical when the
+// contract's bounds hold, as the asm bodies do).  Measured (tools/microbench/fp2_bench.hip,
+// DESIGN.md §4 "Field core"): the squaring 16 % fewer cycles than the asm one; the product and
+// the lazy Fp2 product's halves (mulw, redc) no faster once the digit conversions are paid --
+// so LB_FP_COLS selects them per kind.
 // LB_HD: device code in the library; plain inline C++ for the host tests
 // (tests/native/fp_cols_host.cpp, tests/test_fp_cols.py).
 #pragma once
@@ -113,26 +117,30 @@ LB_HD void reduce384(uint64_t* c) {
   }
   normalize(c, 12, 24);
 }
-// bits 384 .. 767 of the normalised columns 12 .. 25 -> 12 limbs, then one conditional
-// subtraction of p (the value is < 2p)
-LB_HD void out384(const uint64_t* c, uint32_t* r) {
-  uint32_t t[12];
+// bits 384 .. 799 of the normalised columns 12 .. 26 -> 12 limbs + a 13th word, then one
+// conditional subtraction of p.  The value is < 2p for operands < 2p (and w < p R), as the
+// contract states; callers also pass operands up to 2^384, where it is < 2^384 + p: the 13th
+// word keeps such a value whole and the subtraction brings it below 2^384 (the asm bodies do
+// the same with their carry-out limb), so the result is always < 2^384 and < p whenever the
+// value was < 2p.
+LB_HD void out384(uint64_t* c, uint32_t* r) {
+  c[26] += c[25] >> 30;  // (columns 25 and 26 normalised too: bits 750 .. 809)
+  c[25] &= M30;
+  uint32_t t[13];
 #pragma unroll
-  for (int j = 0; j < 12; j++) {
+  for (int j = 0; j < 13; j++) {
     const int o = 384 + 32 * j, k = o / 30, s = o % 30;
     uint32_t v = (uint32_t)c[k] >> s;
-    v |= (uint32_t)c[k + 1] << (30 - s);
-    if (60 - s < 32) v |= (uint32_t)c[k + 2] << (60 - s);
+    if (k + 1 < 27) v |= (uint32_t)c[k + 1] << (30 - s);
+    if (60 - s < 32 && k + 2 < 27) v |= (uint32_t)c[k + 2] << (60 - s);
     t[j] = v;
   }
-  // t - p: 13 digits of 30 bits would avoid the carry flags, but the limb chain is what the
-  // callers' values live in; a borrow chain over 12 limbs
-  uint32_t s[12];
+  uint32_t s[13];
   uint32_t br = 0;
 #pragma unroll
-  for (int j = 0; j < 12; j++) {
+  for (int j = 0; j < 13; j++) {
     constexpr uint32_t P32[12] = LB_P_LIMBS;
-    const uint64_t d = (uint64_t)t[j] - P32[j] - br;
+    const uint64_t d = (uint64_t)t[j] - (j < 12 ? P32[j] : 0u) - br;
     s[j] = (uint32_t)d;
     br = (uint32_t)(d >> 63);
   }

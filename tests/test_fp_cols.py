@@ -55,3 +55,19 @@ def test_columns_against_big_ints(lib):
     for x in reds:
         lib.cols_redc(r, _arr(x, 24))
         assert _val(r, 12) == x * RINV % P, x
+    # operands beyond the contract, up to 2^384 (as callers pass lazily reduced values): the
+    # result stays < 2^384 and congruent (the asm bodies' behaviour), canonical when < 2p
+    big = [R - 1, R - 2, 5 * P, 9 * P + 7] + [rnd.randrange(R) for _ in range(200)]
+    for k, a in enumerate(big):
+        b = big[(3 * k + 1) % len(big)]
+        for fn, args, want in ((lib.cols_mul, (_arr(a, 12), _arr(b, 12)), a * b),
+                               (lib.cols_sqr, (_arr(a, 12),), a * a)):
+            fn(r, *args)
+            v = _val(r, 12)
+            assert v < R and v % P == want * RINV % P, (a, b)
+            if (want + ((-want * pow(P, -1, R)) % R) * P) // R < 2 * P:
+                assert v < P
+        for x in (a * a, a * b, R * R - 1):
+            lib.cols_redc(r, _arr(x % (R * R), 24))
+            v = _val(r, 12)
+            assert v < R and v % P == (x % (R * R)) * RINV % P

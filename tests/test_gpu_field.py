@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tests", "native", "libfield_selftest.so")
+# (LB_FIELD_SELFTEST: another build of the same self-test, e.g. with -DLB_FP_COLS=2)
+LIB = os.environ.get("LB_FIELD_SELFTEST") or os.path.join(ROOT, "tests", "native", "libfield_selftest.so")
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 R = 1 << 384
 RINV = pow(R, -1, P)
