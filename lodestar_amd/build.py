@@ -13,7 +13,7 @@ LIB = os.path.join(HERE, "liblodestar_bls.so")
 UNITS = ["k_final.hip", "k_pairing.hip", "k_aux.hip", "k_hash.hip", "k_miller.hip", "k_scalar.hip", "k_sets.hip",
          "k_prod.hip", "k_tail.hip", "k_ssz.hip", "k_msm.hip", "k_steps.hip", "k_lp.hip", "lp_blob.hip",
          "bls_host.hip"]
-HEADERS = ["bls_kernels.h", "bls_inv.h", "bls_field.h", "bls_fp_ps.h", "bls_fp_cols.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h",
+HEADERS = ["bls_kernels.h", "bls_inv.h", "bls_field.h", "bls_fp_ps.h", "bls_curve.h", "bls_hash.h", "bls_pairing.h",
            "bls_wc12.h", "bls_wc12_tables.h", "gen_constants.py", "gen_fp_asm.py", "gen_wc12.py"]
 # headers / generated files only some units depend on (a regenerated program blob must
 # not rebuild every kernel unit)

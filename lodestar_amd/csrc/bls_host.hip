@@ -209,13 +209,11 @@ struct TicketStats {
 
 struct lb_ctx {
   int device = -1;
-  // total streams <= GPU_MAX_HW_QUEUES (4 on the box; a fifth stream shares a
-  // hardware queue and measured -20 %, profiles/ab_r01i.txt).  Default: one
-  // single-stream slot per hardware queue (4, or 8 with GPU_MAX_HW_QUEUES>=8),
-  // i.e. that many calls in flight on the async API; a
-  // synchronous call runs on slot 0 as the two-stream DAG (lowest latency) by
-  // borrowing slot 1's stream for its duration.  LB_SLOTS=3: slot 0 owns two
-  // streams, slots 1-2 one each; LB_SLOTS=2: two DAG slots.
+  // One single-stream slot per hardware queue HIP gives this process: GPU_MAX_HW_QUEUES
+  // (HIP's default and the box's setting are 4; at most kMaxSlots) -- more streams than
+  // queues share a queue and measured -20 %, profiles/ab_r01i.txt.  That many calls are
+  // in flight on the async API; a synchronous call runs on slot 0 as the two-stream DAG
+  // by borrowing slot 1's stream for its duration.  LB_SLOTS overrides the count.
   // (24 hardware queues failed: HSA_STATUS_ERROR_OUT_OF_RESOURCES at k_miller_acc's dispatch,
   // whose 3.3 KB/lane private segment is reserved per queue; profiles/ab_r03/r03g_q24_fail.txt)
   static constexpr int kMaxSlots = 16;
@@ -266,7 +264,9 @@ struct lb_ctx {
   // below lines_min_sets; stored lines + multi-pair accumulation per request
   // (k_lines/k_miller_acc, highest throughput) from there.  LB_MILLER=wave|lane|lines forces one.
   int miller_mode = 0;  // 0 auto, 1 lane, 2 lines, 3 wave
-  uint32_t lines_min_sets = 8192;
+  // 1025: every call the latency path does not take (lp_max_sets) uses the stored lines;
+  // 1.5k-6k-set calls 25-29 -> 17-19 ms, C5 27.2 -> 21.0 ms (profiles/r06/orgs_probe_r06f.json)
+  uint32_t lines_min_sets = 1025;
   uint32_t wave_max_sets = 1024;
   // LB_LINES_WAVES: 1 or 2 waves/SIMD for k_lines(_rows): 2 spills (3.4 -> 4.7 ms alone) but its
   // waves share SIMDs with other calls' in the pipeline (profiles/ab_r03/ab_r03r, ab_r03s)
@@ -307,7 +307,7 @@ struct lb_ctx {
   uint32_t merge_min_req = 8;
   // merged calls of at least msm_min_sets sets take S_all from the bucket MSM
   // (k_msm.hip) instead of per-set ladders (LB_MSM_MIN, 0 = never)
-  uint32_t msm_min_sets = 4096;
+  uint32_t msm_min_sets = 1025;  // (same probe: from 1025 sets the MSM beats the ladders)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;

@@ -28,7 +28,7 @@ def device_modes(request):
     """A context per verification organisation.  Throughput pipeline (latency
     path off): one pair per lane (k_miller_sets), stored lines + multi-pair
     accumulation (k_lines / k_miller_acc, which the library otherwise picks only
-    for calls of >= 8192 sets) and stored lines + one wave per pair (k_lines /
+    for calls of >= 1025 sets) and stored lines + one wave per pair (k_lines /
     k_pair_wc).  "lp": every call on the latency path (k_lp_verify, one
     workgroup per set running the round programs), whatever its size."""
     import os

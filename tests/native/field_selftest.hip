@@ -27,8 +27,6 @@ LB_DEV void store(uint32_t* p, const fp& a) {
 // op 3: fp_pow_p34 (a: 12 limbs)      -> 12 limbs
 // op 4: fp_mul (a, b: 12 limbs)       -> 12 limbs
 // op 5: fp_sqr (a: 12 limbs)          -> 12 limbs
-// ops 6 - 9: the column bodies themselves (bls_fp_cols.h, whatever LB_FP_COLS selects):
-//   6 cols::mul, 7 cols::sqr (12 limbs out), 8 cols::mulw (24 out), 9 cols::redc (a: 24 limbs)
 __global__ void k_selftest(int op, uint32_t n, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                            uint32_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -66,33 +64,10 @@ __global__ void k_selftest(int op, uint32_t n, const uint32_t* __restrict__ a, c
     load(y, b + 12 * i);
     fp_mul(r, x, y);
     store(out + 12 * i, r);
-  } else if (op == 5) {
+  } else {
     fp x, r;
     load(x, a + 12 * i);
     fp_sqr(r, x);
-    store(out + 12 * i, r);
-  } else if (op == 6 || op == 7) {
-    fp x, y, r;
-    load(x, a + 12 * i);
-    if (op == 6) {
-      load(y, b + 12 * i);
-      cols::mul(r.l, x.l, y.l);
-    } else {
-      cols::sqr(r.l, x.l);
-    }
-    store(out + 12 * i, r);
-  } else if (op == 8) {
-    fp x, y;
-    load(x, a + 12 * i);
-    load(y, b + 12 * i);
-    uint32_t w[24];
-    cols::mulw(w, x.l, y.l);
-    for (int j = 0; j < 24; j++) out[24 * i + j] = w[j];
-  } else {
-    uint32_t w[24];
-    for (int j = 0; j < 24; j++) w[j] = a[24 * i + j];
-    fp r;
-    cols::redc(r.l, w);
     store(out + 12 * i, r);
   }
 }
@@ -100,8 +75,8 @@ __global__ void k_selftest(int op, uint32_t n, const uint32_t* __restrict__ a, c
 
 // Host-buffer entry: copies in, runs op over n elements, copies out.  0 = ok.
 extern "C" int lbt_field_op(int op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
-  const size_t wa = (op == 0 || op == 2 || op == 9) ? 24 : 12, wb = op == 0 ? 24 : 12;
-  const size_t wo = (op == 0 || op == 1 || op == 8) ? 24 : 12;
+  const size_t wa = (op == 0 || op == 2) ? 24 : 12, wb = op == 0 ? 24 : 12;
+  const size_t wo = (op == 0 || op == 1) ? 24 : 12;
   uint32_t *da = nullptr, *db = nullptr, *dout = nullptr;
   if (hipMalloc(&da, n * wa * 4) != hipSuccess || hipMalloc(&db, n * wb * 4) != hipSuccess ||
       hipMalloc(&dout, n * wo * 4) != hipSuccess)

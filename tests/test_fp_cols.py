@@ -1,10 +1,11 @@
-"""The carry-free column products (lodestar_amd/csrc/bls_fp_cols.h: 13 digits of 30 bits,
+"""The carry-free column products (tools/microbench/fp_cols.h, an experiment kept out of the library: 13 digits of 30 bits,
 Montgomery radix 2^384) against Python big integers, on the host (g++ build of the same
 header): mul / sqr (a, b < p -> a b 2^-384 mod p, fully reduced), mulw (a, b < 2^384 -> the
 exact 768-bit product) and redc (w < p 2^384 -> w 2^-384 mod p, fully reduced), on edge values
-(0, 1, p - 1, 2^384 - 1 for mulw, p 2^384 - 1 for redc, all-ones limbs) and random ones.  The
-GPU build of the same functions is exercised by the field self-test (tests/test_gpu_field.py)
-and every parity test when the library is built with them."""
+(0, 1, p - 1, 2^384 - 1 for mulw, p 2^384 - 1 for redc, all-ones limbs) and random ones.
+DESIGN.md §4 "Field core": measured on MI355X, only the squaring came out faster, and the gfx950
+build of the converting bodies disagreed with this host build on the device self-test, so the
+library keeps its product-scanning asm."""
 import ctypes
 import os
 import random

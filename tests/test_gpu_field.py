@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# (LB_FIELD_SELFTEST: another build of the same self-test, e.g. with -DLB_FP_COLS=2)
+# (LB_FIELD_SELFTEST: another build of the same self-test)
 LIB = os.environ.get("LB_FIELD_SELFTEST") or os.path.join(ROOT, "tests", "native", "libfield_selftest.so")
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 R = 1 << 384
@@ -112,21 +112,3 @@ def test_fp_sqr(lib):
     r = run(lib, 5, limbs(xs, 12), None, 12)
     assert ints(r) == [x * x * RINV % P for x in xs]
 
-
-def test_column_bodies_on_device(lib):
-    """bls_fp_cols.h's bodies themselves on the GPU (whichever LB_FP_COLS the library takes):
-    mul / sqr on operands < p, mulw on operands < 2^384, redc on w < p R -- the host test
-    (tests/test_fp_cols.py) runs the same header through g++."""
-    xs = edge_and_random(200, P, 12)
-    ys = edge_and_random(200, P, 13)
-    r = run(lib, 6, limbs(xs, 12), limbs(ys, 12), 12)
-    assert ints(r) == [x * y * RINV % P for x, y in zip(xs, ys)]
-    r = run(lib, 7, limbs(xs, 12), None, 12)
-    assert ints(r) == [x * x * RINV % P for x in xs]
-    wa = edge_and_random(200, 1 << 384, 14)
-    wb = edge_and_random(200, 1 << 384, 15)
-    r = run(lib, 8, limbs(wa, 12), limbs(wb, 12), 24)
-    assert ints(r) == [a * b for a, b in zip(wa, wb)]
-    ws = edge_and_random(200, P * (1 << 384), 16)
-    r = run(lib, 9, limbs(ws, 24), None, 12)
-    assert ints(r) == [w * RINV % P for w in ws]

@@ -372,7 +372,7 @@ def _device_with_env(**env):
 @pytest.mark.parametrize("inject", [True, False])
 def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail):
     """The merged check's sum of r_i sig_i from the bucket MSM (k_msm.hip), forced
-    onto this 1,500-set call (LB_MSM_MIN=1; by default calls of >= 4096 sets):
+    onto this 1,500-set call (LB_MSM_MIN=1; by default calls of >= 1025 sets):
     with injected failures the merged check fails and the per-request tails take
     their S_k from the per-set ladders; without, the merged check passes on the
     MSM's sum alone.  The merged check itself runs as the round program (LB_MTAIL=1,

@@ -7,12 +7,14 @@
 // alone.  A column array is normalised to 30-bit digits (a shift, a mask and a 64-bit add per
 // column) before the Montgomery reduction adds its 13 m_i p terms to the same columns.  The
 // reduction takes 12 digits of 30 bits and a last one of 24 (30 x 12 + 24 = 384), so the
-// Montgomery radix stays R = 2^384 and these bodies are drop-in replacements of the asm ones
+// Montgomery radix stays R = 2^384 and these bodies were drop-in replacements of the asm ones
 // (same arguments and results; operands up to 2^384 give a result < 2^384, canonical when the
 // contract's bounds hold, as the asm bodies do).  Measured (tools/microbench/fp2_bench.hip,
 // DESIGN.md §4 "Field core"): the squaring 16 % fewer cycles than the asm one; the product and
 // the lazy Fp2 product's halves (mulw, redc) no faster once the digit conversions are paid --
-// so LB_FP_COLS selects them per kind.
+// and the gfx950 build of these converting bodies disagreed with this header's host build on
+// the device self-test (round 6, unresolved), so the library keeps the asm bodies; this header
+// stays as the measured experiment (host-tested: tests/test_fp_cols.py).
 // LB_HD: device code in the library; plain inline C++ for the host tests
 // (tests/native/fp_cols_host.cpp, tests/test_fp_cols.py).
 #pragma once
