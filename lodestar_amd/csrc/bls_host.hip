@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "bls_kernels.h"
@@ -307,7 +308,10 @@ struct lb_ctx {
   uint32_t merge_min_req = 8;
   // merged calls of at least msm_min_sets sets take S_all from the bucket MSM
   // (k_msm.hip) instead of per-set ladders (LB_MSM_MIN, 0 = never)
-  uint32_t msm_min_sets = 1025;  // (same probe: from 1025 sets the MSM beats the ladders)
+  uint32_t msm_min_sets = 1025;
+  // merged steps calls: the level products as lane products + wave-cooperative passes
+  // (k_level_part / k_level_wc) instead of k_level_prod's one-lane LDS tree (LB_LEVEL=0)
+  bool level_wc = true;  // (same probe: from 1025 sets the MSM beats the ladders)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -454,6 +458,7 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
   } while (0)
 
 int lp_ensure(lb_ctx* ctx);
+static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req);
 int slot_copy(lb_ctx* ctx, Slot& sl, void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st);
 
 // The latency path (k_lp.hip) for a small call: pubkeys -> per-set inputs -> one
@@ -669,6 +674,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_rmeta = steps ? ws.take<uint32_t>(1) : nullptr;
   uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns) : nullptr;
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
+  // the level products' two stages (k_level_part's partials, the first k_level_wc pass's output)
+  const bool level_wc = steps && merged && ctx->level_wc;
+  const uint32_t lvl_per = level_wc ? level_blocks(n_sets, n_req) * 256u : 0u;
+  fp12* d_lvA = level_wc ? ws.take<fp12>(63 * (size_t)lvl_per) : nullptr;
+  fp12* d_lvB = level_wc ? ws.take<fp12>(63 * (size_t)((lvl_per + LB_LVL_GROUP - 1) / LB_LVL_GROUP)) : nullptr;
+  uint8_t* d_lhA = level_wc ? ws.take<uint8_t>(63 * (size_t)lvl_per) : nullptr;
+  uint8_t* d_lhB = level_wc ? ws.take<uint8_t>(63 * (size_t)lvl_per) : nullptr;
   uint32_t* d_mt_in = mtail ? ws.take<uint32_t>((size_t)LB_MTAIL_NIN * 16) : nullptr;
   uint32_t* d_mt_out = mtail && partial ? ws.take<uint32_t>(12 * 16) : nullptr;
   const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta};
@@ -799,8 +811,28 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
 #undef LB_STEP_STAGE
     if (merged) {
       // (mtail: the merged pair's Miller value comes from the round program, not as lines)
-      LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, mtail ? 0xffffffffu : n_sets + n_req,
-               rows, d_req_off, (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
+      const uint32_t s_pair = mtail ? 0xffffffffu : n_sets + n_req;
+      if (level_wc) {
+        const dim3 g_part(lvl_per / 256u, 63);
+        LB_STAGE("level_prod", 0, k_level_part, g_part, 256u, n_req, n_sets, rows, d_req_off, (const uint32_t*)d_G,
+                 (const uint8_t*)d_bad, lvl_per, d_lvA, d_lhA);
+        uint32_t pin = lvl_per;
+        fp12 *src = d_lvA, *dst = d_lvB;
+        uint8_t *sh = d_lhA, *dh = d_lhB;
+        for (;;) {
+          const uint32_t pout = (pin + LB_LVL_GROUP - 1) / LB_LVL_GROUP;
+          const dim3 g_wc(pout, 63);
+          LB_STAGE("level_wc", 0, k_level_wc, g_wc, TPB, pin, (const fp12*)src, (const uint8_t*)sh, pout, dst, dh,
+                   n_pairs, s_pair, (const uint32_t*)d_lines, pout == 1 ? d_Pl : (fp12*)nullptr);
+          if (pout == 1) break;
+          pin = pout;
+          std::swap(src, dst);
+          std::swap(sh, dh);
+        }
+      } else {
+        LB_STAGE("level_prod", 0, k_level_prod, 63u, 256u, n_req, n_sets, n_pairs, s_pair, rows, d_req_off,
+                 (const uint32_t*)d_G, (const uint8_t*)d_bad, (const uint32_t*)d_lines, d_Pl);
+      }
       // (mtail: the round program runs the Horner chain over the level products itself, on the
       // Miller loop's squarings of (-g1, S_all): no one-wave k_horner_all)
       if (!mtail) LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
@@ -936,6 +968,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   return run_tails(ctx, sl);
 }
 
+// k_level_part's workgroups per level: one request per thread (a merged call's requests are
+// mostly small), and about two lanes per thread when one large request holds the call
+static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req) {
+  const uint32_t w = n_req > n_sets / 126u ? n_req : n_sets / 126u;
+  const uint32_t b = (w + 255u) / 256u;
+  return b < 1u ? 1u : b > 8u ? 8u : b;
+}
+
 size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
   // (+ the bucket MSM: 2 W keys + 2 W sorted entries and 2 W / T chunk partials per set)
@@ -948,8 +988,13 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
                            8 * 256;
   // (+ the merged check's round-program records, k_lp_mtail)
+  // (+ the level products' partials: 63 x 256 B of k_level_part, an eighth of that for the
+  // first k_level_wc pass, their flags)
+  const size_t lvl_per = (size_t)level_blocks(n_sets, n_req) * 256;
+  const size_t lvl = 63 * (lvl_per + (lvl_per + LB_LVL_GROUP - 1) / LB_LVL_GROUP) * sizeof(fp12) + 2 * 63 * lvl_per +
+                     4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
-         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512;
+         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1201,7 +1246,8 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail,
+                           (const void*)k_lp_rtail, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_decode_sigs, (const void*)k_scalar_pk};
   size_t lane = 0;
   for (const void* k : kernels) {
@@ -1271,6 +1317,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MERGE_MIN")) ctx->merge_min_req = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_MIN")) ctx->lines_min_sets = (uint32_t)atoi(e);
+  if (const char* e = getenv("LB_LEVEL")) ctx->level_wc = atoi(e) != 0;
   if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_RTAIL")) ctx->rtail_lp = atoi(e) != 0;

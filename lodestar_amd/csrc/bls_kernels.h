@@ -280,6 +280,19 @@ __global__ void __launch_bounds__(256, 1) k_level_prod(uint32_t n_req, uint32_t 
                                                        const uint32_t* __restrict__ G,
                                                        const uint8_t* __restrict__ req_bad,
                                                        const uint32_t* __restrict__ lines, fp12* __restrict__ Pl);
+// the level products in two stages (round 6): lane products of each level's share, then
+// wave-cooperative products of groups of LB_LVL_GROUP partials (k_steps.hip)
+static constexpr uint32_t LB_LVL_GROUP = 8;
+__global__ void __launch_bounds__(256, 1) k_level_part(uint32_t n_req, uint32_t n_sets, Rows R,
+                                                       const uint32_t* __restrict__ req_off,
+                                                       const uint32_t* __restrict__ G,
+                                                       const uint8_t* __restrict__ req_bad, uint32_t per,
+                                                       fp12* __restrict__ part, uint8_t* __restrict__ has);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_level_wc(uint32_t per_in, const fp12* __restrict__ in,
+                                                             const uint8_t* __restrict__ in_has, uint32_t per_out,
+                                                             fp12* __restrict__ out, uint8_t* __restrict__ out_has,
+                                                             uint32_t n_pairs, uint32_t s_pair,
+                                                             const uint32_t* __restrict__ lines, fp12* __restrict__ Pl);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_horner_all(const fp12* __restrict__ Pl, fp12* __restrict__ F_all);
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, uint32_t n_sets, Rows R,
                                                              const uint32_t* __restrict__ req_off,

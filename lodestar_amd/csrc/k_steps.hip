@@ -460,6 +460,101 @@ __global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, ui
   }
 }
 
+// The level products in two stages (round 6; LB_LEVEL=0 restores k_level_prod).  k_level_prod's
+// 256 threads per level end in an LDS tree of eight single-lane Fp12 products (~150 us each on
+// one lane): ~11 dependent lane products, 1.7 ms for a 65,536-set call.  Here:
+//   k_level_part, grid (B, 63): thread g of level lvl takes the level's lanes of its share of the
+//     requests (one request per thread; a large request's lanes strided over the level's
+//     per = 256 B threads) -- one or two lane products -- and stores its product, or nothing,
+//     at part[lvl * per + g];
+//   k_level_wc, grid (ceil(per_in / 8), 63), one wave each: the product of a group of 8
+//     partials as wave-cooperative Fp12 products (~10 us each, bls_wc12.h), until one value
+//     per level is left; the last pass (Pl given) multiplies in the merged pair's lines of
+//     the level (s_pair, unless the round program does) and writes P[lvl].
+__global__ void __launch_bounds__(256, 1) k_level_part(uint32_t n_req, uint32_t n_sets, Rows R,
+                                                       const uint32_t* __restrict__ req_off,
+                                                       const uint32_t* __restrict__ G,
+                                                       const uint8_t* __restrict__ req_bad, uint32_t per,
+                                                       fp12* __restrict__ part, uint8_t* __restrict__ has) {
+  const int lvl = blockIdx.y;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= per) return;
+  fp12 acc;
+  bool have = false;
+  auto take = [&](uint32_t q) {
+    fp12 v;
+    g_get(v, G, n_sets, q);
+    if (have) {
+      fp12_mul(acc, acc, v);
+    } else {
+      acc = v;
+      have = true;
+    }
+  };
+  uint32_t r0 = 0;
+  for (; r0 < n_req; r0++) {  // (size-descending: the large requests first)
+    const uint32_t k = R.inv[r0], n = req_off[k + 1] - req_off[k];
+    if (n <= 16u * LB_MILLER_LINES) break;
+    if (req_bad[k]) continue;
+    uint32_t lo, hi;
+    level_lanes(n, lvl, lo, hi);
+    for (uint32_t l = lo + g; l < hi; l += per) take(R.rowoff[l] + r0);
+  }
+  for (uint32_t r = r0 + g; r < n_req; r += per) {
+    const uint32_t k = R.inv[r];
+    if (req_bad[k]) continue;
+    uint32_t lo, hi;
+    level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi);
+    for (uint32_t l = lo; l < hi; l++) take(R.rowoff[l] + r);
+  }
+  const size_t o = (size_t)lvl * per + g;
+  if (have) part[o] = acc;
+  has[o] = have ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_level_wc(uint32_t per_in, const fp12* __restrict__ in,
+                                                             const uint8_t* __restrict__ in_has, uint32_t per_out,
+                                                             fp12* __restrict__ out, uint8_t* __restrict__ out_has,
+                                                             uint32_t n_pairs, uint32_t s_pair,
+                                                             const uint32_t* __restrict__ lines, fp12* __restrict__ Pl) {
+  __shared__ wc_smem S;
+  const int lvl = blockIdx.y;
+  const uint32_t c = blockIdx.x;
+  const uint32_t a = c * LB_LVL_GROUP, b = a + LB_LVL_GROUP < per_in ? a + LB_LVL_GROUP : per_in;
+  wc_init_tables(S);
+  bool have = false;
+#pragma unroll 1
+  for (uint32_t i = a; i < b; i++) {
+    const size_t o = (size_t)lvl * per_in + i;
+    if (!in_has[o]) continue;  // (uniform: one wave per group)
+    wc_load12(S, have ? WC_T0 : WC_ACC, in[o]);
+    if (have) wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_T0);
+    have = true;
+  }
+  if (!Pl) {
+    if (have && threadIdx.x < 12) (&out[(size_t)lvl * per_out + c].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
+    if (threadIdx.x == 0) out_has[(size_t)lvl * per_out + c] = have ? 1 : 0;
+    return;
+  }
+  if (s_pair != 0xffffffffu) {
+    if (!have) wc_set_one(S, WC_ACC);
+    have = true;
+#pragma unroll 1
+    for (int j = c_steps.first[lvl]; j < c_steps.first[lvl + 1]; j++) {
+      if (threadIdx.x < 6) {
+        const uint32_t* p = lines + ((size_t)j * 72 + 12 * threadIdx.x) * n_pairs + s_pair;
+        fp v;
+        for (int w = 0; w < 12; w++) v.l[w] = p[(size_t)w * n_pairs];
+        S.slot[WC_LINE][threadIdx.x] = v;
+      }
+      __syncthreads();
+      wc_apply(S, LB_WC_LINE, WC_ACC, WC_ACC, WC_LINE);
+    }
+  }
+  if (!have) wc_set_one(S, WC_ACC);
+  if (threadIdx.x < 12) (&Pl[lvl].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
+}
+
 // F_all = conj(Horner over the 63 levels of P[lvl]) (x < 0): one wave, wave-
 // cooperative Fp12 (62 squarings + 62 products on the merged check's path).
 __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_horner_all(const fp12* __restrict__ Pl, fp12* __restrict__ F_all) {

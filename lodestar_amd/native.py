@@ -798,7 +798,12 @@ class Device:
         ms = (ctypes.c_float * 32)()
         names = (ctypes.c_char_p * 32)()
         n = self.lib.lb_last_stage_times(self._h, ms, names, 32)
-        return [(names[i].decode(), float(ms[i])) for i in range(min(n, 32))]
+        # a stage launched more than once in a call (level_wc's passes) is reported once, summed
+        out: dict = {}
+        for i in range(min(n, 32)):
+            nm = names[i].decode()
+            out[nm] = out.get(nm, 0.0) + float(ms[i])
+        return list(out.items())
 
 
 def scratch_per_queue(device: int = 0) -> Tuple[int, int]:

@@ -453,6 +453,7 @@ def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
             # (the bucket MSM's merged check runs as the mtail round program, which folds the
             # Horner chain over the level products into its Miller loop: no k_horner_all)
             assert ("horner_all" in stages) == (msm == "0") and ("mtail" in stages) == (msm == "1")
+            assert "level_prod" in stages and "level_wc" in stages  # (the two-stage level products)
             assert "req_horner" in stages  # (skips itself when the check passes)
             assert res.batch_retries == (1 if inject else 0)
         else:
@@ -461,13 +462,16 @@ def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
         dev.close()
 
 
+@pytest.mark.parametrize("level", ["1", "0"])
 @pytest.mark.parametrize("layout", ["mixed", "one_large"])
-def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout):
+def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout, level):
     """Row layout edge cases of the steps organisation: equal-size requests (the
     coalesced C2 shape), one-set requests (a lane runs the whole Miller loop), a
     request larger than 68 sets next to small ones, an empty request; and a
     1,200-set request beside small ones (its lanes of a level spread over all the
-    threads of k_level_prod)."""
+    threads of k_level_part / k_level_prod).  The level products both ways: lane
+    products + wave-cooperative passes (LB_LEVEL=1, default) and k_level_prod's
+    one-lane LDS tree (LB_LEVEL=0)."""
     from oracle import c_oracle as C
     req_off, pks, pk_off, msgs, blob, offs = mixed_workload_cache(device, layout == "mixed")
     n = len(pk_off) - 1
@@ -477,14 +481,15 @@ def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout):
         off.append(min(n, off[-1] + z))
     off[-1] = n
     seed = hashlib.sha256(b"steps-rows").digest()
-    dev = _device_with_env(LB_MILLER="lines")
+    dev = _device_with_env(LB_MILLER="lines", LB_LEVEL=level)
     try:
         ro = np.array(off, np.uint32)
         res = dev.verify_requests(ro, pks, pk_off, msgs, blob, offs, seed)
         valid, err = C.verify_requests(ro, pks, pk_off, msgs, blob, offs, seed, threads=16)
         assert list(res.errors) == list(err)
         assert list(res.valid) == list(valid)
-        assert "step_acc" in dict(dev.last_stage_times())
+        stages = dict(dev.last_stage_times())
+        assert "step_acc" in stages and "level_prod" in stages and ("level_wc" in stages) == (level == "1")
         if layout == "one_large":  # all valid: the merged check itself must pass (no per-request retry)
             assert all(valid) and res.batch_retries == 0
     finally:

@@ -3,7 +3,9 @@
 The library picks the Miller organisation by call size (bls_host.hip run_pipeline):
 the latency path up to lp_max_sets, one wave per pair up to wave_max_sets, one pair per
 lane (k_miller_sets + the one-lane merged tail) below lines_min_sets, the stored lines +
-step-major accumulation + the merged-check round program (mtail) from there.  This probe
+step-major accumulation + the merged-check round program (mtail) from there.  Round 6's
+probe (profiles/r06/orgs_probe_r06f.json, then defaults 8192 / 4096) moved both thresholds
+to 1025 ("lines_msm_from_1k"), so "default" now equals that configuration.  This probe
 times lone synchronous calls of the C5 epoch (valid, and with its 1e-3 injection) and of
 uniform 128-set-request calls of 1.5k ... 8k sets in contexts built with different
 thresholds (LB_LINES_MIN, LB_MSM_MIN) and LB_MTAIL, checking every verdict.
@@ -26,9 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 CONFIGS = {
     "default": {},
-    "lines_from_1k": {"LB_LINES_MIN": "1025"},
-    "lines_msm_from_1k": {"LB_LINES_MIN": "1025", "LB_MSM_MIN": "1025"},
+    "level_prod_one_lane": {"LB_LEVEL": "0"},
     "default_mtail_off": {"LB_MTAIL": "0"},
+    "round5_thresholds": {"LB_LINES_MIN": "8192", "LB_MSM_MIN": "4096"},
 }
 SIZES = (1536, 2048, 3072, 4096, 6144, 8192)
 
