@@ -766,9 +766,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_HIP(hipGetLastError());
     LB_STAGE("msm_chunks", 0, k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks,
              (const uint32_t*)d_off, (const uint32_t*)d_coff, (const uint32_t*)d_msorted, (const g2j*)d_sig, d_mcsum);
-    LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS), TPB, (const uint32_t*)d_coff,
+    LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
              (const g2j*)d_mcsum, d_mbsum);
-    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_mbsum, d_mG);
+    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_mbsum, d_mG);
     if (!mtail) LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
     if (!fold && !mtail)
       LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
@@ -927,7 +927,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Pl, (const g2j*)d_mG, d_mt_in);
       LB_HIP(hipGetLastError());
       if (partial) {  // F_all * Miller(-g1, S_all) back into d_Fall, encoded by k_partial below
-        LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_PARTIAL].off,
+        LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_MTAIL_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_PARTIAL].off,
                     (const uint32_t*)d_mt_in, (uint8_t*)nullptr, d_mt_out);
         hipLaunchKernelGGL(k_records_to_fp12, dim3(1), dim3(64), 0, ts, (const uint32_t*)d_mt_out, d_Fall);
         LB_HIP(hipGetLastError());
@@ -955,7 +955,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       return LB_OK;
     }
     if (mtail)
-      LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_CHECK].off,
+      LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_MTAIL_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_CHECK].off,
                   (const uint32_t*)d_mt_in, d_mflag, (uint32_t*)nullptr);
     else
       LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, merged_lines,
@@ -1248,7 +1248,8 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
                            (const void*)k_lp_rtail, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
-                           (const void*)k_msm_buckets, (const void*)k_decode_sigs, (const void*)k_scalar_pk};
+                           (const void*)k_msm_buckets, (const void*)k_msm_bits, (const void*)k_decode_sigs,
+                           (const void*)k_scalar_pk};
   size_t lane = 0;
   for (const void* k : kernels) {
     hipFuncAttributes a{};
@@ -3001,8 +3002,9 @@ int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw
                    (const uint32_t*)d_off, d_cur, d_sorted);
   LB_LAUNCH(k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks, (const uint32_t*)d_off,
             (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum);
-  LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS), TPB, (const uint32_t*)d_coff, (const g2j*)d_csum, d_bsum);
-  LB_LAUNCH(k_msm_bits, LB_MSM_POS, TPB, (const g2j*)d_bsum, d_G);
+  LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
+            (const g2j*)d_csum, d_bsum);
+  LB_LAUNCH(k_msm_bits, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_bsum, d_G);
   LB_LAUNCH(k_msm_final, 1u, TPB, (const g2j*)d_G, d_S);
   LB_LAUNCH(k_g2a_serialize, 1u, TPB, 1u, (const g2a*)d_S, d_out);
   LB_HIP(hipMemcpyAsync(out192, d_out, 192, hipMemcpyDeviceToHost, ctx->stream));
@@ -3058,6 +3060,11 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
                       float* out_ms, uint64_t* stamps) {
   if (!ctx || n == 0 || !in16 || !out16) return LB_ERR_INVALID_ARGUMENT;
   if (!prog_words && prog >= LB_LP_NPROGS) return LB_ERR_INVALID_ARGUMENT;
+  // (the merged-check programs are compiled for k_lp_mtail's LB_LP_MTAIL_ROWS rows, more than
+  // k_lp_program's workgroup runs)
+  if (!prog_words && LB_LP_MTAIL_ROWS > LB_LP_ROWS &&
+      (prog == LB_LP_PROG_MTAIL_CHECK || prog == LB_LP_PROG_MTAIL_PARTIAL))
+    return LB_ERR_INVALID_ARGUMENT;
   if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500004u)) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   LB_TRY(helper_slot(ctx));

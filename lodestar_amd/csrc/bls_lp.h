@@ -103,7 +103,10 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCal
 // The throughput pipeline's merged check as a round program (one workgroup): in16 =
 // LB_MTAIL_NIN records (k_mtail_prep); mflag (check program): [0] = final_exp == 1;
 // out16 (partial program): the shard's partial, 12 records in the one-lane form.
-__global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restrict__ prog,
+#ifndef LB_LP_MTAIL_ROWS
+#define LB_LP_MTAIL_ROWS 64  // (bls_lp_progs.h: the rows gen_lp.py compiled the merged-check programs for)
+#endif
+__global__ void __launch_bounds__(LB_LP_MTAIL_ROWS * 16) k_lp_mtail(const uint32_t* __restrict__ prog,
                                                         const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
                                                         uint32_t* __restrict__ out16);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]

@@ -34,6 +34,8 @@
 #include "bls_lp_progs.h"
 #endif
 
+static_assert(LB_LP_MTAIL_ROWS == LB_LP_MTAIL_ROWS_GEN, "k_lp_mtail's rows == the merged-check programs' (gen_lp.py)");
+
 namespace lb {
 
 using namespace co;
@@ -469,24 +471,26 @@ LB_DEV void lp_run(SH& S, const uint32_t* __restrict__ prog, const uint32_t* __r
                    const uint32_t* __restrict__ in_b, const uint32_t* __restrict__ in_flags,
                    uint32_t* __restrict__ out, uint32_t* __restrict__ out_flags,
                    unsigned long long* __restrict__ stamps = nullptr) {
-  const uint32_t tid = threadIdx.x, lane = tid & 15u, row = tid >> 4;
+  // (rows = the workgroup's: 32 for the verification programs, LB_LP_MTAIL_ROWS for k_lp_mtail's;
+  // a program never schedules more units in a round than the rows it was compiled for)
+  const uint32_t tid = threadIdx.x, lane = tid & 15u, row = tid >> 4, tpb = blockDim.x, rows = tpb >> 4;
   const uint32_t pj = p_limb();
   const uint32_t n_rounds = prog[1], n_const = prog[4], n_in = prog[5], n_inflag = prog[6], n_out = prog[7],
                  n_outflag = prog[8];
   Stream st;
   st.sw = prog[9];
   uint32_t pos = LB_LP_HDR;
-  for (uint32_t i = row; i < n_const; i += LB_LP_ROWS) {
+  for (uint32_t i = row; i < n_const; i += rows) {
     const uint32_t* c = prog + pos + 14 * i;
     S.reg[c[0] * 16u + lane] = lane < 13 ? c[1 + lane] : 0u;
   }
   pos += 14 * n_const;
-  for (uint32_t i = row; i < n_in; i += LB_LP_ROWS) {
+  for (uint32_t i = row; i < n_in; i += rows) {
     const uint32_t* src = i < split ? in_a + 16 * i : in_b + 16 * (i - split);
     S.reg[prog[pos + i] * 16u + lane] = lane < 13 ? src[lane] : 0u;
   }
   pos += n_in;
-  for (uint32_t i = tid; i < n_inflag; i += LB_LP_TPB) S.flag[prog[pos + i]] = in_flags[i] ? 1u : 0u;
+  for (uint32_t i = tid; i < n_inflag; i += tpb) S.flag[prog[pos + i]] = in_flags[i] ? 1u : 0u;
   pos += n_inflag;
   const uint32_t* outs = prog + pos;
   pos += n_out;
@@ -510,7 +514,7 @@ LB_DEV void lp_run(SH& S, const uint32_t* __restrict__ prog, const uint32_t* __r
   }
 #else
   st.done = st.issued = min(st.sw, (uint32_t)(LB_LP_RING - LB_LP_CHUNK));
-  for (uint32_t i = tid; i < st.done; i += LB_LP_TPB) S.ring[i] = st.sp[i];
+  for (uint32_t i = tid; i < st.done; i += tpb) S.ring[i] = st.sp[i];
   __syncthreads();
   if (st.sw) {
     const uint4 h = *reinterpret_cast<const uint4*>(S.ring);
@@ -524,8 +528,8 @@ LB_DEV void lp_run(SH& S, const uint32_t* __restrict__ prog, const uint32_t* __r
   // instruction cache is 64 KB)
 #pragma unroll 1
   for (uint32_t r = 0; r < n_rounds; r++) lp_round(S, st, d, bw, nu, pf, tid, lane, row, pj, stamps, r);
-  for (uint32_t i = row; i < n_out; i += LB_LP_ROWS) out[16 * i + lane] = lane < 13 ? S.reg[outs[i] * 16u + lane] : 0u;
-  for (uint32_t i = tid; i < n_outflag; i += LB_LP_TPB) out_flags[i] = S.flag[outfl[i]];
+  for (uint32_t i = row; i < n_out; i += rows) out[16 * i + lane] = lane < 13 ? S.reg[outs[i] * 16u + lane] : 0u;
+  for (uint32_t i = tid; i < n_outflag; i += tpb) out_flags[i] = S.flag[outfl[i]];
 }
 
 // ---------------------------------------------------------------------------
@@ -781,7 +785,7 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCal
 // Horner value of the call's level products, final exponentiation -- ~880 rounds on one
 // workgroup instead of the one-lane msm_final (1.5 ms) + lines of S_all (3.4 ms) + the
 // one-wave final exponentiation (3.1 ms) on every call's serial tail.
-__global__ void __launch_bounds__(LB_LP_TPB) k_lp_mtail(const uint32_t* __restrict__ prog,
+__global__ void __launch_bounds__(LB_LP_MTAIL_ROWS * 16) k_lp_mtail(const uint32_t* __restrict__ prog,
                                                         const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
                                                         uint32_t* __restrict__ out16) {
   __shared__ LpSharedMtail S;

@@ -19,10 +19,10 @@
 //   k_msm_scatter  one lane per (point, window): counting-sort placement
 //   k_msm_chunks   one lane per chunk of <= T entries of ONE bucket: mixed
 //                  (Jacobian + affine) additions, the bulk of the work
-//   k_msm_buckets  one lane per bucket: sum of its chunk partials
-//   k_msm_bits     one wave per bit position p = 11 w + k: G_p = sum of the
-//                  buckets d of window w with bit k of d set (strided lane
-//                  sums, then an LDS tree)
+//   k_msm_buckets  four lanes per bucket: sum of its chunk partials
+//   k_msm_bits     256 threads per bit position p = 11 w + k: G_p = sum of the
+//                  buckets d of window w with bit k of d set (two per thread,
+//                  then an LDS tree)
 //   k_msm_final    one wave: lane p doubles G_p p times, LDS tree, affine
 // so sum_w 2^(11w) sum_d d B_(w,d) = sum_p 2^p G_p with no serial running sum
 // over the 1024 buckets (critical path: T madds + ~8 adds + 13 adds + 32 dbl).
@@ -206,45 +206,74 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_ch
   csum[c] = acc;
 }
 
-// One lane per bucket: B_b = sum of its chunk partials (infinity when empty).
+// B_b = sum of bucket b's chunk partials (infinity when empty): LB_MSM_BLANES lanes per bucket
+// (round 6: a C2 bucket holds ~8 chunks, which one lane added in 7 dependent Jacobian additions
+// of ~75 us each; 4 lanes take two chunks each and a 2-level LDS tree joins them: 3)
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t* __restrict__ coff,
                                                                   const g2j* __restrict__ csum, g2j* __restrict__ bsum) {
-  const uint32_t bk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bk >= LB_MSM_BUCKETS) return;
-  const uint32_t c0 = coff[bk], c1 = coff[bk + 1];
+  __shared__ LdsRec<g2j> sh[TPB];
+  static_assert(TPB % LB_MSM_BLANES == 0, "a bucket's lanes in one workgroup");
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t bk = t / LB_MSM_BLANES, sub = t % LB_MSM_BLANES;
   g2j acc;
   jac_set_inf(acc);
-  if (c1 > c0) {
-    acc = csum[c0];
+  if (bk < LB_MSM_BUCKETS) {
+    const uint32_t c0 = coff[bk], c1 = coff[bk + 1];
+    bool have = false;
 #pragma unroll 1
-    for (uint32_t c = c0 + 1; c < c1; c++) {
-      g2j t = csum[c];
-      jac_add(acc, acc, t);
+    for (uint32_t c = c0 + sub; c < c1; c += LB_MSM_BLANES) {
+      g2j v = csum[c];
+      if (have) {
+        jac_add(acc, acc, v);
+      } else {
+        acc = v;
+        have = true;
+      }
     }
   }
-  bsum[bk] = acc;
+  sh[threadIdx.x].v = acc;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t s = LB_MSM_BLANES / 2; s > 0; s >>= 1) {
+    if (sub < s) {
+      g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
+      jac_add(m, m, o);
+      sh[threadIdx.x].v = m;
+    }
+    __syncthreads();
+  }
+  if (sub == 0 && bk < LB_MSM_BUCKETS) bsum[bk] = sh[threadIdx.x].v;
 }
 
-// One wave per bit position p = 11 w + k: G_p = sum of the buckets d of
-// window w whose bit k is set (512 of them for k < 10, only d = 1024 for k = 10).
-__global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G) {
-  __shared__ LdsRec<g2j> sh[TPB];
+// One workgroup of LB_MSM_BITS_TPB threads per bit position p = 11 w + k: G_p = sum of the
+// buckets d of window w whose bit k is set (512 of them for k < 10, only d = 1024 for k = 10):
+// two buckets per thread, then an LDS tree (round 6: 256 threads, 9 dependent additions
+// instead of one wave's 8 + 6)
+__global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G) {
+  __shared__ LdsRec<g2j> sh[LB_MSM_BITS_TPB];
   const uint32_t p = blockIdx.x;
   if (p >= LB_MSM_POS) return;
   const uint32_t w = p / LB_MSM_C, k = p % LB_MSM_C;
   const uint32_t n = k < LB_MSM_C - 1 ? LB_MSM_NB / 2 : 1u;
   g2j acc;
   jac_set_inf(acc);
+  bool have = false;
 #pragma unroll 1
-  for (uint32_t m = threadIdx.x; m < n; m += TPB) {
+  for (uint32_t m = threadIdx.x; m < n; m += LB_MSM_BITS_TPB) {
     const uint32_t low = m & ((1u << k) - 1u), high = m >> k;
     const uint32_t d = (high << (k + 1)) | (1u << k) | low;  // 1 <= d <= 1024, bit k set
     g2j t = bsum[w * LB_MSM_NB + d - 1];
-    jac_add(acc, acc, t);
+    if (have) {
+      jac_add(acc, acc, t);
+    } else {
+      acc = t;
+      have = true;
+    }
   }
   sh[threadIdx.x].v = acc;
   __syncthreads();
-  for (uint32_t s = TPB / 2; s > 0; s >>= 1) {
+#pragma unroll 1
+  for (uint32_t s = LB_MSM_BITS_TPB / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
       g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
