@@ -311,7 +311,12 @@ struct lb_ctx {
   uint32_t msm_min_sets = 1025;
   // merged steps calls: the level products as lane products + wave-cooperative passes
   // (k_level_part / k_level_wc) instead of k_level_prod's one-lane LDS tree (LB_LEVEL=0)
-  bool level_wc = true;  // (same probe: from 1025 sets the MSM beats the ladders)
+  bool level_wc = true;
+  // lone calls: the MSM's bucket sums on LB_MSM_BLANES lanes per bucket and its bit sums on 256
+  // threads (LB_MSM_LANES=0: one lane per bucket and one wave per bit, round 5, always), the
+  // merged-check program on 64 rows (LB_WIDE_TAIL=0: 32 rows always)
+  bool msm_lanes = true;
+  bool wide_tail = true;  // (same probe: from 1025 sets the MSM beats the ladders)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -633,6 +638,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // merged check as a round program (k_lp_mtail): S_all, its Miller value and the final
   // exponentiation from the MSM's bit sums and the 63 level products (their Horner chain folded in)
   const bool mtail = steps && use_msm && merged && ctx->mtail_lp;
+  // a lone call's serial tail in its wide forms (the GPU otherwise idle: latency is what counts):
+  // the merged-check program on LB_LP_MTAIL_ROWS rows, the MSM's sums over more lanes.  With other
+  // calls in flight the narrow forms, whose smaller workgroups wait for less of a CU (C2 3.62 vs
+  // 3.67 / 3.68 M sets/s with either wide form in every call, profiles/r06/ab_r06k/)
+  const bool mt_wide = lone && ctx->wide_tail;
+  const uint32_t mt_tpb = mt_wide ? LB_LP_MTAIL_ROWS * 16u : (uint32_t)LB_LP_TPB;
+  const bool msm_wide = lone && ctx->msm_lanes;
   if (mtail) LB_TRY(lp_ensure(ctx));
   // (steps + merged: the merged pair's lines come from a one-lane kernel before the
   // accumulation; as an extra workgroup of k_step_acc they measured 4.8 -> 8.2 ms: the
@@ -766,9 +778,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_HIP(hipGetLastError());
     LB_STAGE("msm_chunks", 0, k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks,
              (const uint32_t*)d_off, (const uint32_t*)d_coff, (const uint32_t*)d_msorted, (const g2j*)d_sig, d_mcsum);
-    LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
-             (const g2j*)d_mcsum, d_mbsum);
-    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_mbsum, d_mG);
+    const uint32_t bl = msm_wide ? LB_MSM_BLANES : 1u;
+    LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS * bl), TPB, (const uint32_t*)d_coff,
+             (const g2j*)d_mcsum, d_mbsum, bl);
+    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, msm_wide ? LB_MSM_BITS_TPB : (uint32_t)TPB, (const g2j*)d_mbsum, d_mG);
     if (!mtail) LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
     if (!fold && !mtail)
       LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
@@ -927,7 +940,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Pl, (const g2j*)d_mG, d_mt_in);
       LB_HIP(hipGetLastError());
       if (partial) {  // F_all * Miller(-g1, S_all) back into d_Fall, encoded by k_partial below
-        LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_MTAIL_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_PARTIAL].off,
+        LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, mt_tpb, ctx->d_lp + LB_LP_PROGS[mt_wide ? LB_LP_PROG_MTAIL_PARTIAL_WIDE : LB_LP_PROG_MTAIL_PARTIAL].off,
                     (const uint32_t*)d_mt_in, (uint8_t*)nullptr, d_mt_out);
         hipLaunchKernelGGL(k_records_to_fp12, dim3(1), dim3(64), 0, ts, (const uint32_t*)d_mt_out, d_Fall);
         LB_HIP(hipGetLastError());
@@ -955,7 +968,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       return LB_OK;
     }
     if (mtail)
-      LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, LB_LP_MTAIL_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MTAIL_CHECK].off,
+      LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, mt_tpb, ctx->d_lp + LB_LP_PROGS[mt_wide ? LB_LP_PROG_MTAIL_CHECK_WIDE : LB_LP_PROG_MTAIL_CHECK].off,
                   (const uint32_t*)d_mt_in, d_mflag, (uint32_t*)nullptr);
     else
       LB_STAGE_ON("tail_all", ts, k_tail, 1u, TPB, 1u, n_pairs, n_sets + n_req, merged_lines,
@@ -1319,6 +1332,8 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MSM_MIN")) ctx->msm_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LINES_MIN")) ctx->lines_min_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_LEVEL")) ctx->level_wc = atoi(e) != 0;
+  if (const char* e = getenv("LB_MSM_LANES")) ctx->msm_lanes = atoi(e) != 0;
+  if (const char* e = getenv("LB_WIDE_TAIL")) ctx->wide_tail = atoi(e) != 0;
   if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_RTAIL")) ctx->rtail_lp = atoi(e) != 0;
@@ -3003,7 +3018,7 @@ int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw
   LB_LAUNCH(k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks, (const uint32_t*)d_off,
             (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum);
   LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
-            (const g2j*)d_csum, d_bsum);
+            (const g2j*)d_csum, d_bsum, LB_MSM_BLANES);
   LB_LAUNCH(k_msm_bits, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_bsum, d_G);
   LB_LAUNCH(k_msm_final, 1u, TPB, (const g2j*)d_G, d_S);
   LB_LAUNCH(k_g2a_serialize, 1u, TPB, 1u, (const g2a*)d_S, d_out);
@@ -3060,10 +3075,10 @@ int lb_lp_program_run(lb_ctx* ctx, uint32_t prog, const uint32_t* prog_words, si
                       float* out_ms, uint64_t* stamps) {
   if (!ctx || n == 0 || !in16 || !out16) return LB_ERR_INVALID_ARGUMENT;
   if (!prog_words && prog >= LB_LP_NPROGS) return LB_ERR_INVALID_ARGUMENT;
-  // (the merged-check programs are compiled for k_lp_mtail's LB_LP_MTAIL_ROWS rows, more than
-  // k_lp_program's workgroup runs)
+  // (the wide merged-check programs are compiled for k_lp_mtail's LB_LP_MTAIL_ROWS rows, more
+  // than k_lp_program's workgroup runs)
   if (!prog_words && LB_LP_MTAIL_ROWS > LB_LP_ROWS &&
-      (prog == LB_LP_PROG_MTAIL_CHECK || prog == LB_LP_PROG_MTAIL_PARTIAL))
+      (prog == LB_LP_PROG_MTAIL_CHECK_WIDE || prog == LB_LP_PROG_MTAIL_PARTIAL_WIDE))
     return LB_ERR_INVALID_ARGUMENT;
   if (prog_words && (n_words < LB_LP_HDR || prog_words[0] != 0x4C500004u)) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));

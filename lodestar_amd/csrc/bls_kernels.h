@@ -250,7 +250,8 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_ch
                                                                  const uint32_t* __restrict__ sorted,
                                                                  const g2j* __restrict__ sig, g2j* __restrict__ csum);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t* __restrict__ coff,
-                                                                  const g2j* __restrict__ csum, g2j* __restrict__ bsum);
+                                                                  const g2j* __restrict__ csum, g2j* __restrict__ bsum,
+                                                                  uint32_t lanes);
 static constexpr uint32_t LB_MSM_BLANES = 4;      // k_msm_buckets: lanes per bucket
 static constexpr uint32_t LB_MSM_BITS_TPB = 256;  // k_msm_bits: threads per bit position
 __global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G);

@@ -50,7 +50,9 @@
 #define LB_LP_PROG_MTAIL_PARTIAL 5  // ... its two-phase form: the shard's partial
 #define LB_LP_PROG_FINAL_LANE 6     // final exponentiation == 1 of a one-lane Fp12 (lb_gt_check)
 #define LB_LP_PROG_RTAIL 7          // one request's tail after a failed merged check (k_lp_rtail)
-#define LB_LP_NPROGS 8
+#define LB_LP_PROG_MTAIL_CHECK_WIDE 8    // the merged-check programs compiled for LB_LP_MTAIL_ROWS rows
+#define LB_LP_PROG_MTAIL_PARTIAL_WIDE 9  // (a lone call's k_lp_mtail: 1,024 threads)
+#define LB_LP_NPROGS 10
 #define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf
 #define LB_LP_RTAIL_REGS 512            // (its program holds ~240 registers: 32 KB of LDS)
 #define LB_MTAIL_LEVELS 63                  // the step-major accumulation's Horner levels (k_steps.hip)
@@ -104,7 +106,7 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCal
 // LB_MTAIL_NIN records (k_mtail_prep); mflag (check program): [0] = final_exp == 1;
 // out16 (partial program): the shard's partial, 12 records in the one-lane form.
 #ifndef LB_LP_MTAIL_ROWS
-#define LB_LP_MTAIL_ROWS 64  // (bls_lp_progs.h: the rows gen_lp.py compiled the merged-check programs for)
+#define LB_LP_MTAIL_ROWS 64  // (bls_lp_progs.h: the rows gen_lp.py compiled the wide merged-check programs for)
 #endif
 __global__ void __launch_bounds__(LB_LP_MTAIL_ROWS * 16) k_lp_mtail(const uint32_t* __restrict__ prog,
                                                         const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,

@@ -209,19 +209,21 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_ch
 // B_b = sum of bucket b's chunk partials (infinity when empty): LB_MSM_BLANES lanes per bucket
 // (round 6: a C2 bucket holds ~8 chunks, which one lane added in 7 dependent Jacobian additions
 // of ~75 us each; 4 lanes take two chunks each and a 2-level LDS tree joins them: 3)
+// (lanes: LB_MSM_BLANES, or 1 -- one lane per bucket, round 5 -- with LB_MSM_LANES=0)
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t* __restrict__ coff,
-                                                                  const g2j* __restrict__ csum, g2j* __restrict__ bsum) {
+                                                                  const g2j* __restrict__ csum, g2j* __restrict__ bsum,
+                                                                  uint32_t lanes) {
   __shared__ LdsRec<g2j> sh[TPB];
   static_assert(TPB % LB_MSM_BLANES == 0, "a bucket's lanes in one workgroup");
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t bk = t / LB_MSM_BLANES, sub = t % LB_MSM_BLANES;
+  const uint32_t bk = t / lanes, sub = t % lanes;
   g2j acc;
   jac_set_inf(acc);
   if (bk < LB_MSM_BUCKETS) {
     const uint32_t c0 = coff[bk], c1 = coff[bk + 1];
     bool have = false;
 #pragma unroll 1
-    for (uint32_t c = c0 + sub; c < c1; c += LB_MSM_BLANES) {
+    for (uint32_t c = c0 + sub; c < c1; c += lanes) {
       g2j v = csum[c];
       if (have) {
         jac_add(acc, acc, v);
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t
   sh[threadIdx.x].v = acc;
   __syncthreads();
 #pragma unroll 1
-  for (uint32_t s = LB_MSM_BLANES / 2; s > 0; s >>= 1) {
+  for (uint32_t s = lanes / 2; s > 0; s >>= 1) {
     if (sub < s) {
       g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
@@ -259,7 +261,7 @@ __global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __re
   jac_set_inf(acc);
   bool have = false;
 #pragma unroll 1
-  for (uint32_t m = threadIdx.x; m < n; m += LB_MSM_BITS_TPB) {
+  for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) {  // (blockDim: 256, or 64 with LB_MSM_LANES=0)
     const uint32_t low = m & ((1u << k) - 1u), high = m >> k;
     const uint32_t d = (high << (k + 1)) | (1u << k) | low;  // 1 <= d <= 1024, bit k set
     g2j t = bsum[w * LB_MSM_NB + d - 1];
@@ -273,7 +275,7 @@ __global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __re
   sh[threadIdx.x].v = acc;
   __syncthreads();
 #pragma unroll 1
-  for (uint32_t s = LB_MSM_BITS_TPB / 2; s > 0; s >>= 1) {
+  for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
       g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);

@@ -368,9 +368,10 @@ def _device_with_env(**env):
                 os.environ[k] = v
 
 
+@pytest.mark.parametrize("wide", ["1", "0"])
 @pytest.mark.parametrize("mtail", ["1", "0"])
 @pytest.mark.parametrize("inject", [True, False])
-def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail):
+def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail, wide):
     """The merged check's sum of r_i sig_i from the bucket MSM (k_msm.hip), forced
     onto this 1,500-set call (LB_MSM_MIN=1; by default calls of >= 1025 sets):
     with injected failures the merged check fails and the per-request tails take
@@ -378,11 +379,13 @@ def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail):
     MSM's sum alone.  The merged check itself runs as the round program (LB_MTAIL=1,
     k_lp_mtail: S_all from the MSM's bit sums, its Miller value, the final
     exponentiation) or as the one-lane / one-wave chain (msm_final, lines of S_all,
-    k_tail).  Verdicts and rejection codes == the C oracle's."""
+    k_tail).  A lone call's wide forms (the merged check on 64 rows, the MSM's sums over
+    more lanes) and the narrow ones of calls sharing the GPU (LB_WIDE_TAIL=0,
+    LB_MSM_LANES=0).  Verdicts and rejection codes == the C oracle's."""
     from oracle import c_oracle as C
     args = mixed_workload_cache(device, inject)
     seed = hashlib.sha256(b"msm-seed").digest()
-    dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail)
+    dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail, LB_WIDE_TAIL=wide, LB_MSM_LANES=wide)
     try:
         res = dev.verify_requests(*args, seed)
         stages = dict(dev.last_stage_times())

@@ -24,7 +24,8 @@ STAGE_OF = {  # pipeline stage (bench.py stage_ms key) -> kernel base name
     "miller_wave": "k_pair_wc", "pubkeys_agg": "k_pubkeys_agg",
     "msm_digits": "k_msm_scalars", "msm_chunks": "k_msm_chunks", "msm_buckets": "k_msm_buckets",
     "msm_bits": "k_msm_bits", "msm_final": "k_msm_final", "msm_scatter": "k_msm_scatter",
-    "step_acc": "k_step_acc", "level_prod": "k_level_prod", "horner_all": "k_horner_all",
+    "step_acc": "k_step_acc", "level_prod": ("k_level_part", "k_level_prod"), "level_wc": "k_level_wc",
+    "horner_all": "k_horner_all",
     "req_status": "k_req_status", "req_horner": "k_req_horner", "lines_all": "k_lines_S",
     "mtail": "k_lp_mtail", "rtail": "k_lp_rtail",
 }
