@@ -308,7 +308,7 @@ struct lb_ctx {
   uint32_t merge_min_req = 8;
   // merged calls of at least msm_min_sets sets take S_all from the bucket MSM
   // (k_msm.hip) instead of per-set ladders (LB_MSM_MIN, 0 = never)
-  uint32_t msm_min_sets = 1025;
+  uint32_t msm_min_sets = 1025;  // (same probe: from 1025 sets the MSM beats the ladders)
   // merged steps calls: the level products as lane products + wave-cooperative passes
   // (k_level_part / k_level_wc) instead of k_level_prod's one-lane LDS tree (LB_LEVEL=0)
   bool level_wc = true;
@@ -316,7 +316,8 @@ struct lb_ctx {
   // threads (LB_MSM_LANES=0: one lane per bucket and one wave per bit, round 5, always), the
   // merged-check program on 64 rows (LB_WIDE_TAIL=0: 32 rows always)
   bool msm_lanes = true;
-  bool wide_tail = true;  // (same probe: from 1025 sets the MSM beats the ladders)
+  bool wide_tail = true;
+  bool msm_bits_lp = true;  // (LB_MSM_BITS_LP=0: a lone call's bit sums by k_msm_bits' 256 threads)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -645,6 +646,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   const bool mt_wide = lone && ctx->wide_tail;
   const uint32_t mt_tpb = mt_wide ? LB_LP_MTAIL_ROWS * 16u : (uint32_t)LB_LP_TPB;
   const bool msm_wide = lone && ctx->msm_lanes;
+  // (and its bit sums as round programs: 9 dependent one-lane additions -> 3 launches of ~10-16 rounds)
+  const bool bits_lp = msm_wide && mtail && ctx->msm_bits_lp;
   if (mtail) LB_TRY(lp_ensure(ctx));
   // (steps + merged: the merged pair's lines come from a one-lane kernel before the
   // accumulation; as an extra workgroup of k_step_acc they measured 4.8 -> 8.2 ms: the
@@ -695,6 +698,9 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint8_t* d_lhB = level_wc ? ws.take<uint8_t>(63 * (size_t)lvl_per) : nullptr;
   uint32_t* d_mt_in = mtail ? ws.take<uint32_t>((size_t)LB_MTAIL_NIN * 16) : nullptr;
   uint32_t* d_mt_out = mtail && partial ? ws.take<uint32_t>(12 * 16) : nullptr;
+  uint32_t* d_mb_in0 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST * LB_MSM_BITS_GROUP * 6 * 16) : nullptr;
+  uint32_t* d_mb_in1 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST * 6 * 16) : nullptr;
+  uint32_t* d_mb_in2 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST / 8 * 6 * 16) : nullptr;
   const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta};
   sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
@@ -781,7 +787,23 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     const uint32_t bl = msm_wide ? LB_MSM_BLANES : 1u;
     LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS * bl), TPB, (const uint32_t*)d_coff,
              (const g2j*)d_mcsum, d_mbsum, bl);
-    LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, msm_wide ? LB_MSM_BITS_TPB : (uint32_t)TPB, (const g2j*)d_mbsum, d_mG);
+    if (bits_lp) {
+      // (a lone call's bit sums as three levels of round programs, 8:1 each; the last writes the
+      // 33 G_p into the merged-check program's input records, so k_mtail_prep skips them)
+      LB_STAGE("msm_bits", 0, k_msm_bits_prep, blocks_for(LB_MSM_BITS_INST * LB_MSM_BITS_GROUP * 6u, 256), 256u,
+               (const g2j*)d_mbsum, d_mb_in0);
+      constexpr uint32_t NI = LB_MSM_BITS_GROUP * 6u;
+      LB_STAGE("msm_bits", 0, k_lp_msm_bits, LB_MSM_BITS_INST, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MSM_BITS0].off,
+               (uint32_t)LB_MSM_BITS_INST, NI, 6u, (const uint32_t*)d_mb_in0, d_mb_in1);
+      LB_STAGE("msm_bits", 0, k_lp_msm_bits, LB_MSM_BITS_INST / 8u, LB_LP_TPB,
+               ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MSM_BITS1].off, (uint32_t)LB_MSM_BITS_INST / 8u, NI, 6u,
+               (const uint32_t*)d_mb_in1, d_mb_in2);
+      LB_STAGE("msm_bits", 0, k_lp_msm_bits, LB_MSM_POS, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MSM_BITS2].off,
+               (uint32_t)LB_MSM_POS, NI, 6u, (const uint32_t*)d_mb_in2, d_mt_in + (size_t)12 * LB_MTAIL_LEVELS * 16);
+    } else {
+      LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, msm_wide ? LB_MSM_BITS_TPB : (uint32_t)TPB, (const g2j*)d_mbsum,
+               d_mG);
+    }
     if (!mtail) LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
     if (!fold && !mtail)
       LB_STAGE("lines_all", 0, k_lines_S, 1u, TPB, 1u, n_pairs, n_sets + n_req, (const g2a*)d_Sall, d_lines,
@@ -937,7 +959,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     }
     const uint32_t* merged_lines = (fold || steps) ? nullptr : (const uint32_t*)d_lines;
     if (mtail) {
-      hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Pl, (const g2j*)d_mG, d_mt_in);
+      hipLaunchKernelGGL(k_mtail_prep, dim3(1), dim3(256), 0, ts, (const fp12*)d_Pl,
+                         bits_lp ? (const g2j*)nullptr : (const g2j*)d_mG, d_mt_in);
       LB_HIP(hipGetLastError());
       if (partial) {  // F_all * Miller(-g1, S_all) back into d_Fall, encoded by k_partial below
         LB_STAGE_ON("mtail", ts, k_lp_mtail, 1u, mt_tpb, ctx->d_lp + LB_LP_PROGS[mt_wide ? LB_LP_PROG_MTAIL_PARTIAL_WIDE : LB_LP_PROG_MTAIL_PARTIAL].off,
@@ -998,8 +1021,9 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
   size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
                    (size_t)LB_RTAIL_NIN * 64 + 4 + 2 * 256 / 64;  // (+ k_lp_rtail's records and flag)
+  // (+ a lone call's bit-sum program records: 8 + 1 + 1/8 points of 6 records per level-0 instance)
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
-                           8 * 256;
+                           8 * 256 + (size_t)LB_MSM_BITS_INST * (LB_MSM_BITS_GROUP + 1 + 1) * 6 * 64 + 3 * 256;
   // (+ the merged check's round-program records, k_lp_mtail)
   // (+ the level products' partials: 63 x 256 B of k_level_part, an eighth of that for the
   // first k_level_wc pass, their flags)
@@ -1259,7 +1283,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_msm_bits, (const void*)k_decode_sigs,
                            (const void*)k_scalar_pk};
@@ -1334,6 +1358,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LEVEL")) ctx->level_wc = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_LANES")) ctx->msm_lanes = atoi(e) != 0;
   if (const char* e = getenv("LB_WIDE_TAIL")) ctx->wide_tail = atoi(e) != 0;
+  if (const char* e = getenv("LB_MSM_BITS_LP")) ctx->msm_bits_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_RTAIL")) ctx->rtail_lp = atoi(e) != 0;

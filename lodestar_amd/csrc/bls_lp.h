@@ -52,7 +52,12 @@
 #define LB_LP_PROG_RTAIL 7          // one request's tail after a failed merged check (k_lp_rtail)
 #define LB_LP_PROG_MTAIL_CHECK_WIDE 8    // the merged-check programs compiled for LB_LP_MTAIL_ROWS rows
 #define LB_LP_PROG_MTAIL_PARTIAL_WIDE 9  // (a lone call's k_lp_mtail: 1,024 threads)
-#define LB_LP_NPROGS 10
+#define LB_LP_PROG_MSM_BITS0 10  // a lone call's MSM bit sums: 8 one-lane Jacobian points -> their sum
+#define LB_LP_PROG_MSM_BITS1 11  // ... 8 partial sums -> one
+#define LB_LP_PROG_MSM_BITS2 12  // ... 8 partial sums -> G_p, one-lane Jacobian (k_lp_msm_bits)
+#define LB_LP_NPROGS 13
+#define LB_MSM_BITS_GROUP 8      // lpgen/bls.py MSM_BITS_GROUP
+#define LB_MSM_BITS_INST (LB_MSM_POS * (LB_MSM_NB / 2 / LB_MSM_BITS_GROUP))  // level-0 instances: 33 x 64
 #define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf
 #define LB_LP_RTAIL_REGS 512            // (its program holds ~240 registers: 32 KB of LDS)
 #define LB_MTAIL_LEVELS 63                  // the step-major accumulation's Horner levels (k_steps.hip)
@@ -111,6 +116,17 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_verify(LpCal
 __global__ void __launch_bounds__(LB_LP_MTAIL_ROWS * 16) k_lp_mtail(const uint32_t* __restrict__ prog,
                                                         const uint32_t* __restrict__ in16, uint8_t* __restrict__ mflag,
                                                         uint32_t* __restrict__ out16);
+// A lone call's MSM bit sums as three levels of round programs (bls_host.hip): the bucket sums
+// gathered into level-0 records (8 per instance, 64 instances per bit position; infinity where a
+// position has fewer buckets), then instance b of a level runs `prog` on in16 + b * n_in * 16 and
+// writes out16 + b * n_out * 16 (level 2: the 33 G_p straight into the merged-check program's
+// input records)
+__global__ void __launch_bounds__(256) k_msm_bits_prep(const g2j* __restrict__ bsum, uint32_t* __restrict__ in16);
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_msm_bits(const uint32_t* __restrict__ prog,
+                                                                             uint32_t n, uint32_t n_in,
+                                                                             uint32_t n_out,
+                                                                             const uint32_t* __restrict__ in16,
+                                                                             uint32_t* __restrict__ out16);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,

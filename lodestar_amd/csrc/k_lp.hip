@@ -820,6 +820,7 @@ __global__ void __launch_bounds__(256) k_mtail_prep(const fp12* __restrict__ Pl,
       fp_set(k, LB_LP_R416_RAW);
       fp_mul(v, (&Pl[i / 12].c0.c0.c0)[i % 12], k);
     } else {
+      if (!G) break;  // (the G_p records already written by the lone call's bit-sum programs)
       v = (&G[(i - NP) / 6].X.c0)[(i - NP) % 6];
     }
 #pragma unroll
@@ -863,6 +864,40 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_rtail(const 
   lp_run(S, prog, in, 0xffffffffu, in, inflag + k, nullptr, s_fl);
   __syncthreads();
   if (threadIdx.x == 0) valid[k] = s_fl[0] ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256) k_msm_bits_prep(const g2j* __restrict__ bsum, uint32_t* __restrict__ in16) {
+  constexpr uint32_t PER_POS = LB_MSM_NB / 2 / LB_MSM_BITS_GROUP;  // instances per bit position
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;        // (instance, point, coordinate)
+  if (t >= (uint32_t)LB_MSM_BITS_INST * LB_MSM_BITS_GROUP * 6u) return;
+  const uint32_t c = t % 6u, j = (t / 6u) % LB_MSM_BITS_GROUP, inst = t / (6u * LB_MSM_BITS_GROUP);
+  const uint32_t p = inst / PER_POS, m = (inst % PER_POS) * LB_MSM_BITS_GROUP + j;
+  const uint32_t w = p / LB_MSM_C, k = p % LB_MSM_C;
+  const uint32_t n = k < LB_MSM_C - 1 ? LB_MSM_NB / 2 : 1u;  // (k_msm_bits' enumeration)
+  fp v;
+  fp_zero(v);  // (a missing point: all zero, Z = 0 -- infinity to the program)
+  if (m < n) {
+    const uint32_t low = m & ((1u << k) - 1u), high = m >> k;
+    const uint32_t d = (high << (k + 1)) | (1u << k) | low;
+    v = (&bsum[w * LB_MSM_NB + d - 1].X.c0)[c];
+  }
+#pragma unroll
+  for (int q = 0; q < 12; q++) in16[16 * t + q] = v.l[q];
+#pragma unroll
+  for (int q = 12; q < 16; q++) in16[16 * t + q] = 0u;
+}
+
+__global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_msm_bits(const uint32_t* __restrict__ prog,
+                                                                             uint32_t n, uint32_t n_in,
+                                                                             uint32_t n_out,
+                                                                             const uint32_t* __restrict__ in16,
+                                                                             uint32_t* __restrict__ out16) {
+  __shared__ LpSharedRtail S;
+  __shared__ uint32_t s_fl[4];
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* in = in16 + (size_t)b * n_in * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * n_out * 16, s_fl);
 }
 
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {

@@ -33,7 +33,7 @@ import os
 
 from .dsl import Flag, Fp, Graph, P, select, select_n
 from .tower import (P34, Fp2, Fp6, Fp12, Jac, Ops, Proj, fp2_lex_largest, fp2_sgn0, fp_pow, jac_add, jac_add_aff,
-                    proj_add, proj_dbl, proj_eq, proj_from_jac, proj_mul_xabs, R384_RAW,
+                    proj_add, proj_dbl, proj_eq, proj_from_jac, proj_mul_xabs, proj_to_jac, R384_RAW,
                     jac_dbl, jac_eq, jac_inf, jsel, line_mul_line)
 
 X_ABS = 0xD201000000010000
@@ -800,6 +800,46 @@ def mtail_program(partial: bool) -> Graph:
             g.output("f%d" % k, x * r384, canonical=True)
     else:
         g.output_flag("is_one", final_exp(f).is_one())
+    return g
+
+
+MSM_BITS_GROUP = 8  # k_msm.hip: bucket sums per instance of the lone call's bit-sum programs
+
+
+def msm_bits_program(level: int) -> Graph:
+    """A lone call's bit sums G_p = sum of window w's bucket sums B_d with bit k of d set
+    (p = 11 w + k), as a tree of round programs over groups of MSM_BITS_GROUP points
+    (bls_host.hip run_pipeline; k_msm_bits' 9 dependent one-lane Jacobian additions, ~0.8 ms,
+    become three launches of ~10-16 rounds).  level 0: Jacobian points in the one-lane form
+    (the bucket sums; Z = 0 is infinity) -> their sum, homogeneous, this domain; level 1:
+    homogeneous -> homogeneous; level 2: homogeneous -> Jacobian in the one-lane form (what
+    the merged-check program takes as its G_p).  Complete additions (proj_add): no
+    exceptional case, infinity included."""
+    g = Graph("msm_bits_%d" % level)
+    F = Ops(g, True)
+    zero, one = Fp2.zero(g), Fp2.one(g)
+    pts = []
+    for i in range(MSM_BITS_GROUP):
+        if level == 0:
+            X, Y, Z = (Fp2(g.input("P%d_%s0" % (i, c)), g.input("P%d_%s1" % (i, c))) for c in "XYZ")
+            pts.append(select(Z.is_zero(), Proj(zero, one, zero), proj_from_jac(Jac(X, Y, Z))))
+        else:
+            X, Y, Z = (Fp2(g.input_raw("P%d_%s0" % (i, c)), g.input_raw("P%d_%s1" % (i, c))) for c in "XYZ")
+            pts.append(Proj(X, Y, Z))
+    while len(pts) > 1:
+        pts = [proj_add(F, pts[i], pts[i + 1]) if i + 1 < len(pts) else pts[i] for i in range(0, len(pts), 2)]
+    S = pts[0]
+    if level == 2:
+        J = proj_to_jac(S)
+        r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+        outs = [(J.X, "X"), (J.Y, "Y"), (J.Z, "Z")]
+        for v, c in outs:
+            g.output("S_%s0" % c, v.c0 * r384, canonical=True)
+            g.output("S_%s1" % c, v.c1 * r384, canonical=True)
+    else:
+        for v, c in ((S.X, "X"), (S.Y, "Y"), (S.Z, "Z")):
+            g.output("S_%s0" % c, v.c0, canonical=True)
+            g.output("S_%s1" % c, v.c1, canonical=True)
     return g
 
 

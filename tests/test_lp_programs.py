@@ -298,3 +298,56 @@ def test_rtail_program_against_oracle():
     assert fl == [1]
     _, fl = g.run([mont(v) for v in f12_fps(good) + [0, 0, 0, 0]], [1])
     assert fl == [0]
+
+
+def test_msm_bits_programs_against_oracle():
+    """A lone call's MSM bit sums as three levels of round programs (k_lp_msm_bits): 8 one-lane
+    Jacobian bucket sums per level-0 instance -- some infinite, as k_msm_buckets writes them
+    (Z = 0) or as k_msm_bits_prep pads a position (all zero) -- summed 8:1 three times; the
+    level-2 output, one-lane Jacobian, equals the oracle's sum of the 64 points."""
+    import random
+    rnd = random.Random(11)
+    progs = [lpc.compile_graph(bls.msm_bits_program(k), rows=32) for k in range(3)]
+    assert [p.stats["regs"] <= 512 for p in progs] == [True] * 3
+    pts = []
+    for i in range(64):
+        pts.append(None if i % 9 == 4 else O.g2_mul(O.G2, 7 + 13 * i))
+    want = None
+    for q in pts:
+        if q is not None:
+            want = q if want is None else O.g2_add(want, q)
+    lvl1 = []
+    for grp in range(8):
+        ins = []
+        for j in range(8):
+            q = pts[8 * grp + j]
+            if q is None and j % 2:  # (the prep kernel's padding: every coordinate zero)
+                ins += [0] * 6
+            else:
+                ins += [mont(v) for v in _jac_inputs(q, rnd.randrange(1, P))]
+        outs, _ = progs[0].run(ins, [])
+        assert len(outs) == 6 and all(v < P for v in outs)
+        lvl1 += outs
+    lvl2, _ = progs[1].run(lvl1, [])
+    inf416 = [0, 0, mont416(1), 0, 0, 0]  # homogeneous (0 : 1 : 0)
+    outs, _ = progs[2].run(lvl2 + inf416 * 7, [])
+    r = pow(1 << 384, -1, P)
+    X0, X1, Y0, Y1, Z0, Z1 = (v * r % P for v in outs)
+    # affine x = X / Z^2, y = Y / Z^3 over Fp2
+    def f2mul(a, b):
+        return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+    def f2inv(a):
+        n = pow((a[0] * a[0] + a[1] * a[1]) % P, -1, P)
+        return (a[0] * n % P, -a[1] * n % P)
+    Z = (Z0, Z1)
+    zi = f2inv(Z)
+    zi2 = f2mul(zi, zi)
+    x = f2mul((X0, X1), zi2)
+    y = f2mul((Y0, Y1), f2mul(zi2, zi))
+    assert (x, y) == want
+    # every point infinite: the sum is infinity (Z = 0)
+    outs0, _ = progs[0].run([0] * 48, [])
+    outs1, _ = progs[1].run(outs0 + inf416 * 7, [])
+    outs2, _ = progs[2].run(outs1 + inf416 * 7, [])
+    assert outs2[4] == 0 and outs2[5] == 0
