@@ -794,10 +794,12 @@ class Device:
         res = (out[:, :n_out], ofl[:, :n_outflag], float(ms.value))
         return res + (st,) if stamps else res
 
-    def last_stage_times(self) -> List[Tuple[str, float]]:
+    def last_stage_times(self, raw: bool = False) -> List[Tuple[str, float]]:
         ms = (ctypes.c_float * 32)()
         names = (ctypes.c_char_p * 32)()
         n = self.lib.lb_last_stage_times(self._h, ms, names, 32)
+        if raw:  # one entry per launch, in launch order (tools/opcount.py pairs them with its counters)
+            return [(names[i].decode(), float(ms[i])) for i in range(min(n, 32))]
         # a stage launched more than once in a call (level_wc's passes) is reported once, summed
         out: dict = {}
         for i in range(min(n, 32)):

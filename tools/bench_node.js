@@ -238,12 +238,14 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
   // slot under gossip load.  A priority call's workgroups cannot preempt the throughput
   // waves already on the GPU, so it waits for CUs to drain (DESIGN.md §7).
   const onset1 = [];
+  const clkOnset = [];  // per sample: where its time went (device time vs the kernel's own clock)
   const onsetSamples = parseInt(process.env.LB_NODE_ONSET_SAMPLES || "20", 10);
   for (let r = 0; r < onsetSamples; r++) {
     await new Promise((res) => setTimeout(res, 600));
     const t = ms();
     ok = ok && (await v.verifySignatureSets([set(r + 3)], {verifyOnMainThread: true})) === true;
     onset1.push(ms() - t);
+    clkOnset.push(v.lastMainThreadResult);
   }
   // steady state: priority traffic every ~10 ms (the reservation held)
   const load1 = [];
@@ -331,7 +333,11 @@ async function c4Leg(dir, n, pks, msgs, sigs) {
                          max_ms_1set: +Math.max(...onset1).toFixed(3),
                          ratio_p50_vs_idle: +(median(onset1) / median(pre1)).toFixed(2),
                          ratio_max_vs_idle: +(Math.max(...onset1) / median(pre1)).toFixed(2),
-                         samples: onset1.length, gap_ms: 600},
+                         samples: onset1.length, gap_ms: 600,
+                         // device_ms: the call's first to last event on the lane's stream; kernel_ms: k_lp_verify's
+                         // own clock from its first workgroup's start -- device - kernel = waiting for CUs
+                         device_ms: clkOnset.map((r) => (r && r.deviceMs !== undefined ? +r.deviceMs.toFixed(2) : null)),
+                         kernel_ms: clkOnset.map((r) => (r && r.kernelMs !== undefined ? +r.kernelMs.toFixed(2) : null))},
       under_load: {
         p50_ms_1set_main_thread: load1.length ? +median(load1).toFixed(3) : null,
         p50_ms_128set_priority: load128.length ? +median(load128).toFixed(3) : null,

@@ -19,7 +19,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT_DIR = os.path.join(ROOT, "tools", "opcount_build")
+# (LB_OPCOUNT_DIR: a directory that travels to the GPU box; tools/opcount_build does not)
+OUT_DIR = os.environ.get("LB_OPCOUNT_DIR", os.path.join(ROOT, "tools", "opcount_build"))
 MADS_PER_FPMUL = 288  # 12x12 limb products + 12x12 reduction products (bls_fp_ps.h)
 MADS_PER_FPSQR = 224  # 66 cross (+2 doubled lone cross) + 12 squares + 144 reduction products
 
@@ -71,7 +72,7 @@ def main():
         res = dev.verify_requests(req, np.frombuffer(b"".join(pks), np.uint8), None,
                                   np.frombuffer(b"".join(msgs), np.uint8), blob, offs, bytes(32))
         assert res.valid.all(), res.valid
-        names = [nm for nm, _ in dev.last_stage_times()]
+        names = [nm for nm, _ in dev.last_stage_times(raw=True)]
         buf = (ctypes.c_ulonglong * 32)()
         k = lib.lb_opcount_stages(dev._h, buf, 32)
         per = {}
@@ -81,8 +82,12 @@ def main():
             muls, sqrs = (int(buf[i]) & 0xFFFFFFFF) / 2, int(buf[i]) >> 32
             tot_mul += muls
             tot_sqr += sqrs
-            per[names[i]] = {"fp_mul_total": muls, "fp_sqr_total": sqrs, "fp_mul_per_set": (muls + sqrs) / n,
-                             "mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n}
+            e = per.setdefault(names[i], {"fp_mul_total": 0, "fp_sqr_total": 0, "fp_mul_per_set": 0.0,
+                                          "mads_per_set": 0.0})  # (a stage's launches summed)
+            e["fp_mul_total"] += muls
+            e["fp_sqr_total"] += sqrs
+            e["fp_mul_per_set"] += (muls + sqrs) / n
+            e["mads_per_set"] += (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / n
         return per, tot_mul, tot_sqr
 
     per, tot_mul, tot_sqr = count("steps")
@@ -132,7 +137,7 @@ def count_workloads(out_path=os.path.join(ROOT, "profiles", "op_counts_workloads
         blob, offs = p.blobs()
         r = dev.verify_requests(p.req_off, None, p.pk_off, p.msg_array(), blob, offs, bytes(32), pk_indices=p.idx)
         assert r.valid.all(), name
-        names = [nm for nm, _ in dev.last_stage_times()]
+        names = [nm for nm, _ in dev.last_stage_times(raw=True)]
         buf = (ctypes.c_ulonglong * 32)()
         k = lib.lb_opcount_stages(dev._h, buf, 32)
         per, tm, ts = {}, 0, 0
@@ -140,7 +145,8 @@ def count_workloads(out_path=os.path.join(ROOT, "profiles", "op_counts_workloads
             muls, sqrs = (int(buf[i]) & 0xFFFFFFFF) / 2, int(buf[i]) >> 32
             tm += muls
             ts += sqrs
-            per[names[i]] = {"mads_per_set": (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / p.n_sets}
+            e = per.setdefault(names[i], {"mads_per_set": 0.0})  # (a stage's launches summed)
+            e["mads_per_set"] += (muls * MADS_PER_FPMUL + sqrs * MADS_PER_FPSQR) / p.n_sets
         out[name] = {"sets": p.n_sets, "requests": p.n_req, "pubkeys": int(len(p.idx)),
                      "keys_per_set": len(p.idx) / p.n_sets, "stages": per,
                      "mads_per_set_total": (tm * MADS_PER_FPMUL + ts * MADS_PER_FPSQR) / p.n_sets}
