@@ -85,6 +85,7 @@ struct PipeState {
   bool steps = false;
   Rows rows{};
   const uint32_t* d_G = nullptr;
+  fp12* d_Fparts = nullptr;  // (a split accumulation: k_req_horner's parts per request, k_req_join)
   // the failed merged check's per-request tails as round programs (k_lp_rtail): staged inputs
   uint32_t* d_rt_in = nullptr;
   uint32_t* d_rt_fl = nullptr;
@@ -318,6 +319,7 @@ struct lb_ctx {
   bool msm_lanes = true;
   bool wide_tail = true;
   bool msm_bits_lp = true;  // (LB_MSM_BITS_LP=0: a lone call's bit sums by k_msm_bits' 256 threads)
+  uint32_t step_split = 0;  // LB_STEP_SPLIT: 1, 2 or 4 lanes per set always (0: by size, lone calls only)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -464,7 +466,8 @@ int ensure_pin(lb_ctx* ctx, Slot& sl, size_t bytes) {
   } while (0)
 
 int lp_ensure(lb_ctx* ctx);
-static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req);
+static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req, bool wide);
+static uint32_t step_split_for(uint32_t n_sets);
 int slot_copy(lb_ctx* ctx, Slot& sl, void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st);
 
 // The latency path (k_lp.hip) for a small call: pubkeys -> per-set inputs -> one
@@ -562,9 +565,14 @@ int run_tails(lb_ctx* ctx, Slot& sl) {
     if (!p.d_rt_in)
       LB_STAGE("lines_S", 0, k_lines_S, blocks_for(p.n_req), TPB, p.n_req, p.n_pairs, p.n_sets, (const g2a*)p.d_S,
                p.d_lines, (const uint8_t*)p.d_mflag);
-    if (p.steps)
-      LB_STAGE("req_horner", 0, k_req_horner, p.n_req, TPB, p.n_req, p.n_sets, p.rows, p.d_req_off, p.d_G,
-               (const uint8_t*)p.d_bad, p.d_F, (const uint8_t*)p.d_mflag);
+    if (p.steps) {
+      const uint32_t sp = p.rows.split;
+      LB_STAGE("req_horner", 0, k_req_horner, p.n_req * sp, TPB, p.n_req, p.n_sets, p.rows, p.d_req_off, p.d_G,
+               (const uint8_t*)p.d_bad, sp > 1 ? p.d_Fparts : p.d_F, (const uint8_t*)p.d_mflag);
+      if (sp > 1)
+        LB_STAGE("req_horner", 0, k_req_join, p.n_req, TPB, p.n_req, sp, (const fp12*)p.d_Fparts,
+                 (const uint8_t*)p.d_bad, p.d_F, (const uint8_t*)p.d_mflag);
+    }
     if (p.d_rt_in) {
       hipLaunchKernelGGL(k_rtail_prep, dim3((p.n_req * LB_RTAIL_NIN + 255) / 256), dim3(256), 0, sl.st[0], p.n_req,
                          (const fp12*)p.d_F, (const g2a*)p.d_S, p.d_rt_in, p.d_rt_fl);
@@ -687,11 +695,19 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_rpos = steps ? ws.take<uint32_t>(n_req) : nullptr;
   uint32_t* d_rinv = steps ? ws.take<uint32_t>(n_req) : nullptr;
   uint32_t* d_rmeta = steps ? ws.take<uint32_t>(1) : nullptr;
-  uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns) : nullptr;
+  // a lone mid-size call splits every lane of the step-major accumulation (its time is the
+  // one-lane latency of a lane's 68 lines: 17 or 34 lines a lane instead; LB_STEP_SPLIT forces)
+  uint32_t lsplit = 1;
+  if (steps) {
+    lsplit = lone ? step_split_for(n_sets) : 1u;
+    if (ctx->step_split) lsplit = ctx->step_split;
+  }
+  uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns * lsplit) : nullptr;
+  fp12* d_Fparts = steps && lsplit > 1 ? ws.take<fp12>((size_t)(n_req ? n_req : 1) * lsplit) : nullptr;
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
   // the level products' two stages (k_level_part's partials, the first k_level_wc pass's output)
   const bool level_wc = steps && merged && ctx->level_wc;
-  const uint32_t lvl_per = level_wc ? level_blocks(n_sets, n_req) * 256u : 0u;
+  const uint32_t lvl_per = level_wc ? level_blocks(n_sets * lsplit, n_req, lone) * 256u : 0u;
   fp12* d_lvA = level_wc ? ws.take<fp12>(63 * (size_t)lvl_per) : nullptr;
   fp12* d_lvB = level_wc ? ws.take<fp12>(63 * (size_t)((lvl_per + LB_LVL_GROUP - 1) / LB_LVL_GROUP)) : nullptr;
   uint8_t* d_lhA = level_wc ? ws.take<uint8_t>(63 * (size_t)lvl_per) : nullptr;
@@ -701,7 +717,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_mb_in0 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST * LB_MSM_BITS_GROUP * 6 * 16) : nullptr;
   uint32_t* d_mb_in1 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST * 6 * 16) : nullptr;
   uint32_t* d_mb_in2 = bits_lp ? ws.take<uint32_t>((size_t)LB_MSM_BITS_INST / 8 * 6 * 16) : nullptr;
-  const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta};
+  const Rows rows{d_rowoff, d_rinv, d_rpos, d_rmeta, lsplit};
   sl.h_stats[0] = sl.h_stats[1] = 0;
   if (ws.off > ws.cap) {
     ctx->err = "workspace overflow";
@@ -801,8 +817,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       LB_STAGE("msm_bits", 0, k_lp_msm_bits, LB_MSM_POS, LB_LP_TPB, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_MSM_BITS2].off,
                (uint32_t)LB_MSM_POS, NI, 6u, (const uint32_t*)d_mb_in2, d_mt_in + (size_t)12 * LB_MTAIL_LEVELS * 16);
     } else {
-      LB_STAGE("msm_bits", 0, k_msm_bits, LB_MSM_POS, msm_wide ? LB_MSM_BITS_TPB : (uint32_t)TPB, (const g2j*)d_mbsum,
-               d_mG);
+      if (msm_wide)
+        LB_STAGE("msm_bits", 0, k_msm_bits<LB_MSM_BITS_TPB>, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_mbsum, d_mG);
+      else
+        LB_STAGE("msm_bits", 0, k_msm_bits<TPB>, LB_MSM_POS, TPB, (const g2j*)d_mbsum, d_mG);
     }
     if (!mtail) LB_STAGE("msm_final", 0, k_msm_final, 1u, TPB, (const g2j*)d_mG, d_Sall);
     if (!fold && !mtail)
@@ -831,7 +849,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   }
   if (steps) {
 #define LB_STEP_STAGE(M, W)                                                                               \
-  LB_STAGE("step_acc", 0, (k_step_acc<M, W>), blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,  \
+  LB_STAGE("step_acc", 0, (k_step_acc<M, W>), blocks_for(n_sets * lsplit), TPB, n_sets, n_pairs, rows, d_req_off, \
            (const uint32_t*)d_lines, d_G)
     if (ctx->step_mode == 1)
       LB_STEP_STAGE(1, 1);
@@ -872,8 +890,11 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
       // Miller loop's squarings of (-g1, S_all): no one-wave k_horner_all)
       if (!mtail) LB_STAGE("horner_all", 0, k_horner_all, 1u, TPB, (const fp12*)d_Pl, d_Fall);
     } else {
-      LB_STAGE("req_horner", 0, k_req_horner, n_req, TPB, n_req, n_sets, rows, d_req_off, (const uint32_t*)d_G,
-               (const uint8_t*)d_bad, d_F, (const uint8_t*)nullptr);
+      LB_STAGE("req_horner", 0, k_req_horner, n_req * lsplit, TPB, n_req, n_sets, rows, d_req_off,
+               (const uint32_t*)d_G, (const uint8_t*)d_bad, lsplit > 1 ? d_Fparts : d_F, (const uint8_t*)nullptr);
+      if (lsplit > 1)
+        LB_STAGE("req_horner", 0, k_req_join, n_req, TPB, n_req, lsplit, (const fp12*)d_Fparts, (const uint8_t*)d_bad,
+                 d_F, (const uint8_t*)nullptr);
     }
   } else if (by_lines) {
     const uint32_t nr = split ? 2 * n_req : n_req;
@@ -938,6 +959,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   ps.steps = steps;
   ps.rows = rows;
   ps.d_G = d_G;
+  ps.d_Fparts = d_Fparts;
   if (merged) {
     // merged check: one tail for the whole call; per-request tails only if it fails.
     // LB_TAIL_PRIO=1 runs its chain of one-wave kernels on a shared high-priority
@@ -1004,10 +1026,18 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   return run_tails(ctx, sl);
 }
 
+// lanes per set of a lone call's step-major accumulation: 4 up to 16,384 sets, 2 up to 32,768 (the
+// call's lanes then fill at most one wave per SIMD), 1 above (profiles/r06/level_probe_r06x.json:
+// 4,096 ... 16,384 sets 16.7-17.4 ms unsplit, 14.1-15.0 split in 4)
+static uint32_t step_split_for(uint32_t n_sets) { return n_sets <= 16384u ? 4u : n_sets <= 32768u ? 2u : 1u; }
+
 // k_level_part's workgroups per level: one request per thread (a merged call's requests are
 // mostly small), and about two lanes per thread when one large request holds the call
-static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req) {
-  const uint32_t w = n_req > n_sets / 126u ? n_req : n_sets / 126u;
+static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req, bool wide) {
+  // (wide, a lone call: about one lane per thread -- the products all in the wave-cooperative
+  // passes, the fastest for the call; otherwise about two, one lane product each: less work)
+  const uint32_t w = wide ? (4 * n_req > n_sets / 32u ? 4 * n_req : n_sets / 32u)
+                          : (n_req > n_sets / 126u ? n_req : n_sets / 126u);
   const uint32_t b = (w + 255u) / 256u;
   return b < 1u ? 1u : b > 8u ? 8u : b;
 }
@@ -1019,7 +1049,7 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 + 16 + 576 +
                    (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 + (2 * LB_MSM_W * sizeof(g2j)) / LB_MSM_T + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
-  size_t per_req = sizeof(g2a) + 4 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
+  size_t per_req = sizeof(g2a) + 8 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
                    (size_t)LB_RTAIL_NIN * 64 + 4 + 2 * 256 / 64;  // (+ k_lp_rtail's records and flag)
   // (+ a lone call's bit-sum program records: 8 + 1 + 1/8 points of 6 records per level-0 instance)
   const size_t msm_fixed = (size_t)(2 * LB_MSM_BUCKETS + LB_MSM_POS) * sizeof(g2j) + 4 * (LB_MSM_BUCKETS + 1) * 4 +
@@ -1027,11 +1057,13 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   // (+ the merged check's round-program records, k_lp_mtail)
   // (+ the level products' partials: 63 x 256 B of k_level_part, an eighth of that for the
   // first k_level_wc pass, their flags)
-  const size_t lvl_per = (size_t)level_blocks(n_sets, n_req) * 256;
+  // (+ the G values of a split accumulation, up to 4 lanes per set: LB_STEP_SPLIT may force 4 at
+  // any size -- 3 more G per set, and 4x the lanes for the level partials)
+  const size_t lvl_per = (size_t)level_blocks(n_sets * 4u, n_req, true) * 256;
   const size_t lvl = 63 * (lvl_per + (lvl_per + LB_LVL_GROUP - 1) / LB_LVL_GROUP) * sizeof(fp12) + 2 * 63 * lvl_per +
                      4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
-         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl;
+         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576;
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1281,11 +1313,12 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_lines<2>, (const void*)k_lines_rows<1>, (const void*)k_lines_rows<2>,
                            (const void*)k_pair_wc, (const void*)k_miller_sets,
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
-                           (const void*)k_tail, (const void*)k_req_horner, (const void*)k_lp_verify,
+                           (const void*)k_tail, (const void*)k_req_horner, (const void*)k_req_join, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
                            (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
-                           (const void*)k_msm_buckets, (const void*)k_msm_bits, (const void*)k_decode_sigs,
+                           (const void*)k_msm_buckets, (const void*)k_msm_bits<TPB>, (const void*)k_msm_bits<LB_MSM_BITS_TPB>,
+                           (const void*)k_decode_sigs,
                            (const void*)k_scalar_pk};
   size_t lane = 0;
   for (const void* k : kernels) {
@@ -1359,6 +1392,10 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MSM_LANES")) ctx->msm_lanes = atoi(e) != 0;
   if (const char* e = getenv("LB_WIDE_TAIL")) ctx->wide_tail = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_BITS_LP")) ctx->msm_bits_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_STEP_SPLIT")) {
+    const int v = atoi(e);
+    ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
+  }
   if (const char* e = getenv("LB_WAVE_MAX")) ctx->wave_max_sets = (uint32_t)atoi(e);
   if (const char* e = getenv("LB_MTAIL")) ctx->mtail_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_RTAIL")) ctx->rtail_lp = atoi(e) != 0;
@@ -3044,7 +3081,7 @@ int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw
             (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum);
   LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
             (const g2j*)d_csum, d_bsum, LB_MSM_BLANES);
-  LB_LAUNCH(k_msm_bits, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_bsum, d_G);
+  LB_LAUNCH(k_msm_bits<LB_MSM_BITS_TPB>, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_bsum, d_G);
   LB_LAUNCH(k_msm_final, 1u, TPB, (const g2j*)d_G, d_S);
   LB_LAUNCH(k_g2a_serialize, 1u, TPB, 1u, (const g2a*)d_S, d_out);
   LB_HIP(hipMemcpyAsync(out192, d_out, 192, hipMemcpyDeviceToHost, ctx->stream));

@@ -116,6 +116,9 @@ struct Rows {
   const uint32_t* inv;
   const uint32_t* pos;
   const uint32_t* meta;
+  // lanes per set of the step-major accumulation (1, 2 or 4: 68 / split lines per lane; a lone
+  // mid-size call's k_step_acc is the one-lane latency of its lanes' lines, k_steps.hip)
+  uint32_t split = 1;
 };
 
 __global__ void __launch_bounds__(TPB) k_req_flags(uint32_t n_req, const uint32_t* __restrict__ req_off,
@@ -254,7 +257,9 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t
                                                                   uint32_t lanes);
 static constexpr uint32_t LB_MSM_BLANES = 4;      // k_msm_buckets: lanes per bucket
 static constexpr uint32_t LB_MSM_BITS_TPB = 256;  // k_msm_bits: threads per bit position
-__global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G);
+template <int T>  // (T threads per bit position: TPB, or LB_MSM_BITS_TPB for a lone call)
+__global__ void __launch_bounds__(T, T == TPB ? LB_W_SCALAR : 1) k_msm_bits(const g2j* __restrict__ bsum,
+                                                                           g2j* __restrict__ G);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_final(const g2j* __restrict__ G, g2a* __restrict__ S);
 __global__ void __launch_bounds__(256) k_rows_hist(uint32_t n_req, const uint32_t* __restrict__ req_off,
                                                    uint32_t* __restrict__ hist);
@@ -302,6 +307,10 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
                                                              const uint32_t* __restrict__ G,
                                                              const uint8_t* __restrict__ req_bad,
                                                              fp12* __restrict__ F, const uint8_t* __restrict__ skip);
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_join(uint32_t n_req, uint32_t split,
+                                                           const fp12* __restrict__ parts,
+                                                           const uint8_t* __restrict__ req_bad,
+                                                           fp12* __restrict__ F, const uint8_t* __restrict__ skip);
 __global__ void __launch_bounds__(TPB) k_msm_load(uint32_t n, const uint8_t* __restrict__ in192, g2j* __restrict__ out,
                                                   uint8_t* __restrict__ status);
 }  // namespace lb

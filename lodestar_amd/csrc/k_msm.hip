@@ -251,8 +251,10 @@ __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t
 // buckets d of window w whose bit k is set (512 of them for k < 10, only d = 1024 for k = 10):
 // two buckets per thread, then an LDS tree (round 6: 256 threads, 9 dependent additions
 // instead of one wave's 8 + 6)
-__global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __restrict__ bsum, g2j* __restrict__ G) {
-  __shared__ LdsRec<g2j> sh[LB_MSM_BITS_TPB];
+template <int T>
+__global__ void __launch_bounds__(T, T == TPB ? LB_W_SCALAR : 1) k_msm_bits(const g2j* __restrict__ bsum,
+                                                                           g2j* __restrict__ G) {
+  __shared__ LdsRec<g2j> sh[T];  // (T = TPB: the narrow form's 19 KB, not the wide one's 78 KB)
   const uint32_t p = blockIdx.x;
   if (p >= LB_MSM_POS) return;
   const uint32_t w = p / LB_MSM_C, k = p % LB_MSM_C;
@@ -261,7 +263,7 @@ __global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __re
   jac_set_inf(acc);
   bool have = false;
 #pragma unroll 1
-  for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) {  // (blockDim: 256, or 64 with LB_MSM_LANES=0)
+  for (uint32_t m = threadIdx.x; m < n; m += T) {
     const uint32_t low = m & ((1u << k) - 1u), high = m >> k;
     const uint32_t d = (high << (k + 1)) | (1u << k) | low;  // 1 <= d <= 1024, bit k set
     g2j t = bsum[w * LB_MSM_NB + d - 1];
@@ -275,7 +277,7 @@ __global__ void __launch_bounds__(LB_MSM_BITS_TPB, 1) k_msm_bits(const g2j* __re
   sh[threadIdx.x].v = acc;
   __syncthreads();
 #pragma unroll 1
-  for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
+  for (uint32_t s = T / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
       g2j m = sh[threadIdx.x].v, o = sh[threadIdx.x + s].v;
       jac_add(m, m, o);
@@ -329,5 +331,8 @@ __global__ void __launch_bounds__(TPB) k_msm_load(uint32_t n, const uint8_t* __r
   out[i] = p;
   status[i] = st;
 }
+
+template __global__ void k_msm_bits<TPB>(const g2j* __restrict__, g2j* __restrict__);
+template __global__ void k_msm_bits<LB_MSM_BITS_TPB>(const g2j* __restrict__, g2j* __restrict__);
 
 }  // namespace lb

@@ -274,20 +274,20 @@ struct AccLds {
 
 template <bool PAIRED, class Acc>
 LB_DEV void step_lines(Acc& acc, const uint32_t* __restrict__ lines, uint32_t n_pairs, const Rows& R, uint32_t r,
-                       uint32_t n, uint32_t t0) {
+                       uint32_t n, uint32_t t0, uint32_t cnt) {
   uint32_t j = t0 / n, i = t0 - j * n;
   int lvl = c_steps.lvl[j];
   bool have = false;
   fp2 l0, l1, l4;
 #pragma unroll 1
-  for (uint32_t c = 0; c < (uint32_t)LB_MILLER_LINES;) {
+  for (uint32_t c = 0; c < cnt;) {
     const int lj = c_steps.lvl[j];
     if (lj != lvl) {  // one doubling step further: one squaring
       if (have) acc.sqr();
       lvl = lj;
     }
     const uint32_t qa = R.rowoff[i] + r;
-    if (PAIRED && i + 1 < n && c + 1 < (uint32_t)LB_MILLER_LINES) {  // two lines of the same step
+    if (PAIRED && i + 1 < n && c + 1 < cnt) {  // two lines of the same step
       const uint32_t qb = R.rowoff[i + 1] + r;
       fp2 m0, m1, m4, y1, y2;
       fp6 x;
@@ -344,33 +344,43 @@ __global__ void __launch_bounds__(TPB, WAVES) k_step_acc(uint32_t n_sets, uint32
                                                             const uint32_t* __restrict__ lines,
                                                             uint32_t* __restrict__ G) {
   __shared__ LdsRec<fp12> sacc[MODE == 1 ? TPB : 1];
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  // thread t: part h of slot q's lane (R.split parts of 68 / split lines; G slot q split + h)
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = t / R.split, h = t - q * R.split;
   if (q >= n_sets) return;
   uint32_t l, r;
   slot_row(R, q, l, r);
   const uint32_t k = R.inv[r];
   const uint32_t n = req_off[k + 1] - req_off[k];
+  const uint32_t L = (uint32_t)LB_MILLER_LINES / R.split, t0 = (uint32_t)LB_MILLER_LINES * l + L * h;
   fp12 out;
   if constexpr (MODE == 1) {
     AccLds acc{&sacc[threadIdx.x].v};
-    step_lines<true>(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    step_lines<true>(acc, lines, n_pairs, R, r, n, t0, L);
     acc.get(out);
   } else {
     AccReg acc;
-    step_lines<MODE == 0>(acc, lines, n_pairs, R, r, n, (uint32_t)LB_MILLER_LINES * l);
+    step_lines<MODE == 0>(acc, lines, n_pairs, R, r, n, t0, L);
     acc.get(out);
   }
-  g_put(G, n_sets, q, out);
+  g_put(G, n_sets * R.split, t, out);
 }
 
-// [lo, hi): the lane indices l of an n-set request whose last line has level lvl
-LB_DEV void level_lanes(uint32_t n, int lvl, uint32_t& lo, uint32_t& hi) {
-  const int64_t a = (int64_t)c_steps.first[lvl] * n - (LB_MILLER_LINES - 1);
-  const int64_t b = (int64_t)c_steps.first[lvl + 1] * n - (LB_MILLER_LINES - 1);
-  lo = a <= 0 ? 0u : (uint32_t)((a + LB_MILLER_LINES - 1) / LB_MILLER_LINES);
-  hi = b <= 0 ? 0u : (uint32_t)((b + LB_MILLER_LINES - 1) / LB_MILLER_LINES);
-  if (hi > n) hi = n;
+// [lo, hi): the (virtual) lane indices v of an n-set request whose last line has level lvl;
+// lane v covers lines [v L, v L + L) with L = 68 / split (split v-lanes per set)
+LB_DEV void level_lanes(uint32_t n, int lvl, uint32_t& lo, uint32_t& hi, uint32_t split = 1) {
+  const int64_t L = LB_MILLER_LINES / (int64_t)split;
+  const int64_t a = (int64_t)c_steps.first[lvl] * n - (L - 1);
+  const int64_t b = (int64_t)c_steps.first[lvl + 1] * n - (L - 1);
+  lo = a <= 0 ? 0u : (uint32_t)((a + L - 1) / L);
+  hi = b <= 0 ? 0u : (uint32_t)((b + L - 1) / L);
+  if (hi > n * split) hi = n * split;
   if (lo > hi) lo = hi;
+}
+// G slot of lane v of the request at position r (k_step_acc: slot q's part h at q split + h)
+LB_DEV uint32_t g_slot(const Rows& R, uint32_t v, uint32_t r) {
+  const uint32_t l = v / R.split;
+  return (R.rowoff[l] + r) * R.split + (v - l * R.split);
 }
 
 // Merged check: P[lvl] = prod over the good requests' lanes at level lvl of G,
@@ -392,7 +402,7 @@ __global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, ui
   bool have = false;
   auto take = [&](uint32_t q) {
     fp12 g;
-    g_get(g, G, n_sets, q);
+    g_get(g, G, n_sets * R.split, q);
     if (have) {
       fp12_mul(acc, acc, g);
     } else {
@@ -406,18 +416,18 @@ __global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, ui
   uint32_t r0 = 0;
   for (; r0 < n_req; r0++) {
     const uint32_t k = R.inv[r0], n = req_off[k + 1] - req_off[k];
-    if (n <= 16u * LB_MILLER_LINES) break;
+    if (n * R.split <= 16u * LB_MILLER_LINES) break;
     if (req_bad[k]) continue;
     uint32_t lo, hi;
-    level_lanes(n, lvl, lo, hi);
-    for (uint32_t l = lo + tid; l < hi; l += LB_LVL_TPB) take(R.rowoff[l] + r0);
+    level_lanes(n, lvl, lo, hi, R.split);
+    for (uint32_t l = lo + tid; l < hi; l += LB_LVL_TPB) take(g_slot(R, l, r0));
   }
   for (uint32_t r = r0 + tid; r < n_req; r += LB_LVL_TPB) {
     const uint32_t k = R.inv[r];
     if (req_bad[k]) continue;
     uint32_t lo, hi;
-    level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi);
-    for (uint32_t l = lo; l < hi; l++) take(R.rowoff[l] + r);
+    level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi, R.split);
+    for (uint32_t l = lo; l < hi; l++) take(g_slot(R, l, r));
   }
   if (have) sh[tid].v = acc;
   has[tid] = have ? 1 : 0;
@@ -463,10 +473,10 @@ __global__ void __launch_bounds__(LB_LVL_TPB, 1) k_level_prod(uint32_t n_req, ui
 // The level products in two stages (round 6; LB_LEVEL=0 restores k_level_prod).  k_level_prod's
 // 256 threads per level end in an LDS tree of eight single-lane Fp12 products (~150 us each on
 // one lane): ~11 dependent lane products, 1.7 ms for a 65,536-set call.  Here:
-//   k_level_part, grid (B, 63): thread g of level lvl takes the level's lanes of its share of the
-//     requests (one request per thread; a large request's lanes strided over the level's
-//     per = 256 B threads) -- one or two lane products -- and stores its product, or nothing,
-//     at part[lvl * per + g];
+//   k_level_part, grid (B, 63): the level's per = 256 B threads dealt over the requests (per /
+//     n_req threads each, each taking every (per / n_req)-th lane of its request at this level;
+//     one request per thread when there are more) -- one or two lane products -- and stores
+//     its product, or nothing, at part[lvl * per + g];
 //   k_level_wc, grid (ceil(per_in / 8), 63), one wave each: the product of a group of 8
 //     partials as wave-cooperative Fp12 products (~10 us each, bls_wc12.h), until one value
 //     per level is left; the last pass (Pl given) multiplies in the merged pair's lines of
@@ -483,7 +493,7 @@ __global__ void __launch_bounds__(256, 1) k_level_part(uint32_t n_req, uint32_t 
   bool have = false;
   auto take = [&](uint32_t q) {
     fp12 v;
-    g_get(v, G, n_sets, q);
+    g_get(v, G, n_sets * R.split, q);
     if (have) {
       fp12_mul(acc, acc, v);
     } else {
@@ -491,21 +501,27 @@ __global__ void __launch_bounds__(256, 1) k_level_part(uint32_t n_req, uint32_t 
       have = true;
     }
   };
-  uint32_t r0 = 0;
-  for (; r0 < n_req; r0++) {  // (size-descending: the large requests first)
-    const uint32_t k = R.inv[r0], n = req_off[k + 1] - req_off[k];
-    if (n <= 16u * LB_MILLER_LINES) break;
-    if (req_bad[k]) continue;
-    uint32_t lo, hi;
-    level_lanes(n, lvl, lo, hi);
-    for (uint32_t l = lo + g; l < hi; l += per) take(R.rowoff[l] + r0);
-  }
-  for (uint32_t r = r0 + g; r < n_req; r += per) {
-    const uint32_t k = R.inv[r];
-    if (req_bad[k]) continue;
-    uint32_t lo, hi;
-    level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi);
-    for (uint32_t l = lo; l < hi; l++) take(R.rowoff[l] + r);
+  // T = per / n_req threads per request (consecutive threads: consecutive requests at the same
+  // lane index -- coalesced G loads), thread j of a request taking its lanes j, j + T, ...; with
+  // more requests than threads, one request per thread and all its lanes of the level
+  const uint32_t T = per >= n_req ? per / n_req : 0u;
+  if (T) {
+    if (g < n_req * T) {
+      const uint32_t r = g % n_req, j = g / n_req, k = R.inv[r];
+      if (!req_bad[k]) {
+        uint32_t lo, hi;
+        level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi, R.split);
+        for (uint32_t l = lo + j; l < hi; l += T) take(g_slot(R, l, r));
+      }
+    }
+  } else {
+    for (uint32_t r = g; r < n_req; r += per) {
+      const uint32_t k = R.inv[r];
+      if (req_bad[k]) continue;
+      uint32_t lo, hi;
+      level_lanes(req_off[k + 1] - req_off[k], lvl, lo, hi, R.split);
+      for (uint32_t l = lo; l < hi; l++) take(g_slot(R, l, r));
+    }
   }
   const size_t o = (size_t)lvl * per + g;
   if (have) part[o] = acc;
@@ -579,8 +595,11 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
                                                              const uint32_t* __restrict__ G,
                                                              const uint8_t* __restrict__ req_bad,
                                                              fp12* __restrict__ F, const uint8_t* __restrict__ skip) {
+  // (a split accumulation: one wave per (request, part h) over the lanes v = h mod split -- the
+  // conjugated Horner value is multiplicative over any partition of the lanes, so each wave
+  // runs the squaring chain of its share and k_req_join multiplies the parts; F: split per request)
   __shared__ wc_smem S;
-  const uint32_t k = blockIdx.x;
+  const uint32_t k = blockIdx.x / R.split, h = blockIdx.x - k * R.split;
   if (k >= n_req || (skip && *skip) || req_bad[k]) return;  // (uniform per workgroup)
   const uint32_t n = req_off[k + 1] - req_off[k], r = R.pos[k];
   wc_init_tables(S);
@@ -589,14 +608,14 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
   for (int lvl = 0; lvl < 63; lvl++) {
     if (started) wc_apply(S, LB_WC_SQR, WC_ACC, WC_ACC, WC_ACC);
     uint32_t lo, hi;
-    level_lanes(n, lvl, lo, hi);
-    for (uint32_t l = lo; l < hi; l++) {
+    level_lanes(n, lvl, lo, hi, R.split);
+    for (uint32_t l = lo + (h + R.split - lo % R.split) % R.split; l < hi; l += R.split) {
       const int dst = started ? WC_T0 : WC_ACC;
       if (threadIdx.x < 12) {
         fp v;
-        const size_t q = (size_t)R.rowoff[l] + r;
+        const size_t q = g_slot(R, l, r);
 #pragma unroll
-        for (int w = 0; w < 12; w++) v.l[w] = G[(size_t)(12 * threadIdx.x + w) * n_sets + q];
+        for (int w = 0; w < 12; w++) v.l[w] = G[(size_t)(12 * threadIdx.x + w) * n_sets * R.split + q];
         S.slot[dst][threadIdx.x] = v;
       }
       __syncthreads();
@@ -606,6 +625,24 @@ __global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_horner(uint32_t n_req, u
   }
   if (!started) wc_set_one(S, WC_ACC);
   wc_apply(S, LB_WC_CONJ, WC_ACC, WC_ACC, WC_ACC);
+  if (threadIdx.x < 12) (&F[blockIdx.x].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
+}
+
+// F[k] = the product of k_req_horner's `split` parts of request k (one wave per request)
+__global__ void __launch_bounds__(TPB, LB_W_TAIL) k_req_join(uint32_t n_req, uint32_t split,
+                                                           const fp12* __restrict__ parts,
+                                                           const uint8_t* __restrict__ req_bad,
+                                                           fp12* __restrict__ F, const uint8_t* __restrict__ skip) {
+  __shared__ wc_smem S;
+  const uint32_t k = blockIdx.x;
+  if (k >= n_req || (skip && *skip) || req_bad[k]) return;  // (uniform per workgroup)
+  wc_init_tables(S);
+  wc_load12(S, WC_ACC, parts[(size_t)k * split]);
+#pragma unroll 1
+  for (uint32_t h = 1; h < split; h++) {
+    wc_load12(S, WC_T0, parts[(size_t)k * split + h]);
+    wc_apply(S, LB_WC_MUL, WC_ACC, WC_ACC, WC_T0);
+  }
   if (threadIdx.x < 12) (&F[k].c0.c0.c0)[threadIdx.x] = S.slot[WC_ACC][threadIdx.x];
 }
 

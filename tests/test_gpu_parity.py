@@ -469,16 +469,19 @@ def test_mixed_workload_steps_vs_c_oracle(device, msm, merge, inject):
         dev.close()
 
 
+@pytest.mark.parametrize("split", ["", "1", "2"])
 @pytest.mark.parametrize("level", ["1", "0"])
 @pytest.mark.parametrize("layout", ["mixed", "one_large"])
-def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout, level):
+def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout, level, split):
     """Row layout edge cases of the steps organisation: equal-size requests (the
     coalesced C2 shape), one-set requests (a lane runs the whole Miller loop), a
     request larger than 68 sets next to small ones, an empty request; and a
     1,200-set request beside small ones (its lanes of a level spread over all the
     threads of k_level_part / k_level_prod).  The level products both ways: lane
     products + wave-cooperative passes (LB_LEVEL=1, default) and k_level_prod's
-    one-lane LDS tree (LB_LEVEL=0)."""
+    one-lane LDS tree (LB_LEVEL=0); the lanes of the accumulation split in 4 (a lone
+    call of this size, default), 2 or not at all (LB_STEP_SPLIT): 17, 34 or 68 lines a
+    lane."""
     from oracle import c_oracle as C
     req_off, pks, pk_off, msgs, blob, offs = mixed_workload_cache(device, layout == "mixed")
     n = len(pk_off) - 1
@@ -488,7 +491,8 @@ def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout, level):
         off.append(min(n, off[-1] + z))
     off[-1] = n
     seed = hashlib.sha256(b"steps-rows").digest()
-    dev = _device_with_env(LB_MILLER="lines", LB_LEVEL=level)
+    env = {"LB_STEP_SPLIT": split} if split else {}
+    dev = _device_with_env(LB_MILLER="lines", LB_LEVEL=level, **env)
     try:
         ro = np.array(off, np.uint32)
         res = dev.verify_requests(ro, pks, pk_off, msgs, blob, offs, seed)
