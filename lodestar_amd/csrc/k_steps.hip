@@ -8,11 +8,13 @@
 // accumulator 62 times.  Here a lane takes 68 consecutive lines of its request
 // in step-major order -- lines t in [68 l, 68 l + 68) with j = t / n_k,
 // i = t mod n_k -- so a lane of a >= 68-set request spans at most two steps and
-// squares at most once; a request has n_k lanes (one per set, as before).
+// squares at most once; a request has n_k lanes (one per set, as before; a lone
+// mid-size call splits each in Rows::split lanes of 68 / split lines).
 // The squarings left are those of one Horner chain over the 63 levels per
-// merged check (k_horner_all, one wave) or per request on the failure path
-// (k_req_horner).  Work per pair: 68 x 11.5 Fp2 products instead of
-// 68 x 17.5 (two pairs per lane) or 68 x 25 (one pair per lane).
+// merged check (folded into the merged-check round program, k_lp_mtail; or
+// k_horner_all, one wave) or per request on the failure path (k_req_horner).
+// Work per pair: 68 x 11.5 Fp2 products instead of 68 x 17.5 (two pairs per
+// lane) or 68 x 25 (one pair per lane).
 //
 // Row layout: requests are ordered by size, descending (position pos(k)); row i
 // holds pair i of every request with n_k > i, so pair (k, i) lives at slot
