@@ -320,6 +320,9 @@ struct lb_ctx {
   bool wide_tail = true;
   bool msm_bits_lp = true;  // (LB_MSM_BITS_LP=0: a lone call's bit sums by k_msm_bits' 256 threads)
   uint32_t step_split = 0;  // LB_STEP_SPLIT: 1, 2 or 4 lanes per set always (0: by size, lone calls only)
+  // same-message packages of at most LB_SM_DEC_MAX signatures decode them as round programs
+  // (k_lp_dec; LB_SM_LP_DECODE=0: k_decode_sigs always)
+  bool sm_lp_decode = true;
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -1315,7 +1318,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_req_join, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_msm_bits<TPB>, (const void*)k_msm_bits<LB_MSM_BITS_TPB>,
                            (const void*)k_decode_sigs,
@@ -1392,6 +1395,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MSM_LANES")) ctx->msm_lanes = atoi(e) != 0;
   if (const char* e = getenv("LB_WIDE_TAIL")) ctx->wide_tail = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_BITS_LP")) ctx->msm_bits_lp = atoi(e) != 0;
+  if (const char* e = getenv("LB_SM_LP_DECODE")) ctx->sm_lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
@@ -2699,7 +2703,9 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   const size_t res_bytes = 4 * al256(nj), retry_bytes = 2 * al256(4 * ns1) + 2 * al256(ns1);
   const size_t extra = ns1 * (sizeof(g2j) + 1) + (size_t)nj * (sizeof(g1j) + 1 + 96 + 192 + 1 + 2) + 16 * 256;
   LB_TRY(ensure_pin(ctx, sl, in_bytes + res_bytes + retry_bytes));
-  LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj) + sm_phase2_bytes(ns)));
+  // (+ a small package's decode records: 4 + 2 records, 5 flags and a status per signature)
+  const size_t dec_bytes = ns <= LB_SM_DEC_MAX ? (size_t)ns * (6 * 64 + 5 * 4 + 1) + 6 * 256 : 0;
+  LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj) + sm_phase2_bytes(ns) + dec_bytes));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   char* h = sl.h_pin;
   size_t ho = 0;
@@ -2749,9 +2755,30 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   uint8_t* d_err = ws.take<uint8_t>(nj);
   LB_TRY(begin_call(ctx, sl));
   LB_HIP(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, sl.st[0]));
-  if (ns)
+  if (ns && ns <= LB_SM_DEC_MAX && ctx->sm_lp_decode) {
+    // a small package: each signature's decode as a round program on an 8-row workgroup (~540
+    // rounds) instead of k_decode_sigs' one-lane chain (~4 ms); the same outputs and statuses
+    LB_TRY(lp_ensure(ctx));
+    uint32_t* d_dec_in = ws.take<uint32_t>((size_t)ns * 4 * 16);
+    uint32_t* d_dec_fl = ws.take<uint32_t>((size_t)ns * 3);
+    uint32_t* d_dec_out = ws.take<uint32_t>((size_t)ns * 2 * 16);
+    uint32_t* d_dec_ofl = ws.take<uint32_t>((size_t)ns * 2);
+    uint8_t* d_dec_pre = ws.take<uint8_t>(ns);
+    if (ws.off > ws.cap) {
+      ctx->err = "workspace overflow";
+      return LB_ERR_OUT_OF_MEMORY;
+    }
+    LB_STAGE("sm_decode", 0, k_sm_dec_prep, blocks_for(ns, 256), 256u, ns, d_sigs, d_sigo, d_dec_in, d_dec_fl,
+             d_dec_pre);
+    LB_STAGE("sm_decode", 0, k_lp_dec, ns, LB_LP_DEC_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SIG_DECODE].off, ns,
+             (const uint32_t*)d_dec_in, (const uint32_t*)d_dec_fl, d_dec_out, d_dec_ofl);
+    LB_STAGE("sm_decode", 0, k_sm_dec_finish, blocks_for(ns, 256), 256u, ns, (const uint8_t*)d_dec_pre,
+             (const uint32_t*)d_dec_in, (const uint32_t*)d_dec_fl, (const uint32_t*)d_dec_out,
+             (const uint32_t*)d_dec_ofl, d_sig, d_sst);
+  } else if (ns) {
     LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
              d_sst);
+  }
   const PkSource src{by_index ? d_rows : d_pks, by_index ? (const uint32_t*)d_pks : nullptr, ctx->d_table,
                      ctx->table_n};
   const uint32_t agg_grid = nj < 16384u ? nj : 16384u;

@@ -55,7 +55,11 @@
 #define LB_LP_PROG_MSM_BITS0 10  // a lone call's MSM bit sums: 8 one-lane Jacobian points -> their sum
 #define LB_LP_PROG_MSM_BITS1 11  // ... 8 partial sums -> one
 #define LB_LP_PROG_MSM_BITS2 12  // ... 8 partial sums -> G_p, one-lane Jacobian (k_lp_msm_bits)
-#define LB_LP_NPROGS 13
+#define LB_LP_PROG_SIG_DECODE 13  // a small same-message package's signature decode (k_lp_dec, 8 rows)
+#define LB_LP_NPROGS 14
+#define LB_LP_DEC_ROWS 8          // gen_lp.py DEC_ROWS
+#define LB_LP_DEC_REGS 128        // gen_lp.py MAX_REGS_DEC
+#define LB_SM_DEC_MAX 512         // packages of at most this many signatures decode on k_lp_dec
 #define LB_MSM_BITS_GROUP 8      // lpgen/bls.py MSM_BITS_GROUP
 #define LB_MSM_BITS_INST (LB_MSM_POS * (LB_MSM_NB / 2 / LB_MSM_BITS_GROUP))  // level-0 instances: 33 x 64
 #define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf
@@ -127,6 +131,24 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_msm_bits(con
                                                                              uint32_t n_out,
                                                                              const uint32_t* __restrict__ in16,
                                                                              uint32_t* __restrict__ out16);
+// A small same-message package's signature decode (bls_host.hip sm path): k_sm_dec_prep parses
+// every signature's bytes (g2_deserialize's encoding rules) into the program's records, flags and
+// a pre-status; k_lp_dec runs the sig_decode program per signature (one 8-row workgroup);
+// k_sm_dec_finish forms k_decode_sigs' outputs (point, status) from them.
+__global__ void __launch_bounds__(256) k_sm_dec_prep(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint32_t* __restrict__ sig_off, uint32_t* __restrict__ in16,
+                                                     uint32_t* __restrict__ fl, uint8_t* __restrict__ pre);
+__global__ void __launch_bounds__(LB_LP_DEC_ROWS * 16) k_lp_dec(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                const uint32_t* __restrict__ in16,
+                                                                const uint32_t* __restrict__ fl,
+                                                                uint32_t* __restrict__ out16,
+                                                                uint32_t* __restrict__ ofl);
+__global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t* __restrict__ pre,
+                                                       const uint32_t* __restrict__ in16,
+                                                       const uint32_t* __restrict__ fl,
+                                                       const uint32_t* __restrict__ out16,
+                                                       const uint32_t* __restrict__ ofl, g2j* __restrict__ sig,
+                                                       uint8_t* __restrict__ status);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,

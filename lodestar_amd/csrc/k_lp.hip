@@ -900,6 +900,105 @@ __global__ void __launch_bounds__(LB_LP_TPB, LB_LP_VERIFY_WPE) k_lp_msm_bits(con
   lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * n_out * 16, s_fl);
 }
 
+__global__ void __launch_bounds__(256) k_sm_dec_prep(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint32_t* __restrict__ sig_off, uint32_t* __restrict__ in16,
+                                                     uint32_t* __restrict__ fl, uint8_t* __restrict__ pre) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // g2_deserialize's encoding rules (bls_curve.h) up to its curve arithmetic
+  const uint32_t a = sig_off[i], len = sig_off[i + 1] - a;
+  const uint8_t* b = sigs + a;
+  fp v[4];  // x.c0, x.c1, y.c0, y.c1 (one-lane Montgomery form)
+#pragma unroll
+  for (int c = 0; c < 4; c++) fp_zero(v[c]);
+  bool inf = false, sign = false, comp = false;
+  uint8_t st = LB_ST_OK;
+  if (len == 0) {
+    st = LB_ST_BAD_ENCODING;
+  } else {
+    const uint8_t f = b[0];
+    comp = (f & 0x80) != 0;
+    if (len != (comp ? 96u : 192u)) {
+      st = LB_ST_BAD_ENCODING;
+    } else if (comp) {
+      if (f & 0x40) {
+        if ((f & 0x3f) == 0 && bytes_zero(b + 1, 95))
+          inf = true;
+        else
+          st = LB_ST_BAD_ENCODING;
+      } else {
+        if (!fp_read_masked(v[1], b, true) || !fp_read_masked(v[0], b + 48, false)) st = LB_ST_BAD_ENCODING;
+        sign = (f & 0x20) != 0;
+      }
+    } else if (f & 0xe0) {
+      if ((f & 0x40) && (f & 0x3f) == 0 && bytes_zero(b + 1, 191))
+        inf = true;
+      else
+        st = LB_ST_BAD_ENCODING;
+    } else if (!fp_read_masked(v[1], b, false) || !fp_read_masked(v[0], b + 48, false) ||
+               !fp_read_masked(v[3], b + 96, false) || !fp_read_masked(v[2], b + 144, false)) {
+      st = LB_ST_BAD_ENCODING;
+    }
+  }
+  if (st != LB_ST_OK || inf) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) fp_zero(v[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) in16[(size_t)(4 * i + c) * 16 + j] = v[c].l[j];
+#pragma unroll
+    for (int j = 12; j < 16; j++) in16[(size_t)(4 * i + c) * 16 + j] = 0u;
+  }
+  fl[3 * i] = inf ? 1u : 0u;  // (lpgen/bls.py SIG_DECODE_FLAGS order)
+  fl[3 * i + 1] = sign ? 1u : 0u;
+  fl[3 * i + 2] = comp ? 1u : 0u;
+  pre[i] = st;
+}
+
+__global__ void __launch_bounds__(LB_LP_DEC_ROWS * 16) k_lp_dec(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                const uint32_t* __restrict__ in16,
+                                                                const uint32_t* __restrict__ fl,
+                                                                uint32_t* __restrict__ out16,
+                                                                uint32_t* __restrict__ ofl) {
+  __shared__ LpSharedT<LB_LP_DEC_REGS> S;
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* in = in16 + (size_t)b * 4 * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, fl + 3 * (size_t)b, out16 + (size_t)b * 2 * 16, ofl + 2 * (size_t)b);
+}
+
+__global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t* __restrict__ pre,
+                                                       const uint32_t* __restrict__ in16,
+                                                       const uint32_t* __restrict__ fl,
+                                                       const uint32_t* __restrict__ out16,
+                                                       const uint32_t* __restrict__ ofl, g2j* __restrict__ sig,
+                                                       uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = pre[i];
+  g2j P;
+  jac_set_inf(P);  // (k_decode_sigs: infinity unless the encoding decoded; infinity itself is OK)
+  if (st == LB_ST_OK && !fl[3 * i]) {
+    if (!ofl[2 * i]) {
+      st = LB_ST_NOT_ON_CURVE;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 12; j++) {
+        P.X.c0.l[j] = in16[(size_t)(4 * i) * 16 + j];
+        P.X.c1.l[j] = in16[(size_t)(4 * i + 1) * 16 + j];
+        P.Y.c0.l[j] = out16[(size_t)(2 * i) * 16 + j];
+        P.Y.c1.l[j] = out16[(size_t)(2 * i + 1) * 16 + j];
+      }
+      fone(P.Z);
+      if (!ofl[2 * i + 1]) st = LB_ST_NOT_IN_GROUP;  // (the point kept, as k_decode_sigs keeps it)
+    }
+  }
+  sig[i] = P;
+  status[i] = st;
+}
+
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {
   const uint32_t i = threadIdx.x;
   if (i >= 12) return;

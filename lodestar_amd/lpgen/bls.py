@@ -803,6 +803,39 @@ def mtail_program(partial: bool) -> Graph:
     return g
 
 
+SIG_DECODE_INPUTS = ["sx0", "sx1", "sy0", "sy1"]
+SIG_DECODE_FLAGS = ["sig_inf", "sig_sign", "sig_comp"]
+
+
+def sig_decode_program() -> Graph:
+    """Signature.fromBytes(validate=true)'s curve arithmetic for a small same-message package
+    (bls_host.hip; k_decode_sigs' one-lane chain, ~4 ms, as ~540 rounds on an 8-row workgroup):
+    inputs x (and y, uncompressed) in the one-lane form and the encoding's flags as
+    k_sm_dec_prep parsed them; outputs y in the one-lane form (the compressed point's root
+    with the sign rule, or the given y) and the flags on_curve and in_group -- the same
+    formulas as set_program's decompression."""
+    g = Graph("sig_decode")
+    v = {n: g.input(n) for n in SIG_DECODE_INPUTS}
+    fl = {n: g.input_flag(n) for n in SIG_DECODE_FLAGS}
+    sx = Fp2(v["sx0"], v["sx1"])
+    rhs = sx.sqr() * sx + c2(g, "LB_B2")
+    yc, sq = fp2_sqrt1(rhs)
+    flip = fp2_lex_largest(yc) ^ fl["sig_sign"]
+    yc = select(flip, -yc, yc)
+    yu = Fp2(v["sy0"], v["sy1"])
+    on_u = (yu.sqr() - rhs).is_zero()
+    comp = fl["sig_comp"]
+    sy = select(comp, yc, yu)
+    on_curve = (comp & sq) | (~comp & on_u)
+    in_group = g2_in_subgroup(Proj(sx, sy, Fp2.one(g)), fl["sig_inf"])
+    r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+    g.output("y0", sy.c0 * r384, canonical=True)
+    g.output("y1", sy.c1 * r384, canonical=True)
+    g.output_flag("on_curve", on_curve)
+    g.output_flag("in_group", in_group)
+    return g
+
+
 MSM_BITS_GROUP = 8  # k_msm.hip: bucket sums per instance of the lone call's bit-sum programs
 
 

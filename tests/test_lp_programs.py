@@ -351,3 +351,50 @@ def test_msm_bits_programs_against_oracle():
     outs1, _ = progs[1].run(outs0 + inf416 * 7, [])
     outs2, _ = progs[2].run(outs1 + inf416 * 7, [])
     assert outs2[4] == 0 and outs2[5] == 0
+
+
+def test_sig_decode_program_against_oracle():
+    """A small same-message package's signature decode (k_lp_dec): for compressed and
+    uncompressed encodings of valid signatures, an x with no curve point, a curve point
+    outside G2 and the infinity encoding -- the program's y (one-lane form), on_curve and
+    in_group equal the oracle's g2_from_bytes / g2_in_subgroup (the byte-level rules stay
+    with k_sm_dec_prep, as in k_lp_prep)."""
+    g = lpc.compile_graph(bls.sig_decode_program(), rows=8)
+    assert g.stats["regs"] <= 128
+    _, _, sigs = sample_sets(2)
+    r384 = pow(1 << 384, -1, P)
+
+    def run(x, y, flags):
+        outs, ofl = g.run([mont(v) for v in (x[0], x[1], y[0], y[1])], flags)
+        return (outs[0] * r384 % P, outs[1] * r384 % P), ofl
+    cases = []
+    for s in sigs:
+        pt = O.g2_from_bytes(s)
+        cases.append((s, pt))
+        cases.append((O.g2_to_bytes(pt, False), pt))
+    for s, pt in cases:
+        comp = len(s) == 96
+        sign = (s[0] >> 5) & 1 if comp else 0
+        y, ofl = run(pt[0], pt[1] if not comp else (0, 0), [0, sign, int(comp)])
+        assert y == pt[1] and ofl == [1, 1]
+    # an x whose x^3 + b has no root: not on the curve (compressed); a curve point outside G2
+    k = 1
+    while O.f2_sqrt(O.f2_add(O.f2_mul(O.f2_sqr((k, 0)), (k, 0)), (4, 4))) is not None:
+        k += 1
+    _, ofl = run((k, 0), (0, 0), [0, 0, 1])
+    assert ofl[0] == 0
+    k = 1
+    while True:
+        x = (k, 1)
+        y = O.f2_sqrt(O.f2_add(O.f2_mul(O.f2_sqr(x), x), (4, 4)))
+        if y is not None and not O.g2_in_subgroup((x, y)):
+            break
+        k += 1
+    yo, ofl = run(x, (0, 0), [0, int(O.f2_lex_largest(y)), 1])
+    assert yo == y and ofl == [1, 0]
+    _, ofl = run(x, y, [0, 0, 0])  # (uncompressed: the same point as given)
+    assert ofl == [1, 0]
+    _, ofl = run(x, O.f2_add(y, (1, 0)), [0, 0, 0])  # uncompressed, y off the curve
+    assert ofl[0] == 0
+    _, ofl = run((0, 0), (0, 0), [1, 0, 1])  # infinity: in the group
+    assert ofl[1] == 1
