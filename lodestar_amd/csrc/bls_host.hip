@@ -323,6 +323,9 @@ struct lb_ctx {
   // same-message packages of at most LB_SM_DEC_MAX signatures decode them as round programs
   // (k_lp_dec; LB_SM_LP_DECODE=0: k_decode_sigs always)
   bool sm_lp_decode = true;
+  // lone pipeline calls of at most LB_LP_DEC_MAX sets decode their signatures the same way
+  // (LB_LP_DECODE=0: k_decode_sigs)
+  bool lp_decode = true;
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -707,6 +710,14 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   }
   uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns * lsplit) : nullptr;
   fp12* d_Fparts = steps && lsplit > 1 ? ws.take<fp12>((size_t)(n_req ? n_req : 1) * lsplit) : nullptr;
+  // a lone mid-size call's signature decode as round programs (k_sm_dec_prep / k_lp_dec / k_sm_dec_finish)
+  const bool dec_lp = lone && !d_sig_pre && n_sets && n_sets <= LB_LP_DEC_MAX && ctx->lp_decode;
+  uint32_t* d_dec_in = dec_lp ? ws.take<uint32_t>((size_t)ns * 4 * 16) : nullptr;
+  uint32_t* d_dec_fl = dec_lp ? ws.take<uint32_t>((size_t)ns * 3) : nullptr;
+  uint32_t* d_dec_out = dec_lp ? ws.take<uint32_t>((size_t)ns * 2 * 16) : nullptr;
+  uint32_t* d_dec_ofl = dec_lp ? ws.take<uint32_t>((size_t)ns * 2) : nullptr;
+  uint8_t* d_dec_pre = dec_lp ? ws.take<uint8_t>(ns) : nullptr;
+  if (dec_lp) LB_TRY(lp_ensure(ctx));
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
   // the level products' two stages (k_level_part's partials, the first k_level_wc pass's output)
   const bool level_wc = steps && merged && ctx->level_wc;
@@ -778,9 +789,21 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("miller_sets", 1, k_miller_sets, blocks_for(n_sets), TPB, n_sets, (const g1j*)d_rpk, (const g2j*)d_h,
              d_f);
   if (n_sets) {
-    if (!d_sig_pre)
+    if (!d_sig_pre && dec_lp) {
+      // (a lone mid-size call: the signatures' decode as round programs, k_lp_dec -- its one-lane
+      // chain is ~5.7 ms whatever the count below the GPU's width)
+      LB_STAGE("decode_sigs", 0, k_sm_dec_prep, blocks_for(n_sets, 256), 256u, n_sets, d_sigs, d_sig_off, d_dec_in,
+               d_dec_fl, d_dec_pre);
+      LB_STAGE("decode_sigs", 0, k_lp_dec, n_sets, LB_LP_DEC_ROWS * 16u,
+               ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_SIG_DECODE].off, n_sets, (const uint32_t*)d_dec_in,
+               (const uint32_t*)d_dec_fl, d_dec_out, d_dec_ofl);
+      LB_STAGE("decode_sigs", 0, k_sm_dec_finish, blocks_for(n_sets, 256), 256u, n_sets, (const uint8_t*)d_dec_pre,
+               (const uint32_t*)d_dec_in, (const uint32_t*)d_dec_fl, (const uint32_t*)d_dec_out,
+               (const uint32_t*)d_dec_ofl, d_sig, d_sig_st, (const uint8_t*)d_single);
+    } else if (!d_sig_pre) {
       LB_STAGE("decode_sigs", 0, k_decode_sigs, blocks_for(n_sets), TPB, n_sets, d_sigs, d_sig_off,
                (const uint8_t*)d_single, d_sig, d_sig_st);
+    }
     if (!use_msm)
       LB_STAGE("scalar_sig", 0, k_scalar_sig, blocks_for(n_sets), TPB, n_sets, d_seed, (const g2j*)d_sig,
                (const uint8_t*)d_sig_st, d_rsig, (const uint8_t*)nullptr);
@@ -1066,7 +1089,8 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   const size_t lvl = 63 * (lvl_per + (lvl_per + LB_LVL_GROUP - 1) / LB_LVL_GROUP) * sizeof(fp12) + 2 * 63 * lvl_per +
                      4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
-         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576;
+         (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576 +
+         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1) + 5 * 256 : 0);  // (+ a lone call's decode records)
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1396,6 +1420,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_WIDE_TAIL")) ctx->wide_tail = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_BITS_LP")) ctx->msm_bits_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_SM_LP_DECODE")) ctx->sm_lp_decode = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_DECODE")) ctx->lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
@@ -2774,7 +2799,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
              (const uint32_t*)d_dec_in, (const uint32_t*)d_dec_fl, d_dec_out, d_dec_ofl);
     LB_STAGE("sm_decode", 0, k_sm_dec_finish, blocks_for(ns, 256), 256u, ns, (const uint8_t*)d_dec_pre,
              (const uint32_t*)d_dec_in, (const uint32_t*)d_dec_fl, (const uint32_t*)d_dec_out,
-             (const uint32_t*)d_dec_ofl, d_sig, d_sst);
+             (const uint32_t*)d_dec_ofl, d_sig, d_sst, (const uint8_t*)nullptr);
   } else if (ns) {
     LB_STAGE("sm_decode", 0, k_decode_sigs, blocks_for(ns), TPB, ns, d_sigs, d_sigo, (const uint8_t*)nullptr, d_sig,
              d_sst);

@@ -60,6 +60,7 @@
 #define LB_LP_DEC_ROWS 8          // gen_lp.py DEC_ROWS
 #define LB_LP_DEC_REGS 128        // gen_lp.py MAX_REGS_DEC
 #define LB_SM_DEC_MAX 512         // packages of at most this many signatures decode on k_lp_dec
+#define LB_LP_DEC_MAX 16384       // ... and lone pipeline calls of at most this many sets
 #define LB_MSM_BITS_GROUP 8      // lpgen/bls.py MSM_BITS_GROUP
 #define LB_MSM_BITS_INST (LB_MSM_POS * (LB_MSM_NB / 2 / LB_MSM_BITS_GROUP))  // level-0 instances: 33 x 64
 #define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf
@@ -148,7 +149,8 @@ __global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t
                                                        const uint32_t* __restrict__ fl,
                                                        const uint32_t* __restrict__ out16,
                                                        const uint32_t* __restrict__ ofl, g2j* __restrict__ sig,
-                                                       uint8_t* __restrict__ status);
+                                                       uint8_t* __restrict__ status,
+                                                       const uint8_t* __restrict__ single_flag);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,

@@ -974,10 +974,13 @@ __global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t
                                                        const uint32_t* __restrict__ fl,
                                                        const uint32_t* __restrict__ out16,
                                                        const uint32_t* __restrict__ ofl, g2j* __restrict__ sig,
-                                                       uint8_t* __restrict__ status) {
+                                                       uint8_t* __restrict__ status,
+                                                       const uint8_t* __restrict__ single_flag) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st = pre[i];
+  // (k_decode_sigs' single-set rule: a 1-set request's core verify rejects the infinite signature)
+  if (st == LB_ST_OK && fl[3 * i] && single_flag && single_flag[i]) st = LB_ST_ZERO_SIGNATURE;
   g2j P;
   jac_set_inf(P);  // (k_decode_sigs: infinity unless the encoding decoded; infinity itself is OK)
   if (st == LB_ST_OK && !fl[3 * i]) {

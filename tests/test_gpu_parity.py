@@ -492,6 +492,8 @@ def test_steps_uniform_and_single_requests_vs_c_oracle(device, layout, level, sp
     off[-1] = n
     seed = hashlib.sha256(b"steps-rows").digest()
     env = {"LB_STEP_SPLIT": split} if split else {}
+    if split == "1":  # (and the signatures decoded by k_decode_sigs instead of the round programs)
+        env["LB_LP_DECODE"] = "0"
     dev = _device_with_env(LB_MILLER="lines", LB_LEVEL=level, **env)
     try:
         ro = np.array(off, np.uint32)
