@@ -326,6 +326,7 @@ struct lb_ctx {
   // lone pipeline calls of at most LB_LP_DEC_MAX sets decode their signatures the same way
   // (LB_LP_DECODE=0: k_decode_sigs)
   bool lp_decode = true;
+  bool lp_hash_finish = true;  // (LB_LP_HASH_FINISH: the same calls' hash finish as round programs)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -718,6 +719,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_dec_ofl = dec_lp ? ws.take<uint32_t>((size_t)ns * 2) : nullptr;
   uint8_t* d_dec_pre = dec_lp ? ws.take<uint8_t>(ns) : nullptr;
   if (dec_lp) LB_TRY(lp_ensure(ctx));
+  // ... and, up to LB_LP_HF_MAX sets, its hash finish (k_hf_prep / k_lp_hf / k_hf_finish; above that
+  // the workgroups queue: 1,536 / 2,048 sets 13.4 -> 11.0 / 11.8 ms, 4,704 (C5) 16.1 -> 17.4,
+  // profiles/r06/orgs_probe_r06hf.json; LB_LP_HASH_FINISH=0: k_hash_finish)
+  const bool hf_lp = lone && n_sets && n_sets <= LB_LP_HF_MAX && ctx->lp_hash_finish;
+  uint32_t* d_hf_in = hf_lp ? ws.take<uint32_t>((size_t)ns * 12 * 16) : nullptr;
+  uint32_t* d_hf_out = hf_lp ? ws.take<uint32_t>((size_t)ns * 6 * 16) : nullptr;
+  if (hf_lp) LB_TRY(lp_ensure(ctx));
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
   // the level products' two stages (k_level_part's partials, the first k_level_wc pass's output)
   const bool level_wc = steps && merged && ctx->level_wc;
@@ -740,7 +748,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   LB_TRY(stream_wait(ctx, sl, 0, 1, 0));
   if (n_sets) {
     LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
-    LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, d_q, d_h);
+    if (hf_lp) {  // (a lone mid-size call: clear_cofactor(Q0 + Q1) as round programs, k_lp_hf)
+      LB_STAGE("hash_finish", 1, k_hf_prep, blocks_for(n_sets * 12u, 256), 256u, n_sets, (const g2j*)d_q, d_hf_in);
+      LB_STAGE("hash_finish", 1, k_lp_hf, n_sets, LB_LP_HF_ROWS * 16u,
+               ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_HASH_FINISH].off, n_sets, (const uint32_t*)d_hf_in, d_hf_out);
+      LB_STAGE("hash_finish", 1, k_hf_finish, blocks_for(n_sets * 6u, 256), 256u, n_sets, (const uint32_t*)d_hf_out,
+               d_h);
+    } else {
+      LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, d_q, d_h);
+    }
   }
   LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
   if (steps) {  // size-descending order and row offsets (before stream 1's lines)
@@ -1090,7 +1106,8 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
                      4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
          (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576 +
-         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1) + 5 * 256 : 0);  // (+ a lone call's decode records)
+         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1 + 18 * 64) + 7 * 256 : 0);  // (+ a lone call's
+                                                                                      // decode / hash records)
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1342,7 +1359,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_req_join, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_lp_hf, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_msm_bits<TPB>, (const void*)k_msm_bits<LB_MSM_BITS_TPB>,
                            (const void*)k_decode_sigs,
@@ -1421,6 +1438,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_MSM_BITS_LP")) ctx->msm_bits_lp = atoi(e) != 0;
   if (const char* e = getenv("LB_SM_LP_DECODE")) ctx->sm_lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_DECODE")) ctx->lp_decode = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;

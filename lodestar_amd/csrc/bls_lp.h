@@ -56,7 +56,10 @@
 #define LB_LP_PROG_MSM_BITS1 11  // ... 8 partial sums -> one
 #define LB_LP_PROG_MSM_BITS2 12  // ... 8 partial sums -> G_p, one-lane Jacobian (k_lp_msm_bits)
 #define LB_LP_PROG_SIG_DECODE 13  // a small same-message package's signature decode (k_lp_dec, 8 rows)
-#define LB_LP_NPROGS 14
+#define LB_LP_PROG_HASH_FINISH 14  // a lone mid-size call's clear_cofactor(Q0 + Q1) (k_lp_hf, 16 rows)
+#define LB_LP_NPROGS 15
+#define LB_LP_HF_ROWS 16           // gen_lp.py HF_ROWS
+#define LB_LP_HF_MAX 3072          // lone calls of at most this many sets finish their hash on k_lp_hf
 #define LB_LP_DEC_ROWS 8          // gen_lp.py DEC_ROWS
 #define LB_LP_DEC_REGS 128        // gen_lp.py MAX_REGS_DEC
 #define LB_SM_DEC_MAX 512         // packages of at most this many signatures decode on k_lp_dec
@@ -151,6 +154,15 @@ __global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t
                                                        const uint32_t* __restrict__ ofl, g2j* __restrict__ sig,
                                                        uint8_t* __restrict__ status,
                                                        const uint8_t* __restrict__ single_flag);
+// A lone mid-size call's hash finish (bls_host.hip): Q0, Q1 of every set into records
+// (k_hf_prep), the hash_finish program per set on a 16-row workgroup (k_lp_hf), H back into
+// Jacobian points (k_hf_finish)
+__global__ void __launch_bounds__(256) k_hf_prep(uint32_t n, const g2j* __restrict__ q, uint32_t* __restrict__ in16);
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hf(const uint32_t* __restrict__ prog, uint32_t n,
+                                                              const uint32_t* __restrict__ in16,
+                                                              uint32_t* __restrict__ out16);
+__global__ void __launch_bounds__(256) k_hf_finish(uint32_t n, const uint32_t* __restrict__ out16,
+                                                   g2j* __restrict__ h);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,

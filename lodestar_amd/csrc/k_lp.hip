@@ -1002,6 +1002,39 @@ __global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t
   status[i] = st;
 }
 
+__global__ void __launch_bounds__(256) k_hf_prep(uint32_t n, const g2j* __restrict__ q, uint32_t* __restrict__ in16) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (set, record): 12 records a set
+  if (t >= n * 12u) return;
+  const uint32_t i = t / 12u, c = t % 12u;
+  const fp v = (&q[2 * i + c / 6u].X.c0)[c % 6u];
+#pragma unroll
+  for (int j = 0; j < 12; j++) in16[(size_t)t * 16 + j] = v.l[j];
+#pragma unroll
+  for (int j = 12; j < 16; j++) in16[(size_t)t * 16 + j] = 0u;
+}
+
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hf(const uint32_t* __restrict__ prog, uint32_t n,
+                                                              const uint32_t* __restrict__ in16,
+                                                              uint32_t* __restrict__ out16) {
+  __shared__ LpSharedT<LB_LP_DEC_REGS> S;
+  __shared__ uint32_t s_fl[4];
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* in = in16 + (size_t)b * 12 * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * 6 * 16, s_fl);
+}
+
+__global__ void __launch_bounds__(256) k_hf_finish(uint32_t n, const uint32_t* __restrict__ out16,
+                                                   g2j* __restrict__ h) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (set, coordinate): 6 a set
+  if (t >= n * 6u) return;
+  const uint32_t i = t / 6u, c = t % 6u;
+  fp v;
+#pragma unroll
+  for (int j = 0; j < 12; j++) v.l[j] = out16[(size_t)t * 16 + j];
+  (&h[i].X.c0)[c] = v;
+}
+
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {
   const uint32_t i = threadIdx.x;
   if (i >= 12) return;

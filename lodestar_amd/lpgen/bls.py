@@ -836,6 +836,26 @@ def sig_decode_program() -> Graph:
     return g
 
 
+def hash_finish_program() -> Graph:
+    """hash_to_G2's second half for a lone mid-size call (k_hash_finish's one-lane chain, ~4.7 ms,
+    as ~300 rounds on a 16-row workgroup): inputs Q0, Q1 (the two mapped points, Jacobian, one-lane
+    form, as k_hash_half writes them; Z = 0 is infinity); output H = clear_cofactor(Q0 + Q1),
+    Jacobian in the one-lane form (k_lines_rows' input)."""
+    g = Graph("hash_finish")
+    F = Ops(g, True)
+    zero, one = Fp2.zero(g), Fp2.one(g)
+    pts = []
+    for i in range(2):
+        X, Y, Z = (Fp2(g.input("Q%d_%s0" % (i, c)), g.input("Q%d_%s1" % (i, c))) for c in "XYZ")
+        pts.append(select(Z.is_zero(), Proj(zero, one, zero), proj_from_jac(Jac(X, Y, Z))))
+    J = proj_to_jac(clear_cofactor_g2(proj_add(F, pts[0], pts[1])))
+    r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+    for v, c in ((J.X, "X"), (J.Y, "Y"), (J.Z, "Z")):
+        g.output("H_%s0" % c, v.c0 * r384, canonical=True)
+        g.output("H_%s1" % c, v.c1 * r384, canonical=True)
+    return g
+
+
 MSM_BITS_GROUP = 8  # k_msm.hip: bucket sums per instance of the lone call's bit-sum programs
 
 

@@ -398,3 +398,36 @@ def test_sig_decode_program_against_oracle():
     assert ofl[0] == 0
     _, ofl = run((0, 0), (0, 0), [1, 0, 1])  # infinity: in the group
     assert ofl[1] == 1
+
+
+def test_hash_finish_program_against_oracle():
+    """A lone mid-size call's hash finish (k_lp_hf): Q0, Q1 -- the two mapped points of a
+    message, as one-lane Jacobian inputs with arbitrary Z -- give H = clear_cofactor(Q0 + Q1),
+    output Jacobian in the one-lane form, equal to the oracle's hash_to_g2; Q0 = -Q1 gives
+    infinity (Z = 0)."""
+    import random
+    rnd = random.Random(5)
+    g = lpc.compile_graph(bls.hash_finish_program(), rows=16)
+    assert g.stats["regs"] <= 128
+    r384 = pow(1 << 384, -1, P)
+
+    def f2mul(a, b):
+        return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+    def f2inv(a):
+        n = pow((a[0] * a[0] + a[1] * a[1]) % P, -1, P)
+        return (a[0] * n % P, -a[1] * n % P)
+    for msg in (b"\x00" * 32, bytes(range(32))):
+        u0, u1 = O.hash_to_field_fp2(msg, 2, O.DST_POP)
+        q0 = O.iso_map_g2(O.map_to_curve_sswu(u0))
+        q1 = O.iso_map_g2(O.map_to_curve_sswu(u1))
+        ins = _jac_inputs(q0, rnd.randrange(1, P)) + _jac_inputs(q1, rnd.randrange(1, P))
+        outs, _ = g.run([mont(v) for v in ins], [])
+        X0, X1, Y0, Y1, Z0, Z1 = (v * r384 % P for v in outs)
+        zi = f2inv((Z0, Z1))
+        zi2 = f2mul(zi, zi)
+        assert (f2mul((X0, X1), zi2), f2mul((Y0, Y1), f2mul(zi2, zi))) == O.hash_to_g2(msg)
+    q = O.g2_mul(O.G2, 7)
+    qn = (q[0], ((-q[1][0]) % P, (-q[1][1]) % P))
+    outs, _ = g.run([mont(v) for v in _jac_inputs(q, 3) + _jac_inputs(qn, 5)], [])
+    assert outs[4] == 0 and outs[5] == 0
