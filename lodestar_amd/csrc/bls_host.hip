@@ -327,6 +327,7 @@ struct lb_ctx {
   // (LB_LP_DECODE=0: k_decode_sigs)
   bool lp_decode = true;
   bool lp_hash_finish = true;  // (LB_LP_HASH_FINISH: the same calls' hash finish as round programs)
+  bool lp_lines = true;  // (LB_LP_LINES: a lone steps call's lines as round programs, up to LB_LP_LINES_MAX sets)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -726,6 +727,12 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_hf_in = hf_lp ? ws.take<uint32_t>((size_t)ns * 12 * 16) : nullptr;
   uint32_t* d_hf_out = hf_lp ? ws.take<uint32_t>((size_t)ns * 6 * 16) : nullptr;
   if (hf_lp) LB_TRY(lp_ensure(ctx));
+  // ... and, up to LB_LP_LINES_MAX sets of the steps organisation, its lines (k_lines_prep /
+  // k_lp_lines / k_lines_store; LB_LP_LINES=0: k_lines_rows)
+  const bool lines_lp = steps && lone && n_sets <= LB_LP_LINES_MAX && ctx->lp_lines;
+  uint32_t* d_ll_in = lines_lp ? ws.take<uint32_t>((size_t)ns * 9 * 16) : nullptr;
+  uint32_t* d_ll_out = lines_lp ? ws.take<uint32_t>((size_t)ns * LB_LP_LINES_NOUT * 16) : nullptr;
+  if (lines_lp) LB_TRY(lp_ensure(ctx));
   fp12* d_Pl = steps ? ws.take<fp12>(63) : nullptr;
   // the level products' two stages (k_level_part's partials, the first k_level_wc pass's output)
   const bool level_wc = steps && merged && ctx->level_wc;
@@ -783,7 +790,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
              (const uint8_t*)d_single, d_pk_st, d_rpk);
   }
   LB_TRY(stream_wait(ctx, sl, 0, 1, 1));
-  if (steps) {
+  if (steps && lines_lp) {
+    // (a lone mid-size call: each slot's 68 lines as a round program, k_lp_lines)
+    LB_STAGE("lines", 1, k_lines_prep, blocks_for(n_sets * 9u, 256), 256u, n_sets, rows, d_req_off, (const g1j*)d_rpk,
+             (const g2j*)d_h, d_ll_in);
+    LB_STAGE("lines", 1, k_lp_lines, n_sets, LB_LP_HF_ROWS * 16u, ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_LINES].off, n_sets,
+             (const uint32_t*)d_ll_in, d_ll_out);
+    LB_STAGE("lines", 1, k_lines_store, (uint32_t)(((size_t)n_sets * LB_MILLER_LINES * 72 + 255) / 256), 256u, n_sets,
+             n_pairs, (const uint32_t*)d_ll_out, d_lines);
+  } else if (steps) {
     if (ctx->lines_waves == 1)
       LB_STAGE("lines", 1, k_lines_rows<1>, blocks_for(n_sets), TPB, n_sets, n_pairs, rows, d_req_off,
                (const g1j*)d_rpk, d_h, d_lines);
@@ -1106,8 +1121,9 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
                      4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
          (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576 +
-         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1 + 18 * 64) + 7 * 256 : 0);  // (+ a lone call's
+         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1 + 18 * 64) + 7 * 256 : 0) +  // (+ a lone call's
                                                                                       // decode / hash records)
+         (ns <= LB_LP_LINES_MAX ? ns * (9 + LB_LP_LINES_NOUT) * 64 + 2 * 256 : 0);  // (+ its line records)
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1359,7 +1375,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_req_join, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_lp_hf, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_lp_hf, (const void*)k_lp_lines, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_msm_bits<TPB>, (const void*)k_msm_bits<LB_MSM_BITS_TPB>,
                            (const void*)k_decode_sigs,
@@ -1439,6 +1455,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_SM_LP_DECODE")) ctx->sm_lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_DECODE")) ctx->lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_LINES")) ctx->lp_lines = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;

@@ -57,7 +57,10 @@
 #define LB_LP_PROG_MSM_BITS2 12  // ... 8 partial sums -> G_p, one-lane Jacobian (k_lp_msm_bits)
 #define LB_LP_PROG_SIG_DECODE 13  // a small same-message package's signature decode (k_lp_dec, 8 rows)
 #define LB_LP_PROG_HASH_FINISH 14  // a lone mid-size call's clear_cofactor(Q0 + Q1) (k_lp_hf, 16 rows)
-#define LB_LP_NPROGS 15
+#define LB_LP_PROG_LINES 15  // a lone mid-size call's Miller lines of one pair (k_lp_lines, 16 rows)
+#define LB_LP_NPROGS 16
+#define LB_LP_LINES_MAX 5120  // lone steps calls of at most this many sets store their lines via k_lp_lines (6,144: -0.5 ms)
+#define LB_LP_LINES_NOUT (68 * 6)
 #define LB_LP_HF_ROWS 16           // gen_lp.py HF_ROWS
 #define LB_LP_HF_MAX 3072          // lone calls of at most this many sets finish their hash on k_lp_hf
 #define LB_LP_DEC_ROWS 8          // gen_lp.py DEC_ROWS
@@ -163,6 +166,17 @@ __global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hf(const uint32_t* __
                                                               uint32_t* __restrict__ out16);
 __global__ void __launch_bounds__(256) k_hf_finish(uint32_t n, const uint32_t* __restrict__ out16,
                                                    g2j* __restrict__ h);
+// A lone mid-size steps call's lines (bls_host.hip): slot q's pair (r pk, H) into records
+// (k_lines_prep, the row layout of k_lines_rows), the lines program per slot on a 16-row
+// workgroup (k_lp_lines), its 68 lines into the SoA line store at slot q (k_lines_store)
+__global__ void __launch_bounds__(256) k_lines_prep(uint32_t n_sets, Rows R, const uint32_t* __restrict__ req_off,
+                                                    const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                    uint32_t* __restrict__ in16);
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_lines(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                 const uint32_t* __restrict__ in16,
+                                                                 uint32_t* __restrict__ out16);
+__global__ void __launch_bounds__(256) k_lines_store(uint32_t n_sets, uint32_t n_pairs, const uint32_t* __restrict__ out16,
+                                                     uint32_t* __restrict__ lines);
 // final_exp(F) == 1 of 12 one-lane records (lb_gt_check's combined product): out[0]
 __global__ void __launch_bounds__(LB_LP_TPB) k_lp_final_lane(const uint32_t* __restrict__ prog,
                                                              const uint32_t* __restrict__ in16,

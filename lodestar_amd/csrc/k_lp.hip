@@ -1035,6 +1035,58 @@ __global__ void __launch_bounds__(256) k_hf_finish(uint32_t n, const uint32_t* _
   (&h[i].X.c0)[c] = v;
 }
 
+// slot q -> (row i, position r) of the steps row layout (k_steps.hip slot_row)
+LB_DEV void lines_slot_row(const Rows& R, uint32_t q, uint32_t& i, uint32_t& r) {
+  uint32_t lo = 0, hi = R.meta[0];
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (R.rowoff[mid] <= q)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  i = lo;
+  r = q - R.rowoff[lo];
+}
+
+__global__ void __launch_bounds__(256) k_lines_prep(uint32_t n_sets, Rows R, const uint32_t* __restrict__ req_off,
+                                                    const g1j* __restrict__ P, const g2j* __restrict__ Q,
+                                                    uint32_t* __restrict__ in16) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (slot, record): P's 3 + H's 6
+  if (t >= n_sets * 9u) return;
+  const uint32_t q = t / 9u, c = t % 9u;
+  uint32_t i, r;
+  lines_slot_row(R, q, i, r);
+  const uint32_t s = req_off[R.inv[r]] + i;
+  const fp v = c < 3u ? (&P[s].X)[c] : (&Q[s].X.c0)[c - 3u];
+#pragma unroll
+  for (int j = 0; j < 12; j++) in16[(size_t)t * 16 + j] = v.l[j];
+#pragma unroll
+  for (int j = 12; j < 16; j++) in16[(size_t)t * 16 + j] = 0u;
+}
+
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_lines(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                 const uint32_t* __restrict__ in16,
+                                                                 uint32_t* __restrict__ out16) {
+  __shared__ LpSharedRtail S;
+  __shared__ uint32_t s_fl[4];
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* in = in16 + (size_t)b * 9 * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * LB_LP_LINES_NOUT * 16, s_fl);
+}
+
+__global__ void __launch_bounds__(256) k_lines_store(uint32_t n_sets, uint32_t n_pairs, const uint32_t* __restrict__ out16,
+                                                     uint32_t* __restrict__ lines) {
+  // thread (word w of line j, slot q): consecutive threads take consecutive slots, so the SoA
+  // stores coalesce (the record reads stride by a slot's 408 records)
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n_sets * LB_MILLER_LINES * 72) return;
+  const uint32_t q = (uint32_t)(t % n_sets), jw = (uint32_t)(t / n_sets);  // jw = j * 72 + w
+  const uint32_t j = jw / 72u, w = jw % 72u, e = w / 12u, limb = w % 12u;
+  lines[(size_t)jw * n_pairs + q] = out16[((size_t)q * LB_LP_LINES_NOUT + j * 6u + e) * 16 + limb];
+}
+
 __global__ void __launch_bounds__(64) k_records_to_fp12(const uint32_t* __restrict__ in16, fp12* __restrict__ F) {
   const uint32_t i = threadIdx.x;
   if (i >= 12) return;

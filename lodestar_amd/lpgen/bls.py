@@ -856,6 +856,34 @@ def hash_finish_program() -> Graph:
     return g
 
 
+def lines_program() -> Graph:
+    """The 68 Miller lines of one pair (r pk, H) for a lone mid-size call (k_lines_rows' one-lane
+    T-chain, ~3.3 ms, as ~210 rounds on a 16-row workgroup): inputs P (Jacobian G1) and H
+    (Jacobian G2) in the one-lane form; outputs the 68 lines (l0, l1, l4) in loop order, one-lane
+    form, as k_lines_rows stores them -- up to Fp2 factors (P and H stay projective: no
+    inversion), which the final exponentiation removes; an infinite P or H gives unit lines."""
+    g = Graph("lines")
+    P = Jac(*(g.input("P_%s" % c) for c in "XYZ"))
+    X, Y, Z = (Fp2(g.input("H_%s0" % c), g.input("H_%s1" % c)) for c in "XYZ")
+    void = g.is_zero(P.Z) | Z.is_zero()
+    Pl = g1_line_point(P)
+    Q = g2_homogeneous(Jac(X, Y, Z))
+    T = Q
+    r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+    lines = []
+    for i in range(62, -1, -1):
+        T, ln = miller_dbl_step(T, Pl)
+        lines.append(ln)
+        if (X_ABS >> i) & 1:
+            T, ln = miller_add_step(T, Q, Pl)
+            lines.append(ln)
+    for j, ln in enumerate(lines):
+        for k, v in enumerate(unit_line(g, void, ln)):
+            g.output("L%d_%d0" % (j, k), v.c0 * r384, canonical=True)
+            g.output("L%d_%d1" % (j, k), v.c1 * r384, canonical=True)
+    return g
+
+
 MSM_BITS_GROUP = 8  # k_msm.hip: bucket sums per instance of the lone call's bit-sum programs
 
 

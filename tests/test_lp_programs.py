@@ -431,3 +431,40 @@ def test_hash_finish_program_against_oracle():
     qn = (q[0], ((-q[1][0]) % P, (-q[1][1]) % P))
     outs, _ = g.run([mont(v) for v in _jac_inputs(q, 3) + _jac_inputs(qn, 5)], [])
     assert outs[4] == 0 and outs[5] == 0
+
+
+def test_lines_program_against_oracle():
+    """A lone mid-size call's lines (k_lp_lines): the 68 lines of (P, H) from projective inputs,
+    multiplied as k_step_acc does (a squaring per level, (l0, l1, l4) at c0.c0, c0.c1, c1.c1),
+    conjugated, give the oracle's pairing after the final exponentiation; an infinite P gives
+    unit lines."""
+    import random
+    rnd = random.Random(9)
+    g = lpc.compile_graph(bls.lines_program(), rows=16)
+    assert g.stats["regs"] <= 512
+    r384 = pow(1 << 384, -1, P)
+    Pt = O.g1_mul(O.G1, 12345)
+    Hq = O.g2_mul(O.G2, 678)
+    zp, zh = rnd.randrange(1, P), rnd.randrange(1, P)
+    px, py = Pt
+    ins = [px * zp * zp % P, py * pow(zp, 3, P) % P, zp] + _jac_inputs(Hq, zh)
+    outs, _ = g.run([mont(v) for v in ins], [])
+    vals = [v * r384 % P for v in outs]
+    zero2 = (0, 0)
+    f = None
+    j = 0
+    for i in range(62, -1, -1):
+        for rep in range(2):
+            if rep == 1 and not (bls.X_ABS >> i) & 1:
+                break
+            l0, l1, l4 = ((vals[6 * j + 2 * k], vals[6 * j + 2 * k + 1]) for k in range(3))
+            line = ((l0, l1, zero2), (zero2, l4, zero2))
+            if rep == 0 and f is not None:
+                f = O.f12_sqr(f)
+            f = line if f is None else O.f12_mul(f, line)
+            j += 1
+    assert j == 68
+    assert O.f12_eq(O.final_exp(O.f12_conj(f)), O.final_exp(O.miller_loop(Pt, Hq)))
+    outs, _ = g.run([mont(v) for v in [1, 1, 0] + _jac_inputs(Hq, zh)], [])  # P = O
+    vals = [v * r384 % P for v in outs]
+    assert all(vals[6 * j:6 * j + 6] == [1, 0, 0, 0, 0, 0] for j in range(68))
