@@ -327,6 +327,7 @@ struct lb_ctx {
   // (LB_LP_DECODE=0: k_decode_sigs)
   bool lp_decode = true;
   bool lp_hash_finish = true;  // (LB_LP_HASH_FINISH: the same calls' hash finish as round programs)
+  bool msm_short = true;  // (LB_MSM_SHORT: a lone mid-size call's MSM chunks of LB_MSM_T_LONE entries)
   bool lp_lines = true;  // (LB_LP_LINES: a lone steps call's lines as round programs, up to LB_LP_LINES_MAX sets)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
@@ -689,7 +690,11 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // bucket MSM workspace: keys + sorted entries (2 half-points x W windows per
   // set), histogram / cursors / offsets, chunk partials, bucket sums, G_p
   const size_t n_ent = use_msm ? 2 * (size_t)n_sets * LB_MSM_W : 0;
-  const size_t max_chunks = use_msm ? n_ent / LB_MSM_T + LB_MSM_BUCKETS : 0;
+  // (a lone mid-size call: chunks of LB_MSM_T_LONE entries -- k_msm_chunks' chains are one lane's
+  // mixed additions, 16 of them ~2.5 ms for C5; LB_MSM_SHORT=0 keeps LB_MSM_T)
+  const bool msm_short = use_msm && lone && n_sets <= 16384u && ctx->msm_short;
+  const uint32_t msm_T = msm_short ? LB_MSM_T_LONE : LB_MSM_T;
+  const size_t max_chunks = use_msm ? n_ent / msm_T + LB_MSM_BUCKETS : 0;
   uint32_t* d_mkeys = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
   uint32_t* d_msorted = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
   uint32_t* d_mhist = use_msm ? ws.take<uint32_t>(4 * (LB_MSM_BUCKETS + 1)) : nullptr;
@@ -850,13 +855,15 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_HIP(hipMemsetAsync(d_mhist, 0, (LB_MSM_BUCKETS + 1) * sizeof(uint32_t), sl.st[0]));
     LB_STAGE("msm_digits", 0, k_msm_scalars, n_req, TPB, n_req, d_req_off, d_seed, (const uint64_t*)nullptr,
              (const g2j*)d_sig, (const uint8_t*)d_sig_st, (const uint8_t*)d_pk_st, d_mkeys, d_mhist);
-    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, sl.st[0], (const uint32_t*)d_mhist, d_off, d_coff, d_cur);
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, sl.st[0], (const uint32_t*)d_mhist, d_off, d_coff, d_cur,
+                       msm_T);
     LB_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_msm_scatter, dim3(blocks_for((uint32_t)n_ent, 256)), dim3(256), 0, sl.st[0], (uint32_t)n_ent,
                        (const uint32_t*)d_mkeys, (const uint32_t*)d_off, d_cur, d_msorted);
     LB_HIP(hipGetLastError());
     LB_STAGE("msm_chunks", 0, k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks,
-             (const uint32_t*)d_off, (const uint32_t*)d_coff, (const uint32_t*)d_msorted, (const g2j*)d_sig, d_mcsum);
+             (const uint32_t*)d_off, (const uint32_t*)d_coff, (const uint32_t*)d_msorted, (const g2j*)d_sig, d_mcsum,
+             msm_T);
     const uint32_t bl = msm_wide ? LB_MSM_BLANES : 1u;
     LB_STAGE("msm_buckets", 0, k_msm_buckets, blocks_for(LB_MSM_BUCKETS * bl), TPB, (const uint32_t*)d_coff,
              (const g2j*)d_mcsum, d_mbsum, bl);
@@ -1104,7 +1111,8 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
   // (+ the bucket MSM: 2 W keys + 2 W sorted entries and 2 W / T chunk partials per set)
   // (+ the steps organisation: size histogram / cursors / gt / row offsets and the lanes' G values)
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 + 16 + 576 +
-                   (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 + (2 * LB_MSM_W * sizeof(g2j)) / LB_MSM_T + 1;
+                   (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 +
+                   (2 * LB_MSM_W * sizeof(g2j)) / (ns <= 16384u ? LB_MSM_T_LONE : LB_MSM_T) + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
   size_t per_req = sizeof(g2a) + 8 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
                    (size_t)LB_RTAIL_NIN * 64 + 4 + 2 * 256 / 64;  // (+ k_lp_rtail's records and flag)
@@ -1456,6 +1464,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LP_DECODE")) ctx->lp_decode = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_LINES")) ctx->lp_lines = atoi(e) != 0;
+  if (const char* e = getenv("LB_MSM_SHORT")) ctx->msm_short = atoi(e) != 0;
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
@@ -3161,11 +3170,11 @@ int lb_g2_msm(lb_ctx* ctx, uint32_t n, const uint8_t* in192, const uint64_t* raw
     LB_LAUNCH(k_msm_scalars, 1u, TPB, 1u, (const uint32_t*)d_req, (const uint8_t*)nullptr, (const uint64_t*)d_raw,
               (const g2j*)d_pts, (const uint8_t*)d_st, (const uint8_t*)nullptr, d_keys, d_hist);
   }
-  LB_LAUNCH(k_msm_scan, 1u, 1024u, (const uint32_t*)d_hist, d_off, d_coff, d_cur);
+  LB_LAUNCH(k_msm_scan, 1u, 1024u, (const uint32_t*)d_hist, d_off, d_coff, d_cur, LB_MSM_T);
   if (n) LB_LAUNCH(k_msm_scatter, blocks_for((uint32_t)n_ent, 256), 256u, (uint32_t)n_ent, (const uint32_t*)d_keys,
                    (const uint32_t*)d_off, d_cur, d_sorted);
   LB_LAUNCH(k_msm_chunks, blocks_for((uint32_t)max_chunks), TPB, (uint32_t)max_chunks, (const uint32_t*)d_off,
-            (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum);
+            (const uint32_t*)d_coff, (const uint32_t*)d_sorted, (const g2j*)d_pts, d_csum, LB_MSM_T);
   LB_LAUNCH(k_msm_buckets, blocks_for(LB_MSM_BUCKETS * LB_MSM_BLANES), TPB, (const uint32_t*)d_coff,
             (const g2j*)d_csum, d_bsum, LB_MSM_BLANES);
   LB_LAUNCH(k_msm_bits<LB_MSM_BITS_TPB>, LB_MSM_POS, LB_MSM_BITS_TPB, (const g2j*)d_bsum, d_G);

@@ -61,6 +61,7 @@ static constexpr int TPB = 64;  // one wave per workgroup: flexible residency at
 #define LB_MSM_NB 1024u
 #define LB_MSM_BUCKETS (LB_MSM_W * LB_MSM_NB)
 #define LB_MSM_T 16u
+#define LB_MSM_T_LONE 4u  // (a lone call of at most LB_LP_DEC_MAX sets: shorter chunk chains, more chunks)
 #define LB_MSM_POS 33u
 #define LB_MSM_NONE 0xffffffffu
 
@@ -244,14 +245,16 @@ __global__ void __launch_bounds__(TPB) k_msm_scalars(uint32_t n_req, const uint3
                                                      const uint8_t* __restrict__ pk_status, uint32_t* __restrict__ keys,
                                                      uint32_t* __restrict__ hist);
 __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ off,
-                                                   uint32_t* __restrict__ coff, uint32_t* __restrict__ cursor);
+                                                   uint32_t* __restrict__ coff, uint32_t* __restrict__ cursor,
+                                                   uint32_t T);
 __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n_ent, const uint32_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
                                                      uint32_t* __restrict__ sorted);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_chunks, const uint32_t* __restrict__ off,
                                                                  const uint32_t* __restrict__ coff,
                                                                  const uint32_t* __restrict__ sorted,
-                                                                 const g2j* __restrict__ sig, g2j* __restrict__ csum);
+                                                                 const g2j* __restrict__ sig, g2j* __restrict__ csum,
+                                                                 uint32_t T);
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_buckets(const uint32_t* __restrict__ coff,
                                                                   const g2j* __restrict__ csum, g2j* __restrict__ bsum,
                                                                   uint32_t lanes);

@@ -99,8 +99,10 @@ __global__ void __launch_bounds__(TPB) k_msm_scalars(uint32_t n_req, const uint3
 // Exclusive prefix sums over the 3072 buckets (one workgroup of 1024 lanes, 3
 // buckets per lane): off = entries, coff = chunks of <= T entries; off/coff
 // [LB_MSM_BUCKETS] are the totals.  Zeroes the scatter cursors.
+// (T: the chunk size -- LB_MSM_T, or LB_MSM_T_LONE for a lone mid-size call's shorter chains)
 __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ off,
-                                                   uint32_t* __restrict__ coff, uint32_t* __restrict__ cursor) {
+                                                   uint32_t* __restrict__ coff, uint32_t* __restrict__ cursor,
+                                                   uint32_t T) {
   constexpr uint32_t PER = LB_MSM_BUCKETS / 1024;
   static_assert(PER * 1024 == LB_MSM_BUCKETS, "3 buckets per lane");
   __shared__ uint32_t se[1024], sc[1024];
@@ -110,7 +112,7 @@ __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ 
   for (uint32_t j = 0; j < PER; j++) {
     h[j] = hist[t * PER + j];
     e += h[j];
-    c += (h[j] + LB_MSM_T - 1) / LB_MSM_T;
+    c += (h[j] + T - 1) / T;
     cursor[t * PER + j] = 0;
   }
   se[t] = e;
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ 
     off[t * PER + j] = re;
     coff[t * PER + j] = rc;
     re += h[j];
-    rc += (h[j] + LB_MSM_T - 1) / LB_MSM_T;
+    rc += (h[j] + T - 1) / T;
   }
   if (t == 1023) {
     off[LB_MSM_BUCKETS] = re;
@@ -188,12 +190,13 @@ LB_DEV uint32_t msm_chunk_bucket(const uint32_t* __restrict__ coff, uint32_t c) 
 __global__ void __launch_bounds__(TPB, LB_W_SCALAR) k_msm_chunks(uint32_t max_chunks, const uint32_t* __restrict__ off,
                                                                  const uint32_t* __restrict__ coff,
                                                                  const uint32_t* __restrict__ sorted,
-                                                                 const g2j* __restrict__ sig, g2j* __restrict__ csum) {
+                                                                 const g2j* __restrict__ sig, g2j* __restrict__ csum,
+                                                                 uint32_t T) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= max_chunks || c >= coff[LB_MSM_BUCKETS]) return;
   const uint32_t bk = msm_chunk_bucket(coff, c);
-  const uint32_t e0 = off[bk] + (c - coff[bk]) * LB_MSM_T;
-  const uint32_t e1 = min(e0 + LB_MSM_T, off[bk + 1]);
+  const uint32_t e0 = off[bk] + (c - coff[bk]) * T;
+  const uint32_t e1 = min(e0 + T, off[bk + 1]);
   g2a q;
   msm_point(q, sig, sorted[e0]);
   g2j acc;
