@@ -328,6 +328,9 @@ struct lb_ctx {
   bool lp_decode = true;
   bool lp_hash_finish = true;  // (LB_LP_HASH_FINISH: the same calls' hash finish as round programs)
   bool msm_short = true;  // (LB_MSM_SHORT: a lone mid-size call's MSM chunks of LB_MSM_T_LONE entries)
+  uint32_t msm_short_max = 16384u, msm_t_lone = LB_MSM_T_LONE;  // (LB_MSM_SHORT_MAX / LB_MSM_T_LONE probes)
+  // (the lone-call round-program size bounds; env LB_LP_DEC_MAX / LB_LP_HF_MAX / LB_LP_LINES_MAX probe others)
+  uint32_t lp_dec_max = LB_LP_DEC_MAX, lp_hf_max = LB_LP_HF_MAX, lp_lines_max = LB_LP_LINES_MAX;
   bool lp_lines = true;  // (LB_LP_LINES: a lone steps call's lines as round programs, up to LB_LP_LINES_MAX sets)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
@@ -692,8 +695,8 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   const size_t n_ent = use_msm ? 2 * (size_t)n_sets * LB_MSM_W : 0;
   // (a lone mid-size call: chunks of LB_MSM_T_LONE entries -- k_msm_chunks' chains are one lane's
   // mixed additions, 16 of them ~2.5 ms for C5; LB_MSM_SHORT=0 keeps LB_MSM_T)
-  const bool msm_short = use_msm && lone && n_sets <= 16384u && ctx->msm_short;
-  const uint32_t msm_T = msm_short ? LB_MSM_T_LONE : LB_MSM_T;
+  const bool msm_short = use_msm && lone && n_sets <= ctx->msm_short_max && ctx->msm_short;
+  const uint32_t msm_T = msm_short ? ctx->msm_t_lone : LB_MSM_T;
   const size_t max_chunks = use_msm ? n_ent / msm_T + LB_MSM_BUCKETS : 0;
   uint32_t* d_mkeys = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
   uint32_t* d_msorted = use_msm ? ws.take<uint32_t>(n_ent) : nullptr;
@@ -718,7 +721,7 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   uint32_t* d_G = steps ? ws.take<uint32_t>(144 * (size_t)ns * lsplit) : nullptr;
   fp12* d_Fparts = steps && lsplit > 1 ? ws.take<fp12>((size_t)(n_req ? n_req : 1) * lsplit) : nullptr;
   // a lone mid-size call's signature decode as round programs (k_sm_dec_prep / k_lp_dec / k_sm_dec_finish)
-  const bool dec_lp = lone && !d_sig_pre && n_sets && n_sets <= LB_LP_DEC_MAX && ctx->lp_decode;
+  const bool dec_lp = lone && !d_sig_pre && n_sets && n_sets <= ctx->lp_dec_max && ctx->lp_decode;
   uint32_t* d_dec_in = dec_lp ? ws.take<uint32_t>((size_t)ns * 4 * 16) : nullptr;
   uint32_t* d_dec_fl = dec_lp ? ws.take<uint32_t>((size_t)ns * 3) : nullptr;
   uint32_t* d_dec_out = dec_lp ? ws.take<uint32_t>((size_t)ns * 2 * 16) : nullptr;
@@ -728,13 +731,13 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // ... and, up to LB_LP_HF_MAX sets, its hash finish (k_hf_prep / k_lp_hf / k_hf_finish; above that
   // the workgroups queue: 1,536 / 2,048 sets 13.4 -> 11.0 / 11.8 ms, 4,704 (C5) 16.1 -> 17.4,
   // profiles/r06/orgs_probe_r06hf.json; LB_LP_HASH_FINISH=0: k_hash_finish)
-  const bool hf_lp = lone && n_sets && n_sets <= LB_LP_HF_MAX && ctx->lp_hash_finish;
+  const bool hf_lp = lone && n_sets && n_sets <= ctx->lp_hf_max && ctx->lp_hash_finish;
   uint32_t* d_hf_in = hf_lp ? ws.take<uint32_t>((size_t)ns * 12 * 16) : nullptr;
   uint32_t* d_hf_out = hf_lp ? ws.take<uint32_t>((size_t)ns * 6 * 16) : nullptr;
   if (hf_lp) LB_TRY(lp_ensure(ctx));
   // ... and, up to LB_LP_LINES_MAX sets of the steps organisation, its lines (k_lines_prep /
   // k_lp_lines / k_lines_store; LB_LP_LINES=0: k_lines_rows)
-  const bool lines_lp = steps && lone && n_sets <= LB_LP_LINES_MAX && ctx->lp_lines;
+  const bool lines_lp = steps && lone && n_sets <= ctx->lp_lines_max && ctx->lp_lines;
   uint32_t* d_ll_in = lines_lp ? ws.take<uint32_t>((size_t)ns * 9 * 16) : nullptr;
   uint32_t* d_ll_out = lines_lp ? ws.take<uint32_t>((size_t)ns * LB_LP_LINES_NOUT * 16) : nullptr;
   if (lines_lp) LB_TRY(lp_ensure(ctx));
@@ -1106,13 +1109,13 @@ static uint32_t level_blocks(uint32_t n_sets, uint32_t n_req, bool wide) {
   return b < 1u ? 1u : b > 8u ? 8u : b;
 }
 
-size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
+size_t pipeline_ws_bytes(const lb_ctx* ctx, uint32_t n_req, uint32_t n_sets) {
   size_t ns = n_sets ? n_sets : 1;
   // (+ the bucket MSM: 2 W keys + 2 W sorted entries and 2 W / T chunk partials per set)
   // (+ the steps organisation: size histogram / cursors / gt / row offsets and the lanes' G values)
   size_t per_set = sizeof(g2j) * 5 + sizeof(g1j) * 2 + sizeof(fp12) + 3 + 16 * 256 / 64 + 16 + 576 +
                    (size_t)LB_MILLER_LINES * 72 * 4 + 4 * LB_MSM_W * 4 +
-                   (2 * LB_MSM_W * sizeof(g2j)) / (ns <= 16384u ? LB_MSM_T_LONE : LB_MSM_T) + 1;
+                   (2 * LB_MSM_W * sizeof(g2j)) / (ns <= ctx->msm_short_max ? ctx->msm_t_lone : LB_MSM_T) + 1;
   // (+ the halves of a split Miller accumulation: 2 fp12, 2 flags, 2 offsets)
   size_t per_req = sizeof(g2a) + 8 * sizeof(fp12) + 1 + 4 + 8 + 8 + 4 * 256 / 64 + (size_t)LB_MILLER_LINES * 72 * 4 +
                    (size_t)LB_RTAIL_NIN * 64 + 4 + 2 * 256 / 64;  // (+ k_lp_rtail's records and flag)
@@ -1129,9 +1132,9 @@ size_t pipeline_ws_bytes(uint32_t n_req, uint32_t n_sets) {
                      4 * 256;
   return ns * per_set + (size_t)(n_req + 1) * per_req + msm_fixed + 64 * sizeof(fp12) + 80 * 256 + 4096 +
          (size_t)(LB_MTAIL_NIN + 12) * 64 + 512 + lvl + ns * 3 * 576 +
-         (ns <= LB_LP_DEC_MAX ? ns * (6 * 64 + 5 * 4 + 1 + 18 * 64) + 7 * 256 : 0) +  // (+ a lone call's
+         (ns <= std::max(ctx->lp_dec_max, ctx->lp_hf_max) ? ns * (6 * 64 + 5 * 4 + 1 + 18 * 64) + 7 * 256 : 0) +  // (+ a lone call's
                                                                                       // decode / hash records)
-         (ns <= LB_LP_LINES_MAX ? ns * (9 + LB_LP_LINES_NOUT) * 64 + 2 * 256 : 0);  // (+ its line records)
+         (ns <= ctx->lp_lines_max ? ns * (9 + LB_LP_LINES_NOUT) * 64 + 2 * 256 : 0);  // (+ its line records)
 }
 
 int validate_batch(lb_ctx* ctx, const lb_request_batch* b) {
@@ -1465,6 +1468,14 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_LINES")) ctx->lp_lines = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_SHORT")) ctx->msm_short = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_DEC_MAX")) ctx->lp_dec_max = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char* e = getenv("LB_LP_HF_MAX")) ctx->lp_hf_max = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char* e = getenv("LB_LP_LINES_MAX")) ctx->lp_lines_max = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char* e = getenv("LB_MSM_SHORT_MAX")) ctx->msm_short_max = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char* e = getenv("LB_MSM_T_LONE")) {
+    const unsigned long t = strtoul(e, nullptr, 10);
+    if (t >= 1 && t <= LB_MSM_T) ctx->msm_t_lone = (uint32_t)t;
+  }
   if (const char* e = getenv("LB_STEP_SPLIT")) {
     const int v = atoi(e);
     ctx->step_split = (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
@@ -1658,7 +1669,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (ok && ctx->lp_max_sets) {
     Slot& pl = ctx->slots[ctx->n_slots];
     const size_t ns = ctx->lp_max_sets, in = ns * (32 + 192 + 16 + 16 * 96) + 65536, out = 3 * ns + 4096;
-    ok = ensure_pin(ctx, pl, in + out) == LB_OK && ensure_ws(ctx, pl, in + out + pipeline_ws_bytes(ns, ns)) == LB_OK;
+    ok = ensure_pin(ctx, pl, in + out) == LB_OK && ensure_ws(ctx, pl, in + out + pipeline_ws_bytes(ctx, ns, ns)) == LB_OK;
   }
   if (!ok) {
     lb_destroy(ctx);
@@ -1857,7 +1868,7 @@ static int submit_device(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8
   LB_TRY(finish_slot(ctx, sl));  // at most kSlots calls in flight
   pick_streams(ctx, sl);
   if (!partial) borrow_idle_stream(ctx, sl);  // (a pending two-phase call never holds a lent slot)
-  LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(b->n_requests, b->n_sets)));
+  LB_TRY(ensure_ws(ctx, sl, pipeline_ws_bytes(ctx, b->n_requests, b->n_sets)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   uint8_t* d_partial = partial ? ws.take<uint8_t>(LB_GT_BYTES) : nullptr;
   LB_TRY(begin_call(ctx, sl));
@@ -1959,7 +1970,7 @@ static int submit_host(lb_ctx* ctx, Slot& sl, const lb_request_batch* b, uint8_t
   t_finish = ms_since(t0);
   if (!partial) borrow_idle_stream(ctx, sl);
   LB_TRY(ensure_pin(ctx, sl, in_bytes + out_bytes));
-  LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(nr, ns)));
+  LB_TRY(ensure_ws(ctx, sl, in_bytes + out_bytes + pipeline_ws_bytes(ctx, nr, ns)));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   char* h = sl.h_pin;
   size_t ho = 0;
@@ -2744,9 +2755,9 @@ int sm_validate(lb_ctx* ctx, const lb_same_message_batch* b) {
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // phase-2 device reserve: the retry pipeline over at most every set, its gathered inputs
-size_t sm_phase2_bytes(uint32_t ns) {
+size_t sm_phase2_bytes(const lb_ctx* ctx, uint32_t ns) {
   const size_t n = ns ? ns : 1;
-  return pipeline_ws_bytes(ns, ns) + n * (2 * 4 + sizeof(g2j) + 1 + 32 + 4 + 4 + 2) + 16 * 256;
+  return pipeline_ws_bytes(ctx, ns, ns) + n * (2 * 4 + sizeof(g2j) + 1 + 32 + 4 + 4 + 2) + 16 * 256;
 }
 
 // Phase 1 on slot `sl` (already retired by the caller); the call stays busy
@@ -2774,7 +2785,7 @@ int sm_submit(lb_ctx* ctx, Slot& sl, const lb_same_message_batch* b, uint8_t* ou
   LB_TRY(ensure_pin(ctx, sl, in_bytes + res_bytes + retry_bytes));
   // (+ a small package's decode records: 4 + 2 records, 5 flags and a status per signature)
   const size_t dec_bytes = ns <= LB_SM_DEC_MAX ? (size_t)ns * (6 * 64 + 5 * 4 + 1) + 6 * 256 : 0;
-  LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(nj, nj) + sm_phase2_bytes(ns) + dec_bytes));
+  LB_TRY(ensure_ws(ctx, sl, in_bytes + extra + pipeline_ws_bytes(ctx, nj, nj) + sm_phase2_bytes(ctx, ns) + dec_bytes));
   Bump ws{sl.d_ws, 0, sl.ws_cap};
   char* h = sl.h_pin;
   size_t ho = 0;

@@ -66,7 +66,7 @@
 #define LB_LP_DEC_ROWS 8          // gen_lp.py DEC_ROWS
 #define LB_LP_DEC_REGS 128        // gen_lp.py MAX_REGS_DEC
 #define LB_SM_DEC_MAX 512         // packages of at most this many signatures decode on k_lp_dec
-#define LB_LP_DEC_MAX 16384       // ... and lone pipeline calls of at most this many sets
+#define LB_LP_DEC_MAX 5120        // ... and lone pipeline calls of at most this many sets
 #define LB_MSM_BITS_GROUP 8      // lpgen/bls.py MSM_BITS_GROUP
 #define LB_MSM_BITS_INST (LB_MSM_POS * (LB_MSM_NB / 2 / LB_MSM_BITS_GROUP))  // level-0 instances: 33 x 64
 #define LB_RTAIL_NIN 16                 // rtail inputs: F_k (12 Fp), S_k affine (4 Fp); inflag S_inf

@@ -33,6 +33,11 @@ CONFIGS = {
     "round5_thresholds": {"LB_LINES_MIN": "8192", "LB_MSM_MIN": "4096"},
 }
 SIZES = (1536, 2048, 3072, 4096, 6144, 8192)
+# (ORGS_CONFIGS: a JSON object replacing CONFIGS; ORGS_SIZES: comma-separated call sizes)
+if os.environ.get("ORGS_CONFIGS"):
+    CONFIGS = json.loads(os.environ["ORGS_CONFIGS"])
+if os.environ.get("ORGS_SIZES"):
+    SIZES = tuple(int(x) for x in os.environ["ORGS_SIZES"].split(","))
 
 
 def p50(fn, reps):
@@ -95,7 +100,8 @@ def main():
                 assert r.valid.all(), (name, n)
             call()
             ms = p50(call, reps)
-            res["n%d" % n] = {"p50_ms": round(ms, 3), "stages": [k for k, _ in d.last_stage_times()]}
+            res["n%d" % n] = {"p50_ms": round(ms, 3), "stage_ms": {
+                k: round(v, 3) for k, v in d.last_stage_times()}}
         d.close()
         out["configs"][name] = res
         print(name, json.dumps({k: (v["p50_ms"] if isinstance(v, dict) and "p50_ms" in v else None)
