@@ -331,6 +331,7 @@ struct lb_ctx {
   uint32_t msm_short_max = 16384u, msm_t_lone = LB_MSM_T_LONE;  // (LB_MSM_SHORT_MAX / LB_MSM_T_LONE probes)
   // (the lone-call round-program size bounds; env LB_LP_DEC_MAX / LB_LP_HF_MAX / LB_LP_LINES_MAX probe others)
   uint32_t lp_dec_max = LB_LP_DEC_MAX, lp_hf_max = LB_LP_HF_MAX, lp_lines_max = LB_LP_LINES_MAX;
+  uint32_t lp_narrow = 1;  // (LB_LP_NARROW=1: the hash-finish program on LB_LP_NARROW_ROWS rows, default; 0: 16 rows)
   bool lp_lines = true;  // (LB_LP_LINES: a lone steps call's lines as round programs, up to LB_LP_LINES_MAX sets)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
   g1a* d_table = nullptr;
@@ -765,8 +766,10 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
     LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
     if (hf_lp) {  // (a lone mid-size call: clear_cofactor(Q0 + Q1) as round programs, k_lp_hf)
       LB_STAGE("hash_finish", 1, k_hf_prep, blocks_for(n_sets * 12u, 256), 256u, n_sets, (const g2j*)d_q, d_hf_in);
-      LB_STAGE("hash_finish", 1, k_lp_hf, n_sets, LB_LP_HF_ROWS * 16u,
-               ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_HASH_FINISH].off, n_sets, (const uint32_t*)d_hf_in, d_hf_out);
+      const bool nar = ctx->lp_narrow & 1u;
+      LB_STAGE("hash_finish", 1, k_lp_hf, n_sets, (nar ? LB_LP_NARROW_ROWS : LB_LP_HF_ROWS) * 16u,
+               ctx->d_lp + LB_LP_PROGS[nar ? LB_LP_PROG_HASH_FINISH_NARROW : LB_LP_PROG_HASH_FINISH].off, n_sets,
+               (const uint32_t*)d_hf_in, d_hf_out);
       LB_STAGE("hash_finish", 1, k_hf_finish, blocks_for(n_sets * 6u, 256), 256u, n_sets, (const uint32_t*)d_hf_out,
                d_h);
     } else {
@@ -1468,6 +1471,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_LINES")) ctx->lp_lines = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_SHORT")) ctx->msm_short = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_NARROW")) ctx->lp_narrow = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_DEC_MAX")) ctx->lp_dec_max = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_HF_MAX")) ctx->lp_hf_max = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_LINES_MAX")) ctx->lp_lines_max = (uint32_t)strtoul(e, nullptr, 10);

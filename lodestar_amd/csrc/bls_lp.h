@@ -58,7 +58,9 @@
 #define LB_LP_PROG_SIG_DECODE 13  // a small same-message package's signature decode (k_lp_dec, 8 rows)
 #define LB_LP_PROG_HASH_FINISH 14  // a lone mid-size call's clear_cofactor(Q0 + Q1) (k_lp_hf, 16 rows)
 #define LB_LP_PROG_LINES 15  // a lone mid-size call's Miller lines of one pair (k_lp_lines, 16 rows)
-#define LB_LP_NPROGS 16
+#define LB_LP_PROG_HASH_FINISH_NARROW 16  // the hash finish compiled for LB_LP_NARROW_ROWS rows
+#define LB_LP_NPROGS 17
+#define LB_LP_NARROW_ROWS 8  // gen_lp.py DEC_ROWS
 #define LB_LP_LINES_MAX 5120  // lone steps calls of at most this many sets store their lines via k_lp_lines (6,144: -0.5 ms)
 #define LB_LP_LINES_NOUT (68 * 6)
 #define LB_LP_HF_ROWS 16           // gen_lp.py HF_ROWS

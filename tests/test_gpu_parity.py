@@ -368,7 +368,7 @@ def _device_with_env(**env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("wide", ["1", "lanes", "0"])
+@pytest.mark.parametrize("wide", ["1", "lanes", "0", "chunk1", "chunk16"])
 @pytest.mark.parametrize("mtail", ["1", "0"])
 @pytest.mark.parametrize("inject", [True, False])
 def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail, wide):
@@ -382,14 +382,17 @@ def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail, wide):
     k_tail).  A lone call's wide forms (the merged check on 64 rows, the MSM's sums over
     more lanes, its bit sums as three levels of round programs) and the narrow ones of calls
     sharing the GPU (LB_WIDE_TAIL=0, LB_MSM_LANES=0); "lanes": the bit sums by k_msm_bits'
-    256 threads instead of the programs (LB_MSM_BITS_LP=0).  Verdicts and rejection codes ==
-    the C oracle's."""
+    256 threads instead of the programs (LB_MSM_BITS_LP=0).  A lone call of this size accumulates
+    chunks of <= 4 entries; "chunk1" / "chunk16": chunks of one entry (LB_MSM_T_LONE=1) / the
+    shared calls' 16 (LB_MSM_SHORT=0; with the hash finish's 16-row program, LB_LP_NARROW=0, instead
+    of the default 8-row one).  Verdicts and rejection codes == the C oracle's."""
     from oracle import c_oracle as C
     args = mixed_workload_cache(device, inject)
     seed = hashlib.sha256(b"msm-seed").digest()
     w = "0" if wide == "0" else "1"
+    chunks = {"chunk1": {"LB_MSM_T_LONE": "1"}, "chunk16": {"LB_MSM_SHORT": "0", "LB_LP_NARROW": "0"}}.get(wide, {})
     dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail, LB_WIDE_TAIL=w, LB_MSM_LANES=w,
-                           LB_MSM_BITS_LP="0" if wide == "lanes" else "1")
+                           LB_MSM_BITS_LP="0" if wide == "lanes" else "1", **chunks)
     try:
         res = dev.verify_requests(*args, seed)
         stages = dict(dev.last_stage_times())

@@ -400,14 +400,15 @@ def test_sig_decode_program_against_oracle():
     assert ofl[1] == 1
 
 
-def test_hash_finish_program_against_oracle():
+@pytest.mark.parametrize("rows", [16, 8])
+def test_hash_finish_program_against_oracle(rows):
     """A lone mid-size call's hash finish (k_lp_hf): Q0, Q1 -- the two mapped points of a
     message, as one-lane Jacobian inputs with arbitrary Z -- give H = clear_cofactor(Q0 + Q1),
     output Jacobian in the one-lane form, equal to the oracle's hash_to_g2; Q0 = -Q1 gives
-    infinity (Z = 0)."""
+    infinity (Z = 0).  Compiled for 16 rows and for the default narrow 8-row workgroup."""
     import random
     rnd = random.Random(5)
-    g = lpc.compile_graph(bls.hash_finish_program(), rows=16)
+    g = lpc.compile_graph(bls.hash_finish_program(), rows=rows)
     assert g.stats["regs"] <= 128
     r384 = pow(1 << 384, -1, P)
 
