@@ -331,6 +331,9 @@ struct lb_ctx {
   uint32_t msm_short_max = 16384u, msm_t_lone = LB_MSM_T_LONE;  // (LB_MSM_SHORT_MAX / LB_MSM_T_LONE probes)
   // (the lone-call round-program size bounds; env LB_LP_DEC_MAX / LB_LP_HF_MAX / LB_LP_LINES_MAX probe others)
   uint32_t lp_dec_max = LB_LP_DEC_MAX, lp_hf_max = LB_LP_HF_MAX, lp_lines_max = LB_LP_LINES_MAX;
+  // (LB_LP_HASH_FULL: lone calls of at most this many sets run hash_to_G2's whole curve part as one
+  // program per set, k_lp_hash -- profiles/r06/orgs_probe_r06hf3.json; 0: never)
+  uint32_t lp_hash_full = 2048;
   uint32_t lp_narrow = 1;  // (LB_LP_NARROW=1: the hash-finish program on LB_LP_NARROW_ROWS rows, default; 0: 16 rows)
   bool lp_lines = true;  // (LB_LP_LINES: a lone steps call's lines as round programs, up to LB_LP_LINES_MAX sets)
   // device-resident pubkey table (index2pubkey mirror, lb_pubkey_table_*)
@@ -763,17 +766,25 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   }
   LB_TRY(stream_wait(ctx, sl, 0, 1, 0));
   if (n_sets) {
-    LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
-    if (hf_lp) {  // (a lone mid-size call: clear_cofactor(Q0 + Q1) as round programs, k_lp_hf)
-      LB_STAGE("hash_finish", 1, k_hf_prep, blocks_for(n_sets * 12u, 256), 256u, n_sets, (const g2j*)d_q, d_hf_in);
-      const bool nar = ctx->lp_narrow & 1u;
-      LB_STAGE("hash_finish", 1, k_lp_hf, n_sets, (nar ? LB_LP_NARROW_ROWS : LB_LP_HF_ROWS) * 16u,
-               ctx->d_lp + LB_LP_PROGS[nar ? LB_LP_PROG_HASH_FINISH_NARROW : LB_LP_PROG_HASH_FINISH].off, n_sets,
-               (const uint32_t*)d_hf_in, d_hf_out);
+    if (hf_lp && n_sets <= ctx->lp_hash_full) {  // (the whole curve part as one program per set, k_lp_hash)
+      LB_STAGE("hash_finish", 1, k_hu_prep, blocks_for(n_sets, 256), 256u, n_sets, d_msgs, d_hf_in);
+      LB_STAGE("hash_finish", 1, k_lp_hash, n_sets, LB_LP_NARROW_ROWS * 16u,
+               ctx->d_lp + LB_LP_PROGS[LB_LP_PROG_HASH_FULL].off, n_sets, (const uint32_t*)d_hf_in, d_hf_out);
       LB_STAGE("hash_finish", 1, k_hf_finish, blocks_for(n_sets * 6u, 256), 256u, n_sets, (const uint32_t*)d_hf_out,
                d_h);
     } else {
-      LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, d_q, d_h);
+      LB_STAGE("hash_half", 1, k_hash_half, blocks_for(2 * n_sets), TPB, n_sets, d_msgs, d_q);
+      if (hf_lp) {  // (a lone mid-size call: clear_cofactor(Q0 + Q1) as round programs, k_lp_hf)
+        LB_STAGE("hash_finish", 1, k_hf_prep, blocks_for(n_sets * 12u, 256), 256u, n_sets, (const g2j*)d_q, d_hf_in);
+        const bool nar = ctx->lp_narrow & 1u;
+        LB_STAGE("hash_finish", 1, k_lp_hf, n_sets, (nar ? LB_LP_NARROW_ROWS : LB_LP_HF_ROWS) * 16u,
+                 ctx->d_lp + LB_LP_PROGS[nar ? LB_LP_PROG_HASH_FINISH_NARROW : LB_LP_PROG_HASH_FINISH].off, n_sets,
+                 (const uint32_t*)d_hf_in, d_hf_out);
+        LB_STAGE("hash_finish", 1, k_hf_finish, blocks_for(n_sets * 6u, 256), 256u, n_sets, (const uint32_t*)d_hf_out,
+                 d_h);
+      } else {
+        LB_STAGE("hash_finish", 1, k_hash_finish, blocks_for(n_sets), TPB, n_sets, d_q, d_h);
+      }
     }
   }
   LB_STAGE("req_flags", 0, k_req_flags, blocks_for(n_req), TPB, n_req, d_req_off, d_single);
@@ -1389,7 +1400,7 @@ size_t scratch_per_queue(int device, uint32_t* out_lane_bytes) {
                            (const void*)k_hash_half, (const void*)k_hash_finish, (const void*)k_final,
                            (const void*)k_tail, (const void*)k_req_horner, (const void*)k_req_join, (const void*)k_lp_verify,
                            (const void*)k_lp_mtail, (const void*)k_lp_final_lane, (const void*)k_gt_prod,
-                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_lp_hf, (const void*)k_lp_lines, (const void*)k_level_prod, (const void*)k_level_part,
+                           (const void*)k_lp_rtail, (const void*)k_lp_msm_bits, (const void*)k_lp_dec, (const void*)k_lp_hf, (const void*)k_lp_hash, (const void*)k_lp_lines, (const void*)k_level_prod, (const void*)k_level_part,
                            (const void*)k_level_wc,
                            (const void*)k_msm_buckets, (const void*)k_msm_bits<TPB>, (const void*)k_msm_bits<LB_MSM_BITS_TPB>,
                            (const void*)k_decode_sigs,
@@ -1471,6 +1482,7 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LP_HASH_FINISH")) ctx->lp_hash_finish = atoi(e) != 0;
   if (const char* e = getenv("LB_LP_LINES")) ctx->lp_lines = atoi(e) != 0;
   if (const char* e = getenv("LB_MSM_SHORT")) ctx->msm_short = atoi(e) != 0;
+  if (const char* e = getenv("LB_LP_HASH_FULL")) ctx->lp_hash_full = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_NARROW")) ctx->lp_narrow = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_DEC_MAX")) ctx->lp_dec_max = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LP_HF_MAX")) ctx->lp_hf_max = (uint32_t)strtoul(e, nullptr, 10);

@@ -59,7 +59,9 @@
 #define LB_LP_PROG_HASH_FINISH 14  // a lone mid-size call's clear_cofactor(Q0 + Q1) (k_lp_hf, 16 rows)
 #define LB_LP_PROG_LINES 15  // a lone mid-size call's Miller lines of one pair (k_lp_lines, 16 rows)
 #define LB_LP_PROG_HASH_FINISH_NARROW 16  // the hash finish compiled for LB_LP_NARROW_ROWS rows
-#define LB_LP_NPROGS 17
+#define LB_LP_PROG_HASH_FULL 17  // a lone mid-size call's whole hash_to_G2 curve part (k_lp_hash, 8 rows)
+#define LB_LP_NPROGS 18
+#define LB_LP_HASH_REGS 384  // gen_lp.py MAX_REGS_HASH
 #define LB_LP_NARROW_ROWS 8  // gen_lp.py DEC_ROWS
 #define LB_LP_LINES_MAX 5120  // lone steps calls of at most this many sets store their lines via k_lp_lines (6,144: -0.5 ms)
 #define LB_LP_LINES_NOUT (68 * 6)
@@ -162,6 +164,13 @@ __global__ void __launch_bounds__(256) k_sm_dec_finish(uint32_t n, const uint8_t
 // A lone mid-size call's hash finish (bls_host.hip): Q0, Q1 of every set into records
 // (k_hf_prep), the hash_finish program per set on a 16-row workgroup (k_lp_hf), H back into
 // Jacobian points (k_hf_finish)
+// LB_LP_HASH_FULL: hash_to_field on one lane per set (k_hu_prep: u0, u1 as 4 records), the
+// hash_full program per set (k_lp_hash), H back into Jacobian by k_hf_finish
+__global__ void __launch_bounds__(256) k_hu_prep(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                 uint32_t* __restrict__ in16);
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hash(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                const uint32_t* __restrict__ in16,
+                                                                uint32_t* __restrict__ out16);
 __global__ void __launch_bounds__(256) k_hf_prep(uint32_t n, const g2j* __restrict__ q, uint32_t* __restrict__ in16);
 __global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hf(const uint32_t* __restrict__ prog, uint32_t n,
                                                               const uint32_t* __restrict__ in16,

@@ -1024,6 +1024,36 @@ __global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hf(const uint32_t* __
   lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * 6 * 16, s_fl);
 }
 
+__global__ void __launch_bounds__(256) k_hu_prep(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                 uint32_t* __restrict__ in16) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t m[32];
+  for (int k = 0; k < 32; k++) m[k] = msgs[(size_t)i * 32 + k];
+  fp2 u[2];
+  hash_to_field_fp2_2(u, m);
+  uint32_t* rec = in16 + (size_t)i * 4 * 16;
+  const fp* v[4] = {&u[0].c0, &u[0].c1, &u[1].c0, &u[1].c1};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) rec[16 * k + j] = v[k]->l[j];
+#pragma unroll
+    for (int j = 12; j < 16; j++) rec[16 * k + j] = 0u;
+  }
+}
+
+__global__ void __launch_bounds__(LB_LP_HF_ROWS * 16) k_lp_hash(const uint32_t* __restrict__ prog, uint32_t n,
+                                                                const uint32_t* __restrict__ in16,
+                                                                uint32_t* __restrict__ out16) {
+  __shared__ LpSharedT<LB_LP_HASH_REGS> S;
+  __shared__ uint32_t s_fl[4];
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+  const uint32_t* in = in16 + (size_t)b * 4 * 16;
+  lp_run(S, prog, in, 0xffffffffu, in, nullptr, out16 + (size_t)b * 6 * 16, s_fl);
+}
+
 __global__ void __launch_bounds__(256) k_hf_finish(uint32_t n, const uint32_t* __restrict__ out16,
                                                    g2j* __restrict__ h) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (set, coordinate): 6 a set

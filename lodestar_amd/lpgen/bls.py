@@ -856,6 +856,21 @@ def hash_finish_program() -> Graph:
     return g
 
 
+def hash_full_program() -> Graph:
+    """The whole hash_to_G2 curve part for a lone mid-size call (k_hash_half's SSWU + isogeny
+    chains and k_hash_finish's cofactor clearing as ONE program, k_lp_hash): inputs u0, u1 (the
+    hash_to_field outputs, one-lane Montgomery form, as k_lp_prep writes them); output
+    H = clear_cofactor(map(u0) + map(u1)), Jacobian in the one-lane form."""
+    g = Graph("hash_full")
+    u = [Fp2(g.input("u%dc0" % i), g.input("u%dc1" % i)) for i in range(2)]
+    J = proj_to_jac(hash_to_g2(u[0], u[1]))
+    r384 = g.const_raw(R384_RAW)  # x * R384 / R416: back to the one-lane form
+    for v, c in ((J.X, "X"), (J.Y, "Y"), (J.Z, "Z")):
+        g.output("H_%s0" % c, v.c0 * r384, canonical=True)
+        g.output("H_%s1" % c, v.c1 * r384, canonical=True)
+    return g
+
+
 def lines_program() -> Graph:
     """The 68 Miller lines of one pair (r pk, H) for a lone mid-size call (k_lines_rows' one-lane
     T-chain, ~3.3 ms, as ~210 rounds on a 16-row workgroup): inputs P (Jacobian G1) and H

@@ -384,13 +384,13 @@ def test_mixed_workload_bucket_msm_vs_c_oracle(device, inject, mtail, wide):
     sharing the GPU (LB_WIDE_TAIL=0, LB_MSM_LANES=0); "lanes": the bit sums by k_msm_bits'
     256 threads instead of the programs (LB_MSM_BITS_LP=0).  A lone call of this size accumulates
     chunks of <= 4 entries; "chunk1" / "chunk16": chunks of one entry (LB_MSM_T_LONE=1) / the
-    shared calls' 16 (LB_MSM_SHORT=0; with the hash finish's 16-row program, LB_LP_NARROW=0, instead
-    of the default 8-row one).  Verdicts and rejection codes == the C oracle's."""
+    shared calls' 16 (LB_MSM_SHORT=0; with the hash as k_hash_half + the hash finish's 16-row program,
+    LB_LP_HASH_FULL=0 / LB_LP_NARROW=0, instead of the default whole-hash program).  Verdicts and rejection codes == the C oracle's."""
     from oracle import c_oracle as C
     args = mixed_workload_cache(device, inject)
     seed = hashlib.sha256(b"msm-seed").digest()
     w = "0" if wide == "0" else "1"
-    chunks = {"chunk1": {"LB_MSM_T_LONE": "1"}, "chunk16": {"LB_MSM_SHORT": "0", "LB_LP_NARROW": "0"}}.get(wide, {})
+    chunks = {"chunk1": {"LB_MSM_T_LONE": "1"}, "chunk16": {"LB_MSM_SHORT": "0", "LB_LP_NARROW": "0", "LB_LP_HASH_FULL": "0"}}.get(wide, {})
     dev = _device_with_env(LB_MSM_MIN="1", LB_MILLER="lines", LB_MTAIL=mtail, LB_WIDE_TAIL=w, LB_MSM_LANES=w,
                            LB_MSM_BITS_LP="0" if wide == "lanes" else "1", **chunks)
     try:

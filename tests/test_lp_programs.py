@@ -434,6 +434,29 @@ def test_hash_finish_program_against_oracle(rows):
     assert outs[4] == 0 and outs[5] == 0
 
 
+def test_hash_full_program_against_oracle():
+    """LB_LP_HASH_FULL's program (k_lp_hash): u0, u1 -- hash_to_field's outputs in the one-lane
+    Montgomery form -- give H = clear_cofactor(map(u0) + map(u1)) as one-lane Jacobian, equal to
+    the oracle's hash_to_g2 (8 rows, the kernel's workgroup)."""
+    g = lpc.compile_graph(bls.hash_full_program(), rows=8)
+    assert g.stats["regs"] <= 384
+    r384 = pow(1 << 384, -1, P)
+
+    def f2mul(a, b):
+        return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+    def f2inv(a):
+        n = pow((a[0] * a[0] + a[1] * a[1]) % P, -1, P)
+        return (a[0] * n % P, -a[1] * n % P)
+    for msg in (b"\x00" * 32, bytes(range(32)), b"\xff" * 32):
+        u0, u1 = O.hash_to_field_fp2(msg, 2, O.DST_POP)
+        outs, _ = g.run([mont(v) for v in (u0[0], u0[1], u1[0], u1[1])], [])
+        X0, X1, Y0, Y1, Z0, Z1 = (v * r384 % P for v in outs)
+        zi = f2inv((Z0, Z1))
+        zi2 = f2mul(zi, zi)
+        assert (f2mul((X0, X1), zi2), f2mul((Y0, Y1), f2mul(zi2, zi))) == O.hash_to_g2(msg)
+
+
 def test_lines_program_against_oracle():
     """A lone mid-size call's lines (k_lp_lines): the 68 lines of (P, H) from projective inputs,
     multiplied as k_step_acc does (a squaring per level, (l0, l1, l4) at c0.c0, c0.c1, c1.c1),
