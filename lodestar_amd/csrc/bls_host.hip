@@ -362,6 +362,8 @@ struct lb_ctx {
   // (LB_LP_MAX, lb_set_latency_path; 0 = never)
   uint32_t* d_lp = nullptr;
   uint32_t lp_max_sets = 1024;
+  uint32_t lp_lone_max = 896;  // (LB_LP_LONE_MAX, 0 = off: lone calls above it take the pipeline, run_pipeline)
+  bool lp_explicit = false;    // (the bound set by lb_set_latency_path / LB_LP_MAX: no lone rule)
   // the merged check of a steps + MSM call as a round program (k_lp_mtail: S_all from the
   // MSM's bit sums, Miller(-g1, S_all), final exponentiation on one workgroup) instead of
   // msm_final + lines of S_all + the one-wave k_tail (LB_MTAIL=0: the one-wave chain)
@@ -614,6 +616,18 @@ int run_tails(lb_ctx* ctx, Slot& sl) {
   return LB_OK;
 }
 
+// lone calls of lp_lone_max < n_sets <= lp_max_sets leave the latency path for the pipeline
+// (run_pipeline's lone_mid; the synchronous entry points then take slot 0's two-stream DAG)
+static bool lp_lone_rule(const lb_ctx* ctx, uint32_t n_sets) {
+  return !ctx->lp_explicit && ctx->lp_lone_max && n_sets > ctx->lp_lone_max && n_sets <= ctx->lp_max_sets;
+}
+
+static bool any_slot_busy(const lb_ctx* ctx) {
+  for (int s = 0; s <= ctx->n_slots; s++)
+    if (ctx->slots[s].busy) return true;
+  return false;
+}
+
 int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const uint32_t* d_req_off,
                  const uint8_t* d_pks, const uint32_t* d_pk_off, const uint32_t* d_pk_idx, const uint8_t* d_msgs, const uint8_t* d_sigs,
                  const uint32_t* d_sig_off, const uint8_t* d_seed, uint8_t* d_valid, uint8_t* d_req_err,
@@ -622,7 +636,16 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   // d_sig_pre / d_sst_pre: signatures already decoded and validated (same-message
   // phase 2): no k_decode_sigs, d_sigs / d_sig_off unused
   const bool partial = d_partial != nullptr;
-  if (!partial && !d_sig_pre && n_sets <= ctx->lp_max_sets) {
+  bool lone = true;  // (no other slot busy: the GPU is this call's)
+  for (int s = 0; s < ctx->n_slots; s++)
+    if (&ctx->slots[s] != &sl && ctx->slots[s].busy && ctx->slots[s].lent_to != &sl) lone = false;
+  // a lone call of lp_lone_max < n_sets <= lp_max_sets runs the pipeline's steps + MSM + merged-check
+  // program instead of the latency path (~7.0 ms flat from ~400 sets against the latency path's
+  // 7.2 / 8.0 ms at 896 / 1,024 sets, profiles/r06/orgs_probe_r06lp2.json), merged whatever its
+  // request count; not when the latency-path bound was set explicitly (lb_set_latency_path, LB_LP_MAX)
+  const bool lone_mid = !partial && !d_sig_pre && lone && &sl != &ctx->prio() && lp_lone_rule(ctx, n_sets) &&
+                        ctx->miller_mode == 0 && ctx->tail_wave && ctx->acc_steps;
+  if (!partial && !d_sig_pre && n_sets <= ctx->lp_max_sets && !lone_mid) {
     sl.h_stats[0] = sl.h_stats[1] = 0;
     return run_lp(ctx, sl, n_req, n_sets, d_req_off, d_pks, d_pk_off, d_pk_idx, d_msgs, d_sigs, d_sig_off, d_seed,
                   d_valid, d_req_err, d_set_status, ws);
@@ -634,24 +657,21 @@ int run_pipeline(lb_ctx* ctx, Slot& sl, uint32_t n_req, uint32_t n_sets, const u
   g2j* d_h = ws.take<g2j>(ns);
   g1j* d_pk = ws.take<g1j>(ns);
   g1j* d_rpk = ws.take<g1j>(ns);
-  const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets);
+  const bool by_lines = ctx->miller_mode == 2 || (ctx->miller_mode == 0 && n_sets >= ctx->lines_min_sets) || lone_mid;
   const bool by_wave =
       !by_lines && (ctx->miller_mode == 3 || (ctx->miller_mode == 0 && n_sets <= ctx->wave_max_sets));
   fp12* d_f = by_lines ? nullptr : ws.take<fp12>(ns);  // per-set Miller values (lane / wave modes)
   // a two-phase call always merges (its partial is the merged product) and uses the wave tails
   const bool tail_wave = ctx->tail_wave || partial;
   // stored lines: set pairs [0, n_sets) (lines mode), S pairs [n_sets, n_sets + n_req) (wave tails)
-  const bool merged = partial || (tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req);
+  const bool merged = partial || (tail_wave && ctx->merge_min_req && n_req >= ctx->merge_min_req) || lone_mid;
   const uint32_t n_pairs = n_sets + n_req + (merged ? 1u : 0u);  // + the merged pair (-g1, S_all)
-  const bool use_msm = merged && n_sets && ctx->msm_min_sets && n_sets >= ctx->msm_min_sets;
+  const bool use_msm = merged && n_sets && ctx->msm_min_sets && (n_sets >= ctx->msm_min_sets || lone_mid);
   // a lone call on an otherwise idle GPU splits every request of the Miller
   // accumulation in two halves: twice the waves (one per SIMD for a 65,536-set
   // call instead of one per two SIMDs) at the price of the halves' separate
   // Fp12 squarings; with other calls in flight the idle SIMDs run their stages
   // instead and the work-efficient form is kept (LB_ACC_SPLIT=0|1 forces one)
-  bool lone = true;
-  for (int s = 0; s < ctx->n_slots; s++)
-    if (&ctx->slots[s] != &sl && ctx->slots[s].busy && ctx->slots[s].lent_to != &sl) lone = false;
   // steps organisation (k_steps.hip): no split (a request already has one lane per set)
   const bool steps = by_lines && tail_wave && n_sets && ctx->acc_steps;
   const bool split = by_lines && !steps && (ctx->acc_split == 1 || (ctx->acc_split < 0 && lone && n_req >= 64));
@@ -1507,7 +1527,9 @@ static int create_ctx(int device, lb_ctx** out_ctx, bool lane) {
   if (const char* e = getenv("LB_LP_MAX")) {
     const long v = atol(e);  // clamped like lb_set_latency_path: the product tree's 2^LB_LP_TREE_LEVELS sets
     ctx->lp_max_sets = v <= 0 ? 0u : v < (1l << LB_LP_TREE_LEVELS) ? (uint32_t)v : (1u << LB_LP_TREE_LEVELS);
+    ctx->lp_explicit = true;
   }
+  if (const char* e = getenv("LB_LP_LONE_MAX")) ctx->lp_lone_max = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("LB_LINES_WAVES")) ctx->lines_waves = ctx->lines_waves_small = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("LB_ACC_SPLIT")) ctx->acc_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("LB_ACC")) ctx->acc_steps = strcmp(e, "pairs") ? 1 : 0;
@@ -2362,7 +2384,8 @@ int lb_verify_requests_device(lb_ctx* ctx, const lb_request_batch* b, uint8_t* d
   if (!d_valid || !d_req_err) return LB_ERR_INVALID_ARGUMENT;
   LB_HIP(hipSetDevice(ctx->device));
   uint64_t t = 0;
-  if (b->n_sets <= ctx->lp_max_sets) {  // latency path: the priority lane, beside any calls in flight
+  if (b->n_sets <= ctx->lp_max_sets && !(lp_lone_rule(ctx, b->n_sets) && !any_slot_busy(ctx))) {
+    // latency path: the priority lane, beside any calls in flight
     LB_TRY(submit_device(ctx, ctx->prio(), b, d_valid, d_req_err, d_set_status, false, &t));
     return lb_wait(ctx, t, stats);
   }
@@ -2383,7 +2406,8 @@ int lb_verify_requests(lb_ctx* ctx, const lb_request_batch* b, uint8_t* out_vali
     return LB_OK;
   }
   uint64_t t = 0;
-  if (b->n_sets <= ctx->lp_max_sets) {  // latency path: the priority lane, beside any calls in flight
+  if (b->n_sets <= ctx->lp_max_sets && !(lp_lone_rule(ctx, b->n_sets) && !any_slot_busy(ctx))) {
+    // latency path: the priority lane, beside any calls in flight
     LB_TRY(submit_host(ctx, ctx->prio(), b, out_valid, out_req_err, out_set_status, false, &t));
     return lb_wait(ctx, t, stats);
   }
@@ -3293,6 +3317,7 @@ int lb_set_latency_path(lb_ctx* ctx, uint32_t max_sets) {
   // (k_lp_verify's product tree has LB_LP_TREE_LEVELS levels of arrival counters: a
   // request longer than 2^levels sets would count past them)
   ctx->lp_max_sets = max_sets < (1u << LB_LP_TREE_LEVELS) ? max_sets : (1u << LB_LP_TREE_LEVELS);
+  ctx->lp_explicit = true;
   return LB_OK;
 }
 

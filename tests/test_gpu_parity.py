@@ -529,3 +529,30 @@ def test_poll_reports_completion_without_blocking(device, mixed_workload):
     assert seen_busy  # a 1,500-set call takes milliseconds: the first poll saw it running
     assert device.poll(pc.ticket)  # retired
     assert list(res.valid) == list(ref.valid) and list(res.errors) == list(ref.errors)
+
+
+@pytest.mark.parametrize("inject", [True, False])
+@pytest.mark.parametrize("n_req_sets", [(1, 1000), (0, 960)])
+def test_lone_mid_call_pipeline_vs_c_oracle(device, inject, n_req_sets):
+    """A lone call of lp_lone_max (896) < n_sets <= lp_max_sets (1,024) leaves the latency path
+    for the pipeline's steps + MSM + merged-check program, merged whatever its request count
+    (run_pipeline's lone_mid): a mixed 960-set workload of 1..128-set requests, and one request
+    of 1,000 single sets.  Verdicts and rejection codes == the C oracle's; the default context
+    (no explicit latency-path bound)."""
+    from oracle import c_oracle as C
+    from lodestar_amd.native import Device
+    one, n = n_req_sets
+    args = _mixed_workload(device, n_keys=256, n_sets=n, seed=23, inject=inject)
+    if one:
+        args = (np.array([0, n], np.uint32),) + tuple(args[1:])
+    seed = hashlib.sha256(b"lone-mid").digest()
+    dev = Device(0)
+    try:
+        res = dev.verify_requests(*args, seed)
+        stages = dict(dev.last_stage_times())
+        valid, err = C.verify_requests(*args, seed, threads=16)
+        assert list(res.errors) == list(err)
+        assert list(res.valid) == list(valid)
+        assert "lp_verify" not in stages and "mtail" in stages and "msm_chunks" in stages
+    finally:
+        dev.close()
